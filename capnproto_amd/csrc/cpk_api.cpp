@@ -1,0 +1,472 @@
+// cpk_api.cpp -- the C ABI (include/cpk.h) over the HIP kernels.  Host side only: argument
+// checks, scratch management, launch sequencing.  No C++ exception crosses the boundary.
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+#include <string.h>
+
+#include <new>
+
+#include "../../include/cpk.h"
+#include "cpk_kernels.h"
+
+struct cpk_ctx {
+  int device = 0;
+  void* scratch = nullptr;       // device scratch (descriptors, bitmaps, tile tables)
+  size_t scratch_size = 0;
+  uint32_t* err = nullptr;       // device error word (first batch-level error)
+  // device staging for the *_host entry points
+  void* stage[4] = {nullptr, nullptr, nullptr, nullptr};
+  size_t stage_size[4] = {0, 0, 0, 0};
+};
+
+namespace {
+
+inline size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
+
+cpk_status hip_status(hipError_t e) { return e == hipSuccess ? CPK_OK : CPK_ERR_HIP; }
+
+cpk_status ensure(void** p, size_t* size, size_t need) {
+  if (need <= *size) return CPK_OK;
+  if (*p) {
+    if (hipFree(*p) != hipSuccess) return CPK_ERR_HIP;
+    *p = nullptr;
+    *size = 0;
+  }
+  size_t sz = need + need / 8 + 4096;
+  if (hipMalloc(p, sz) != hipSuccess) return CPK_ERR_HIP;
+  *size = sz;
+  return CPK_OK;
+}
+
+// Carves aligned sub-buffers out of the context scratch.
+struct Carve {
+  char* base;
+  size_t off = 0;
+  explicit Carve(void* b) : base((char*)b) {}
+  template <class T>
+  T* take(size_t count) {
+    T* p = (T*)(base + off);
+    off = align16(off + count * sizeof(T));
+    return p;
+  }
+};
+
+struct PackScratch {
+  uint32_t* counter;
+  uint64_t* desc;
+  uint32_t* state;
+  uint64_t* bits;
+  size_t zero_bytes;
+  uint64_t* tile_first;
+  size_t total;
+};
+
+size_t pack_scratch_bytes(uint64_t N, uint64_t ntiles) {
+  const uint64_t nbitw = (N + 63) / 64;
+  return 16 + align16(8 * ntiles) + align16(4 * ntiles) + align16(8 * nbitw) +
+         align16(8 * ntiles) + 64;
+}
+
+PackScratch carve_pack(void* base, uint64_t N, uint64_t ntiles) {
+  Carve c(base);
+  PackScratch s;
+  s.counter = c.take<uint32_t>(4);
+  s.desc = c.take<uint64_t>(ntiles);
+  s.state = c.take<uint32_t>(ntiles);
+  s.bits = c.take<uint64_t>((N + 63) / 64);
+  s.zero_bytes = c.off;
+  s.tile_first = c.take<uint64_t>(ntiles);
+  s.total = c.off;
+  return s;
+}
+
+cpk_status pack_common(cpk_ctx* ctx, const uint64_t* d_words, uint64_t N, const uint64_t* d_off,
+                       uint64_t n, bool messages, uint8_t* d_out, uint64_t cap,
+                       uint64_t* d_out_off, int32_t* d_status, hipStream_t stream) {
+  if (!ctx || (!d_off && n) || (!d_words && N) || (!d_out && cap)) return CPK_ERR_INVALID_ARGUMENT;
+  if (hipSetDevice(ctx->device) != hipSuccess) return CPK_ERR_HIP;
+  const uint64_t T = cpk::kPackTileWords;
+  const uint64_t ntiles = (N + T - 1) / T;
+  cpk_status st = ensure(&ctx->scratch, &ctx->scratch_size, pack_scratch_bytes(N, ntiles));
+  if (st != CPK_OK) return st;
+  PackScratch s = carve_pack(ctx->scratch, N, ntiles);
+  if (hipMemsetAsync(ctx->scratch, 0, s.zero_bytes, stream) != hipSuccess) return CPK_ERR_HIP;
+  if (N == 0) {
+    if (d_out_off && hipMemsetAsync(d_out_off, 0, (n + 1) * 8, stream) != hipSuccess)
+      return CPK_ERR_HIP;
+    if (messages && n)
+      return hip_status(cpk::launch_message_bits(d_words, d_off, n, s.bits, d_status, stream));
+    return CPK_OK;
+  }
+  if (messages && n == 0) return CPK_ERR_INVALID_ARGUMENT;  // words outside any message
+  hipError_t e = messages ? cpk::launch_message_bits(d_words, d_off, n, s.bits, d_status, stream)
+                          : cpk::launch_chunk_bits(d_off, n, N, s.bits, stream);
+  if (e != hipSuccess) return CPK_ERR_HIP;
+  if (d_out_off && n) {
+    e = cpk::launch_tile_first(d_off, n, ntiles, T, s.tile_first, stream);
+    if (e != hipSuccess) return CPK_ERR_HIP;
+  }
+  cpk::PackTileArgs a;
+  a.words = d_words;
+  a.nwords = N;
+  a.chunk_bits = s.bits;
+  a.ntiles = ntiles;
+  a.out = d_out;
+  a.out_capacity = cap;
+  a.pos = (d_out_off && n) ? d_off : nullptr;
+  a.npos = n;
+  a.tile_first = s.tile_first;
+  a.pos_out = d_out_off;
+  a.total_out = nullptr;
+  a.tile_counter = s.counter;
+  a.desc = s.desc;
+  a.state = s.state;
+  a.err = ctx->err;
+  return hip_status(cpk::launch_pack_tiles(a, stream));
+}
+
+struct UnpackScratch {
+  uint32_t* counter;
+  uint64_t* desc;
+  uint32_t* state;
+  uint32_t* fail_flag;
+  uint32_t* fail_count;
+  uint32_t* scan_counter;
+  uint64_t* scan_desc;
+  size_t zero_bytes;
+  uint64_t* tile_first;
+  uint64_t* flat;
+  int32_t* hdr_status;
+  uint32_t* fail_list;
+  size_t total;
+};
+
+UnpackScratch carve_unpack(void* base, uint64_t ntiles, uint64_t n) {
+  Carve c(base);
+  UnpackScratch s;
+  s.counter = c.take<uint32_t>(4);
+  s.desc = c.take<uint64_t>(ntiles);
+  s.state = c.take<uint32_t>(ntiles);
+  s.fail_flag = c.take<uint32_t>(n);
+  s.fail_count = c.take<uint32_t>(4);
+  s.scan_counter = c.take<uint32_t>(4);
+  s.scan_desc = c.take<uint64_t>(cpk::scan_tiles(n + 1));
+  s.zero_bytes = c.off;
+  s.tile_first = c.take<uint64_t>(ntiles);
+  s.flat = c.take<uint64_t>(n + 1);
+  s.hdr_status = c.take<int32_t>(n);
+  s.fail_list = c.take<uint32_t>(n);
+  s.total = c.off;
+  return s;
+}
+
+cpk_status unpack_common(cpk_ctx* ctx, uint32_t mode, const uint8_t* d_packed, uint64_t P,
+                         const uint64_t* d_in_off, uint64_t n, const uint64_t* d_word_off_in,
+                         uint64_t* d_words, uint64_t cap, uint64_t* d_word_off_out,
+                         int32_t* d_status, uint64_t* d_size_out, uint64_t limit,
+                         hipStream_t stream) {
+  if (!ctx || (!d_in_off && n) || (!d_packed && P) || (!d_status && n))
+    return CPK_ERR_INVALID_ARGUMENT;
+  if (hipSetDevice(ctx->device) != hipSuccess) return CPK_ERR_HIP;
+  const uint64_t B = cpk::kUnpackTileBytes;
+  const uint64_t ntiles = (P + B - 1) / B;
+  UnpackScratch probe = carve_unpack(nullptr, ntiles, n);
+  cpk_status st = ensure(&ctx->scratch, &ctx->scratch_size, probe.total + 64);
+  if (st != CPK_OK) return st;
+  UnpackScratch s = carve_unpack(ctx->scratch, ntiles, n);
+  if (hipMemsetAsync(ctx->scratch, 0, s.zero_bytes, stream) != hipSuccess) return CPK_ERR_HIP;
+  const uint64_t* word_off = d_word_off_in;
+  hipError_t e = hipSuccess;
+  if (mode == 0) {
+    if (!d_word_off_out) return CPK_ERR_INVALID_ARGUMENT;
+    if (n == 0) return hip_status(hipMemsetAsync(d_word_off_out, 0, 8, stream));
+    e = cpk::launch_unpack_header(d_packed, d_in_off, n, limit, s.flat, s.hdr_status, d_status,
+                                  stream);
+    if (e != hipSuccess) return CPK_ERR_HIP;
+    e = cpk::launch_exclusive_scan(s.flat, n, d_word_off_out, s.scan_counter, s.scan_desc,
+                                   ctx->err, stream);
+    if (e != hipSuccess) return CPK_ERR_HIP;
+    word_off = d_word_off_out;
+  } else {
+    if (n == 0) return CPK_OK;
+    e = cpk::launch_unpack_init(mode, d_in_off, word_off, n, d_status, d_size_out, stream);
+    if (e != hipSuccess) return CPK_ERR_HIP;
+  }
+  if (ntiles == 0) return CPK_OK;
+  e = cpk::launch_tile_first(d_in_off, n, ntiles, B, s.tile_first, stream);
+  if (e != hipSuccess) return CPK_ERR_HIP;
+  cpk::UnpackArgs a;
+  a.packed = d_packed;
+  a.nbytes = P;
+  a.in_off = d_in_off;
+  a.nmsgs = n;
+  a.tile_first = s.tile_first;
+  a.word_off = mode == 2 ? nullptr : word_off;
+  a.hdr_status = mode == 0 ? s.hdr_status : nullptr;
+  a.words = d_words;
+  a.words_capacity = d_words ? cap : 0;
+  a.status = d_status;
+  a.size_out = d_size_out;
+  a.mode = mode;
+  a.ntiles = ntiles;
+  a.tile_counter = s.counter;
+  a.desc = s.desc;
+  a.state = s.state;
+  a.fail_flag = s.fail_flag;
+  a.fail_list = s.fail_list;
+  a.fail_count = s.fail_count;
+  a.err = ctx->err;
+  return hip_status(cpk::launch_unpack_body(a, stream));
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* cpk_status_string(int32_t status) {
+  switch (status) {
+    case CPK_OK: return "";
+    case CPK_ERR_PREMATURE_EOF: return "Premature end of packed input.";
+    case CPK_ERR_RUN_OVERSHOOT: return "Packed input did not end cleanly on a segment boundary.";
+    case CPK_ERR_TOO_MANY_SEGMENTS: return "Message has too many segments.";
+    case CPK_ERR_MESSAGE_TOO_LARGE:
+      return "Message is too large.  To increase the limit on the receiving end, see "
+             "capnp::ReaderOptions.";
+    case CPK_ERR_INVALID_PACKED: return "invalid packed data";
+    case CPK_ERR_BAD_FRAMING: return "Segment table does not match the message size.";
+    case CPK_ERR_TRAILING_BYTES: return "Packed input holds bytes past the end of the message.";
+    case CPK_ERR_CAPACITY: return "backing array was not large enough for the data";
+    case CPK_ERR_INVALID_ARGUMENT: return "invalid argument";
+    case CPK_ERR_HIP: return "HIP runtime error";
+    case CPK_ERR_EMPTY_MESSAGE: return "Tried to serialize uninitialized message.";
+    case CPK_ERR_INTERNAL: return "internal error (device wait timed out)";
+    case CPK_ERR_NO_DEVICE: return "no HIP device";
+    default: return "unknown status";
+  }
+}
+
+int cpk_abi_version(void) { return CPK_ABI_VERSION; }
+
+uint64_t cpk_packed_bound(uint64_t words, uint64_t chunks) {
+  return words * 8 + (words + 1) / 2 + 2 * chunks;
+}
+
+cpk_status cpk_init(int device, cpk_ctx** out) {
+  if (!out) return CPK_ERR_INVALID_ARGUMENT;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return CPK_ERR_NO_DEVICE;
+  if (device < 0 || device >= n) return CPK_ERR_INVALID_ARGUMENT;
+  if (hipSetDevice(device) != hipSuccess) return CPK_ERR_HIP;
+  cpk_ctx* c = new (std::nothrow) cpk_ctx();
+  if (!c) return CPK_ERR_INTERNAL;
+  c->device = device;
+  if (hipMalloc((void**)&c->err, 16) != hipSuccess || hipMemset(c->err, 0, 16) != hipSuccess) {
+    delete c;
+    return CPK_ERR_HIP;
+  }
+  *out = c;
+  return CPK_OK;
+}
+
+cpk_status cpk_destroy(cpk_ctx* ctx) {
+  if (!ctx) return CPK_OK;
+  (void)hipSetDevice(ctx->device);
+  (void)hipDeviceSynchronize();
+  if (ctx->scratch) (void)hipFree(ctx->scratch);
+  if (ctx->err) (void)hipFree(ctx->err);
+  for (int i = 0; i < 4; i++)
+    if (ctx->stage[i]) (void)hipFree(ctx->stage[i]);
+  delete ctx;
+  return CPK_OK;
+}
+
+cpk_status cpk_reserve(cpk_ctx* ctx, uint64_t max_words, uint64_t max_packed_bytes,
+                       uint64_t max_items) {
+  if (!ctx) return CPK_ERR_INVALID_ARGUMENT;
+  if (hipSetDevice(ctx->device) != hipSuccess) return CPK_ERR_HIP;
+  const uint64_t pt = (max_words + cpk::kPackTileWords - 1) / cpk::kPackTileWords;
+  size_t need = pack_scratch_bytes(max_words, pt);
+  const uint64_t ut = (max_packed_bytes + cpk::kUnpackTileBytes - 1) / cpk::kUnpackTileBytes;
+  const size_t un = 16 + align16(16 * ut) + align16(8 * ut) + 16 * align16(8 * (max_items + 1)) +
+                    align16(8 * cpk::scan_tiles(max_items + 1)) + 64;
+  if (un > need) need = un;
+  return ensure(&ctx->scratch, &ctx->scratch_size, need);
+}
+
+cpk_status cpk_sync(cpk_ctx* ctx, void* stream) {
+  if (!ctx) return CPK_ERR_INVALID_ARGUMENT;
+  if (hipSetDevice(ctx->device) != hipSuccess) return CPK_ERR_HIP;
+  if (hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return CPK_ERR_HIP;
+  uint32_t e = 0;
+  if (hipMemcpy(&e, ctx->err, 4, hipMemcpyDeviceToHost) != hipSuccess) return CPK_ERR_HIP;
+  if (e) {
+    if (hipMemset(ctx->err, 0, 4) != hipSuccess) return CPK_ERR_HIP;
+  }
+  return (cpk_status)e;
+}
+
+cpk_status cpk_pack_chunks(cpk_ctx* ctx, const uint64_t* d_words, uint64_t total_words,
+                           const uint64_t* d_chunk_word_off, uint64_t nchunks, uint8_t* d_out,
+                           uint64_t out_capacity, uint64_t* d_chunk_out_off, void* stream) {
+  return pack_common(ctx, d_words, total_words, d_chunk_word_off, nchunks, false, d_out,
+                     out_capacity, d_chunk_out_off, nullptr, (hipStream_t)stream);
+}
+
+cpk_status cpk_pack_messages(cpk_ctx* ctx, const uint64_t* d_words, uint64_t total_words,
+                             const uint64_t* d_msg_word_off, uint64_t nmsgs, uint8_t* d_out,
+                             uint64_t out_capacity, uint64_t* d_msg_out_off, int32_t* d_status,
+                             void* stream) {
+  return pack_common(ctx, d_words, total_words, d_msg_word_off, nmsgs, true, d_out, out_capacity,
+                     d_msg_out_off, d_status, (hipStream_t)stream);
+}
+
+cpk_status cpk_pack_messages_host(cpk_ctx* ctx, const uint64_t* h_words, uint64_t total_words,
+                                  const uint64_t* h_msg_word_off, uint64_t nmsgs, uint8_t* h_out,
+                                  uint64_t out_capacity, uint64_t* h_msg_out_off,
+                                  int32_t* h_status) {
+  if (!ctx || !h_msg_word_off) return CPK_ERR_INVALID_ARGUMENT;
+  if (hipSetDevice(ctx->device) != hipSuccess) return CPK_ERR_HIP;
+  const size_t wbytes = total_words * 8, obytes = (nmsgs + 1) * 8;
+  cpk_status st;
+  if ((st = ensure(&ctx->stage[0], &ctx->stage_size[0], wbytes + 16)) != CPK_OK) return st;
+  if ((st = ensure(&ctx->stage[1], &ctx->stage_size[1], out_capacity + 16)) != CPK_OK) return st;
+  if ((st = ensure(&ctx->stage[2], &ctx->stage_size[2], 2 * obytes + 4 * nmsgs + 64)) != CPK_OK)
+    return st;
+  uint64_t* d_words = (uint64_t*)ctx->stage[0];
+  uint8_t* d_out = (uint8_t*)ctx->stage[1];
+  uint64_t* d_off = (uint64_t*)ctx->stage[2];
+  uint64_t* d_out_off = d_off + (nmsgs + 1);
+  int32_t* d_status = (int32_t*)(d_out_off + (nmsgs + 1));
+  hipStream_t s = nullptr;
+  if (hipMemcpyAsync(d_words, h_words, wbytes, hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipMemcpyAsync(d_off, h_msg_word_off, obytes, hipMemcpyHostToDevice, s) != hipSuccess)
+    return CPK_ERR_HIP;
+  st = cpk_pack_messages(ctx, d_words, total_words, d_off, nmsgs, d_out, out_capacity, d_out_off,
+                         d_status, s);
+  if (st != CPK_OK) return st;
+  st = cpk_sync(ctx, s);
+  uint64_t total = 0;
+  if (hipMemcpy(&total, d_out_off + nmsgs, 8, hipMemcpyDeviceToHost) != hipSuccess)
+    return CPK_ERR_HIP;
+  if (h_msg_out_off && hipMemcpy(h_msg_out_off, d_out_off, obytes, hipMemcpyDeviceToHost))
+    return CPK_ERR_HIP;
+  if (h_status && nmsgs && hipMemcpy(h_status, d_status, 4 * nmsgs, hipMemcpyDeviceToHost))
+    return CPK_ERR_HIP;
+  if (st != CPK_OK) return st;
+  if (total > out_capacity) return CPK_ERR_CAPACITY;
+  if (total && hipMemcpy(h_out, d_out, total, hipMemcpyDeviceToHost) != hipSuccess)
+    return CPK_ERR_HIP;
+  return CPK_OK;
+}
+
+cpk_status cpk_unpack_messages(cpk_ctx* ctx, const uint8_t* d_packed, uint64_t total_bytes,
+                               const uint64_t* d_msg_in_off, uint64_t nmsgs, uint64_t* d_words,
+                               uint64_t words_capacity, uint64_t* d_msg_word_off,
+                               int32_t* d_status, const cpk_limits* limits, void* stream) {
+  const uint64_t limit = limits ? limits->traversal_limit_words : 8ull * 1024 * 1024;
+  return unpack_common(ctx, 0, d_packed, total_bytes, d_msg_in_off, nmsgs, nullptr, d_words,
+                       words_capacity, d_msg_word_off, d_status, nullptr, limit,
+                       (hipStream_t)stream);
+}
+
+cpk_status cpk_unpacked_size(cpk_ctx* ctx, const uint8_t* d_packed, uint64_t total_bytes,
+                             const uint64_t* d_in_off, uint64_t n, uint64_t* d_words_out,
+                             int32_t* d_status, void* stream) {
+  if (!d_words_out && n) return CPK_ERR_INVALID_ARGUMENT;
+  return unpack_common(ctx, 2, d_packed, total_bytes, d_in_off, n, nullptr, nullptr, 0, nullptr,
+                       d_status, d_words_out, 0, (hipStream_t)stream);
+}
+
+cpk_status cpk_unpack_chunks(cpk_ctx* ctx, const uint8_t* d_packed, uint64_t total_bytes,
+                             const uint64_t* d_in_off, const uint64_t* d_word_off, uint64_t n,
+                             uint64_t* d_words, uint64_t words_capacity, int32_t* d_status,
+                             void* stream) {
+  if (!d_word_off && n) return CPK_ERR_INVALID_ARGUMENT;
+  return unpack_common(ctx, 1, d_packed, total_bytes, d_in_off, n, d_word_off, d_words,
+                       words_capacity, nullptr, d_status, nullptr, 0, (hipStream_t)stream);
+}
+
+cpk_status cpk_unpack_messages_host(cpk_ctx* ctx, const uint8_t* h_packed, uint64_t total_bytes,
+                                    const uint64_t* h_msg_in_off, uint64_t nmsgs,
+                                    uint64_t* h_words, uint64_t words_capacity,
+                                    uint64_t* h_msg_word_off, int32_t* h_status,
+                                    const cpk_limits* limits) {
+  if (!ctx || !h_msg_in_off || (!h_words && words_capacity)) return CPK_ERR_INVALID_ARGUMENT;
+  if (hipSetDevice(ctx->device) != hipSuccess) return CPK_ERR_HIP;
+  const size_t obytes = (nmsgs + 1) * 8;
+  cpk_status st;
+  if ((st = ensure(&ctx->stage[0], &ctx->stage_size[0], words_capacity * 8 + 16)) != CPK_OK)
+    return st;
+  if ((st = ensure(&ctx->stage[1], &ctx->stage_size[1], total_bytes + 16)) != CPK_OK) return st;
+  if ((st = ensure(&ctx->stage[2], &ctx->stage_size[2], 2 * obytes + 4 * nmsgs + 64)) != CPK_OK)
+    return st;
+  uint64_t* d_words = (uint64_t*)ctx->stage[0];
+  uint8_t* d_packed = (uint8_t*)ctx->stage[1];
+  uint64_t* d_in_off = (uint64_t*)ctx->stage[2];
+  uint64_t* d_word_off = d_in_off + (nmsgs + 1);
+  int32_t* d_status = (int32_t*)(d_word_off + (nmsgs + 1));
+  hipStream_t s = nullptr;
+  if ((total_bytes &&
+       hipMemcpyAsync(d_packed, h_packed, total_bytes, hipMemcpyHostToDevice, s) != hipSuccess) ||
+      hipMemcpyAsync(d_in_off, h_msg_in_off, obytes, hipMemcpyHostToDevice, s) != hipSuccess)
+    return CPK_ERR_HIP;
+  st = cpk_unpack_messages(ctx, d_packed, total_bytes, d_in_off, nmsgs, d_words, words_capacity,
+                           d_word_off, d_status, limits, s);
+  if (st != CPK_OK) return st;
+  st = cpk_sync(ctx, s);
+  uint64_t total = 0;
+  if (hipMemcpy(&total, d_word_off + nmsgs, 8, hipMemcpyDeviceToHost) != hipSuccess)
+    return CPK_ERR_HIP;
+  if (h_msg_word_off && hipMemcpy(h_msg_word_off, d_word_off, obytes, hipMemcpyDeviceToHost))
+    return CPK_ERR_HIP;
+  if (h_status && nmsgs && hipMemcpy(h_status, d_status, 4 * nmsgs, hipMemcpyDeviceToHost))
+    return CPK_ERR_HIP;
+  if (st != CPK_OK) return st;
+  const uint64_t n = total < words_capacity ? total : words_capacity;
+  if (n && hipMemcpy(h_words, d_words, n * 8, hipMemcpyDeviceToHost) != hipSuccess)
+    return CPK_ERR_HIP;
+  return CPK_OK;
+}
+
+cpk_status cpk_gen_messages(cpk_ctx* ctx, int profile, uint64_t seed, uint64_t first_msg,
+                            uint64_t nmsgs, uint32_t nseg, const uint64_t* d_msg_word_off,
+                            uint64_t* d_words, void* stream) {
+  if (!ctx || profile < 0 || profile > 3 || nseg == 0) return CPK_ERR_INVALID_ARGUMENT;
+  if (hipSetDevice(ctx->device) != hipSuccess) return CPK_ERR_HIP;
+  return hip_status(cpk::launch_gen(profile, seed, first_msg, nmsgs, nseg, d_msg_word_off,
+                                    d_words, (hipStream_t)stream));
+}
+
+cpk_status cpk_gen_offsets(cpk_ctx* ctx, uint64_t seed, uint64_t first_msg, uint64_t nmsgs,
+                           uint32_t nseg, uint64_t seg_words, uint64_t* d_msg_word_off,
+                           uint64_t* total_words_out, void* stream) {
+  if (!ctx || nseg == 0 || (seg_words == 0 && nseg != 1)) return CPK_ERR_INVALID_ARGUMENT;
+  if (hipSetDevice(ctx->device) != hipSuccess) return CPK_ERR_HIP;
+  hipStream_t s = (hipStream_t)stream;
+  const uint64_t nt = cpk::scan_tiles(nmsgs);
+  const size_t need = 16 + align16(8 * nt) + align16(8 * (nmsgs + 1)) + 64;
+  cpk_status st = ensure(&ctx->scratch, &ctx->scratch_size, need);
+  if (st != CPK_OK) return st;
+  Carve c(ctx->scratch);
+  uint32_t* counter = c.take<uint32_t>(4);
+  uint64_t* desc = c.take<uint64_t>(nt);
+  const size_t zero = c.off;
+  uint64_t* sizes = c.take<uint64_t>(nmsgs + 1);
+  if (hipMemsetAsync(ctx->scratch, 0, zero, s) != hipSuccess) return CPK_ERR_HIP;
+  if (cpk::launch_gen_sizes(seed, first_msg, nmsgs, nseg, seg_words, sizes, s) != hipSuccess)
+    return CPK_ERR_HIP;
+  if (cpk::launch_exclusive_scan(sizes, nmsgs, d_msg_word_off, counter, desc, ctx->err, s) !=
+      hipSuccess)
+    return CPK_ERR_HIP;
+  if (total_words_out) {
+    if (hipMemcpyAsync(total_words_out, d_msg_word_off + nmsgs, 8, hipMemcpyDeviceToHost, s) !=
+            hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      return CPK_ERR_HIP;
+  }
+  return CPK_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,82 @@
+// cpk_kernels.h -- internal launch interface between the C-ABI layer (cpk_api.cpp) and the HIP
+// kernels.  Not installed; include/cpk.h is the public boundary.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace cpk {
+
+constexpr int kPackSteps = 16;                  // words per pack tile = 64 * kPackSteps
+constexpr uint64_t kPackTileWords = 64 * kPackSteps;
+constexpr uint64_t kUnpackTileBytes = 4096;     // packed bytes per unpack tile (>= 2050)
+
+struct PackTileArgs {
+  const uint64_t* words;       // batch of words (all chunks back to back)
+  uint64_t nwords;
+  const uint64_t* chunk_bits;  // bit i set <=> word i starts a chunk (word 0 always)
+  uint64_t ntiles;
+  uint8_t* out;
+  uint64_t out_capacity;
+  // optional: output byte offset of each word position pos[0..npos] (sorted)
+  const uint64_t* pos;
+  uint64_t npos;               // index of the last entry (pos has npos + 1 entries)
+  const uint64_t* tile_first;  // per tile: first i with pos[i] >= tile start
+  uint64_t* pos_out;
+  uint64_t* total_out;         // optional: total packed bytes
+  // scratch (zeroed before the launch)
+  uint32_t* tile_counter;
+  uint64_t* desc;              // ntiles look-back descriptors
+  uint32_t* state;             // ntiles exit budgets (0x80000000 | budget)
+  uint32_t* err;
+};
+
+hipError_t launch_pack_tiles(const PackTileArgs& a, hipStream_t stream);
+hipError_t launch_message_bits(const uint64_t* words, const uint64_t* off, uint64_t n,
+                               uint64_t* bits, int32_t* status, hipStream_t stream);
+hipError_t launch_chunk_bits(const uint64_t* off, uint64_t n, uint64_t N, uint64_t* bits,
+                             hipStream_t stream);
+hipError_t launch_tile_first(const uint64_t* pos, uint64_t npos, uint64_t ntiles, uint64_t T,
+                             uint64_t* tile_first, hipStream_t stream);
+
+struct UnpackArgs {
+  const uint8_t* packed;        // batch of packed bytes
+  uint64_t nbytes;
+  const uint64_t* in_off;       // nmsgs + 1 byte offsets
+  uint64_t nmsgs;
+  const uint64_t* tile_first;   // per tile: first m with in_off[m] >= tile start
+  const uint64_t* word_off;     // nmsgs + 1 word offsets (NULL in size-only mode)
+  const int32_t* hdr_status;    // header verdicts (NULL: all OK)
+  uint64_t* words;
+  uint64_t words_capacity;
+  int32_t* status;
+  uint64_t* size_out;           // mode 2
+  uint32_t mode;                // 0 messages, 1 exact-size chunks (flat-packed), 2 size only
+  uint64_t ntiles;
+  uint32_t* tile_counter;
+  uint64_t* desc;
+  uint32_t* state;
+  uint32_t* fail_flag;          // per message
+  uint32_t* fail_list;
+  uint32_t* fail_count;
+  uint32_t* err;
+};
+
+hipError_t launch_unpack_header(const uint8_t* packed, const uint64_t* in_off, uint64_t n,
+                                uint64_t limit, uint64_t* flat, int32_t* hdr_status,
+                                int32_t* status, hipStream_t stream);
+hipError_t launch_unpack_body(const UnpackArgs& a, hipStream_t stream);
+hipError_t launch_unpack_init(uint32_t mode, const uint64_t* in_off, const uint64_t* word_off,
+                              uint64_t n, int32_t* status, uint64_t* size_out, hipStream_t stream);
+
+hipError_t launch_gen(int profile, uint64_t seed, uint64_t first_msg, uint64_t nmsgs,
+                      uint32_t nseg, const uint64_t* off, uint64_t* words, hipStream_t stream);
+hipError_t launch_gen_sizes(uint64_t seed, uint64_t first_msg, uint64_t nmsgs, uint32_t nseg,
+                            uint64_t seg_words, uint64_t* sizes, hipStream_t stream);
+
+uint64_t scan_tiles(uint64_t n);
+// out[0..n] = exclusive prefix sums of in[0..n), out[n] = total.  counter/desc zeroed before.
+hipError_t launch_exclusive_scan(const uint64_t* in, uint64_t n, uint64_t* out, uint32_t* counter,
+                                 uint64_t* desc, uint32_t* err, hipStream_t stream);
+
+}  // namespace cpk

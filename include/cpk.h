@@ -1,21 +1,24 @@
 /* cpk.h -- C ABI of the MI355X-native Cap'n Proto *packed* wire codec (libcpk_hip.so).
  *
- * This is the drop-in boundary under the reference's packed stream/message API
- * (capnproto c++/src/capnp/serialize-packed.h:32-107).  Every entry point takes plain
- * pointers and sizes; device pointers are HBM allocations (hipMalloc or torch tensors),
- * `stream` is a hipStream_t passed as void* (NULL = the default stream).  No C++ exception
- * crosses this boundary: failures come back as cpk_status, per-message failures as int32
- * codes in a caller-owned status array (same enum).
+ * This is the drop-in boundary under the reference's packed stream / message API
+ * (capnproto c++/src/capnp/serialize-packed.h:32-124).  Each entry point below names the
+ * reference function it replaces.  All arguments are plain pointers and sizes: `d_*` pointers
+ * are device (HBM) allocations, `h_*` pointers host memory, `stream` is a hipStream_t passed as
+ * void* (NULL = the default stream).  No C++ exception crosses this boundary.
  *
- * Ownership (mirrors serialize-packed.h:46,60 -- streams borrow, never own): the caller owns
- * every buffer; a cpk_ctx owns only its scratch (look-back flags, tile maps, scans).
- * Threading: one cpk_ctx per (device, host thread); any number of contexts may run in parallel.
+ * Ownership mirrors serialize-packed.h:46,60 (streams borrow, never own): the caller owns every
+ * buffer; a cpk_ctx owns only its device scratch.  Threading: a cpk_ctx is single-threaded; any
+ * number of contexts may be used in parallel (one per device / host thread).
  *
- * Wire format recap (doc/encoding.md:296-349): the input is a sequence of 8-byte words.  Each
- * word becomes a tag byte (bit i set <=> byte i non-zero) followed by its non-zero bytes.  Tag
- * 0x00 is followed by a count N<=255 of further all-zero words; tag 0xff by a count N<=255 of
- * further words with at most one zero byte, copied raw.  Runs never cross a chunk: a "chunk" is
- * one OutputStream::write() piece -- the segment table, then each segment
+ * Asynchrony: the device entry points only enqueue work on `stream` and return CPK_OK when the
+ * launch succeeded.  Per-message results land in caller-owned d_status arrays; batch-level
+ * failures found on the device (output capacity exceeded, internal protocol timeout) are kept in
+ * the context's error word and returned by cpk_sync().
+ *
+ * Wire format (doc/encoding.md:296-349): each 8-byte word becomes a tag byte (bit i <=> byte i
+ * non-zero) followed by its non-zero bytes.  Tag 0x00 is followed by a count N <= 255 of further
+ * all-zero words; tag 0xff by a count N <= 255 of further words copied raw.  Runs never cross a
+ * chunk: a chunk is one OutputStream::write() piece -- the segment table, then each segment
  * (serialize.c++:332-357 -> kj/io.c++:109-113).
  */
 #ifndef CPK_H_
@@ -32,11 +35,11 @@ extern "C" {
 
 typedef enum cpk_status {
   CPK_OK = 0,
-  /* kj/io.c++:53 / :118 "Premature EOF" -- packed input ended before the message did.
-   * (PackedInputStream's own "Premature end of packed input." at serialize-packed.c++:57 is
-   * unreachable behind BufferedInputStream::getReadBuffer's check; pinned by oracle/_ref.) */
+  /* Input ended before the message did: kj/io.c++:53 "Premature EOF" (InputStream::read) and
+   * serialize-packed.c++:57 "Premature end of packed input." */
   CPK_ERR_PREMATURE_EOF = 1,
-  /* serialize-packed.c++:128-131, :140-143 */
+  /* serialize-packed.c++:128-131, :140-143 "Packed input did not end cleanly on a segment
+   * boundary." -- a zero or raw run overshoots the words being read. */
   CPK_ERR_RUN_OVERSHOOT = 2,
   /* serialize.c++:217 "Message has too many segments." (segment count > 512) */
   CPK_ERR_TOO_MANY_SEGMENTS = 3,
@@ -44,117 +47,146 @@ typedef enum cpk_status {
   CPK_ERR_MESSAGE_TOO_LARGE = 4,
   /* serialize-packed.c++:491-502 "invalid packed data" (computeUnpackedSizeInWords) */
   CPK_ERR_INVALID_PACKED = 5,
-  /* pack input: a flat message's segment table disagrees with its word count */
+  /* pack input: a flat message's segment table disagrees with its word count (the message is
+   * then packed as a single chunk so offsets stay defined) */
   CPK_ERR_BAD_FRAMING = 6,
-  /* unpack batch: the message parse finished before its [in_off[i], in_off[i+1]) range did */
+  /* unpack batch: the message ended before its [in_off[i], in_off[i+1]) byte range did */
   CPK_ERR_TRAILING_BYTES = 7,
   /* kj/io.c++:281-282 "backing array was not large enough" -- output capacity too small */
   CPK_ERR_CAPACITY = 8,
   CPK_ERR_INVALID_ARGUMENT = 9,
   CPK_ERR_HIP = 10,
-  /* serialize.c++:333 "Tried to serialize uninitialized message." (zero segments) */
+  /* serialize.c++:333 "Tried to serialize uninitialized message." (zero segments / words) */
   CPK_ERR_EMPTY_MESSAGE = 11,
-  /* internal: the device look-back gave up waiting (should never happen; bounded spin) */
+  /* internal: a device-side wait gave up (bounded spin); never expected */
   CPK_ERR_INTERNAL = 12,
   CPK_ERR_NO_DEVICE = 13
 } cpk_status;
 
 /* Reference message text for a status ("" for CPK_OK). */
 const char* cpk_status_string(int32_t status);
+int cpk_abi_version(void);
 
-/* ReaderOptions (capnp/message.h:51-84).  traversal_limit_words default 8 Mi words
- * (message.h:54); the 512-segment cap is fixed by serialize.c++:217. */
+/* ReaderOptions (capnp/message.h:51-84): traversal_limit_words defaults to 8 Mi words
+ * (message.h:54).  The 512-segment cap is fixed by serialize.c++:217. */
 typedef struct cpk_limits {
   uint64_t traversal_limit_words;
 } cpk_limits;
 
 typedef struct cpk_ctx cpk_ctx;
 
-/* One context per device.  Allocates no large buffers up front; scratch grows on demand. */
+/* One context per (device, host thread).  Scratch grows on demand; cpk_reserve pre-sizes it so
+ * that later calls allocate nothing (required before capturing calls into a hipGraph). */
 cpk_status cpk_init(int device, cpk_ctx** out);
 cpk_status cpk_destroy(cpk_ctx* ctx);
-int        cpk_abi_version(void);
-/* Device synchronisation helper (hipStreamSynchronize); the batch calls are asynchronous. */
-cpk_status cpk_stream_sync(cpk_ctx* ctx, void* stream);
+cpk_status cpk_reserve(cpk_ctx* ctx, uint64_t max_words, uint64_t max_packed_bytes,
+                       uint64_t max_items);
+/* hipStreamSynchronize(stream), then return (and clear) the first device-side batch error since
+ * the previous cpk_sync: CPK_OK, CPK_ERR_CAPACITY or CPK_ERR_INTERNAL. */
+cpk_status cpk_sync(cpk_ctx* ctx, void* stream);
 
-/* Worst-case packed bytes for `words` words split into `chunks` chunks:
- *   8*words + ceil(words/2) + 2*chunks  (an F word costs 10 B but must be followed by a
- *   cheaper word unless the chunk ends).  Use it to size d_out. */
+/* Worst-case packed bytes for `words` words in `chunks` chunks: 8*words + ceil(words/2) +
+ * 2*chunks (a lone F word costs 10 B and cannot be followed by another raw-eligible word
+ * without joining its run; doc/encoding.md:328-329).  Use it to size packed buffers. */
 uint64_t cpk_packed_bound(uint64_t words, uint64_t chunks);
 
 /* ------------------------------------------------------------------------------------------
- * a1 + a6: PackedOutputStream::write per piece (serialize-packed.c++:307-431, kj/io.c++:109-113).
- * Packs `nchunks` independent word chunks d_words[chunk_word_off[c] .. chunk_word_off[c+1]) and
- * concatenates the packed bytes in chunk order into d_out.  d_chunk_out_off[c] receives each
- * chunk's packed start, d_chunk_out_off[nchunks] the total.  chunk_word_off must be
- * non-decreasing (empty chunks allowed).  Asynchronous on `stream`. */
-cpk_status cpk_pack_chunks(cpk_ctx* ctx, const uint64_t* d_words, const uint64_t* d_chunk_word_off,
-                           uint64_t nchunks, uint8_t* d_out, uint64_t out_capacity,
-                           uint64_t* d_chunk_out_off, void* stream);
+ * PACK (device-resident)
+ *
+ * a1 + a6: PackedOutputStream::write once per piece (serialize-packed.c++:307-431 via
+ * kj/io.c++:109-113).  Chunk c is d_words[chunk_word_off[c] .. chunk_word_off[c+1]);
+ * chunk_word_off has nchunks+1 non-decreasing entries, [0] == 0 and [nchunks] == total_words
+ * (empty chunks allowed).  The packed chunks are concatenated into d_out;
+ * d_chunk_out_off[c] (nchunks+1 entries) receives each chunk's packed start and the total. */
+cpk_status cpk_pack_chunks(cpk_ctx* ctx, const uint64_t* d_words, uint64_t total_words,
+                           const uint64_t* d_chunk_word_off, uint64_t nchunks,
+                           uint8_t* d_out, uint64_t out_capacity, uint64_t* d_chunk_out_off,
+                           void* stream);
 
-/* a5 + a7: writePackedMessage for a batch (serialize-packed.c++:460-464 over
- * serialize.c++:332-357).  Message i is the flat serialized message
- * d_words[msg_word_off[i] .. msg_word_off[i+1]) -- segment table then segments, i.e. the
- * layout messageToFlatArray (serialize.c++:161-190) produces.  The table is read in place to
- * find the chunk boundaries.  d_msg_out_off[i] receives message i's packed start (nmsgs+1
- * entries); d_status[i] its status (CPK_OK / BAD_FRAMING / TOO_MANY_SEGMENTS).  A message
- * with bad framing is packed as one chunk so offsets stay defined. */
-cpk_status cpk_pack_messages(cpk_ctx* ctx, const uint64_t* d_words, const uint64_t* d_msg_word_off,
-                             uint64_t nmsgs, uint8_t* d_out, uint64_t out_capacity,
-                             uint64_t* d_msg_out_off, int32_t* d_status, void* stream);
+/* a5 + a7: writePackedMessage(BufferedOutputStream&, segments) for a batch
+ * (serialize-packed.c++:460-464 over writeMessage serialize.c++:332-357).  Message i is the flat
+ * serialized message d_words[msg_word_off[i] .. msg_word_off[i+1]) -- segment table then
+ * segments, the layout messageToFlatArray produces (serialize.c++:161-190); msg_word_off has
+ * nmsgs+1 entries, [0] == 0, [nmsgs] == total_words.  The table is read in place to find the
+ * chunk boundaries.  d_msg_out_off (nmsgs+1 entries) receives each message's packed start and
+ * the total; d_status (may be NULL) CPK_OK, CPK_ERR_BAD_FRAMING or CPK_ERR_EMPTY_MESSAGE. */
+cpk_status cpk_pack_messages(cpk_ctx* ctx, const uint64_t* d_words, uint64_t total_words,
+                             const uint64_t* d_msg_word_off, uint64_t nmsgs,
+                             uint8_t* d_out, uint64_t out_capacity, uint64_t* d_msg_out_off,
+                             int32_t* d_status, void* stream);
 
-/* a2 + a8: PackedMessageReader over an array for a batch (serialize-packed.c++:437-440 ->
- * serialize.c++:202-302, PackedInputStream::tryRead serialize-packed.c++:34-183).  Message i's
- * packed bytes are d_packed[msg_in_off[i] .. msg_in_off[i+1]).  The flat unpacked message
- * (table + segments) is written to d_words at d_msg_word_off[i] (computed here: nmsgs+1
- * entries, exclusive scan of each message's table-declared size, or of 0 for a message whose
- * header is rejected).  words_capacity is checked against the total.  Statuses per message
- * follow the reference's first failure (PREMATURE_EOF, RUN_OVERSHOOT, TOO_MANY_SEGMENTS,
- * MESSAGE_TOO_LARGE) plus TRAILING_BYTES when the range holds more than one message.
- * limits may be NULL (reference defaults). */
-cpk_status cpk_unpack_messages(cpk_ctx* ctx, const uint8_t* d_packed, const uint64_t* d_msg_in_off,
-                               uint64_t nmsgs, uint64_t* d_words, uint64_t words_capacity,
+/* ------------------------------------------------------------------------------------------
+ * UNPACK (device-resident)
+ *
+ * a2 + a8: PackedMessageReader over an array, for a batch (serialize-packed.c++:437-440 ->
+ * InputStreamMessageReader serialize.c++:202-302 -> PackedInputStream::tryRead
+ * serialize-packed.c++:34-183).  Message i's packed bytes are
+ * d_packed[msg_in_off[i] .. msg_in_off[i+1]) (nmsgs+1 entries, [nmsgs] == total_bytes).  The
+ * flat unpacked message (table + segments) is written to d_words at d_msg_word_off[i], which
+ * this call computes (nmsgs+1 entries: exclusive scan of each message's table-declared size, 0
+ * for a message whose header is rejected).  d_status[i] is the reference's first failure for
+ * message i (PREMATURE_EOF, RUN_OVERSHOOT, TOO_MANY_SEGMENTS, MESSAGE_TOO_LARGE), or
+ * TRAILING_BYTES when the range holds more than one message, or CAPACITY when the message does
+ * not fit words_capacity.  limits may be NULL (reference defaults). */
+cpk_status cpk_unpack_messages(cpk_ctx* ctx, const uint8_t* d_packed, uint64_t total_bytes,
+                               const uint64_t* d_msg_in_off, uint64_t nmsgs,
+                               uint64_t* d_words, uint64_t words_capacity,
                                uint64_t* d_msg_word_off, int32_t* d_status,
                                const cpk_limits* limits, void* stream);
 
 /* a4: computeUnpackedSizeInWords (serialize-packed.c++:482-508) for n independent buffers
- * d_packed[in_off[i] .. in_off[i+1]).  d_words_out[i] = total words, d_status[i] = CPK_OK or
- * CPK_ERR_INVALID_PACKED. */
-cpk_status cpk_unpacked_size(cpk_ctx* ctx, const uint8_t* d_packed, const uint64_t* d_in_off,
-                             uint64_t n, uint64_t* d_words_out, int32_t* d_status, void* stream);
+ * d_packed[in_off[i] .. in_off[i+1]).  d_words_out[i] = total words; d_status[i] = CPK_OK or
+ * CPK_ERR_INVALID_PACKED (then d_words_out[i] = 0). */
+cpk_status cpk_unpacked_size(cpk_ctx* ctx, const uint8_t* d_packed, uint64_t total_bytes,
+                             const uint64_t* d_in_off, uint64_t n, uint64_t* d_words_out,
+                             int32_t* d_status, void* stream);
 
-/* flat-packed (capnp.c++:1063-1076, :1126-1134): unpack n single-chunk buffers with no
- * segment table.  Word offsets come from cpk_unpacked_size; each buffer must decode to
- * exactly that many words (computeUnpackedSizeInWords + PackedInputStream::read). */
-cpk_status cpk_unpack_chunks(cpk_ctx* ctx, const uint8_t* d_packed, const uint64_t* d_in_off,
-                             uint64_t n, uint64_t* d_words, uint64_t words_capacity,
-                             uint64_t* d_word_off, int32_t* d_status, void* stream);
-
-/* a3: PackedInputStream::skip semantics (serialize-packed.c++:185-299): given one packed
- * buffer, advance over `skip_words` unpacked words and report the packed byte position
- * reached.  Synchronous; returns PREMATURE_EOF / RUN_OVERSHOOT like the reference. */
-cpk_status cpk_skip_words(cpk_ctx* ctx, const uint8_t* d_packed, uint64_t packed_len,
-                          uint64_t skip_words, uint64_t* packed_pos_out, void* stream);
+/* a2 (flat-packed, capnp.c++:1063-1076): PackedInputStream::read of exactly
+ * word_off[i+1]-word_off[i] words from each single-chunk buffer d_packed[in_off[i] ..
+ * in_off[i+1]) into d_words[word_off[i] ..).  Runs may not overshoot a buffer's word count
+ * (RUN_OVERSHOOT); a buffer that ends early is PREMATURE_EOF; unread bytes TRAILING_BYTES. */
+cpk_status cpk_unpack_chunks(cpk_ctx* ctx, const uint8_t* d_packed, uint64_t total_bytes,
+                             const uint64_t* d_in_off, const uint64_t* d_word_off, uint64_t n,
+                             uint64_t* d_words, uint64_t words_capacity, int32_t* d_status,
+                             void* stream);
 
 /* ------------------------------------------------------------------------------------------
- * Host-buffer convenience (pinned or pageable host memory in and out).  These include the
- * H2D and D2H copies -- the path the reference actually sits on (a socket or file buffer).
- * Synchronous. */
-cpk_status cpk_pack_messages_host(cpk_ctx* ctx, const uint64_t* h_words, const uint64_t* h_msg_word_off,
-                                  uint64_t nmsgs, uint8_t* h_out, uint64_t out_capacity,
-                                  uint64_t* h_msg_out_off, int32_t* h_status);
-cpk_status cpk_unpack_messages_host(cpk_ctx* ctx, const uint8_t* h_packed, const uint64_t* h_msg_in_off,
-                                    uint64_t nmsgs, uint64_t* h_words, uint64_t words_capacity,
+ * Host-buffer convenience: the path the reference actually sits on (a socket or file buffer).
+ * These stage through the context's device buffers and include the H2D and D2H copies.
+ * Synchronous.  Offsets arrays are host arrays with the same meaning as above. */
+cpk_status cpk_pack_messages_host(cpk_ctx* ctx, const uint64_t* h_words, uint64_t total_words,
+                                  const uint64_t* h_msg_word_off, uint64_t nmsgs,
+                                  uint8_t* h_out, uint64_t out_capacity, uint64_t* h_msg_out_off,
+                                  int32_t* h_status);
+cpk_status cpk_unpack_messages_host(cpk_ctx* ctx, const uint8_t* h_packed, uint64_t total_bytes,
+                                    const uint64_t* h_msg_in_off, uint64_t nmsgs,
+                                    uint64_t* h_words, uint64_t words_capacity,
                                     uint64_t* h_msg_word_off, int32_t* h_status,
                                     const cpk_limits* limits);
-cpk_status cpk_pack_chunks_host(cpk_ctx* ctx, const uint64_t* h_words, const uint64_t* h_chunk_word_off,
-                                uint64_t nchunks, uint8_t* h_out, uint64_t out_capacity,
-                                uint64_t* h_chunk_out_off);
-cpk_status cpk_unpacked_size_host(cpk_ctx* ctx, const uint8_t* h_packed, uint64_t len,
-                                  uint64_t* words_out);
+
+/* ------------------------------------------------------------------------------------------
+ * Synthetic workloads (benchmarks and tests).  Fills d_words with nmsgs flat
+ * messages whose word offsets are given in d_msg_word_off (nmsgs+1 entries, e.g. from
+ * cpk_gen_offsets).  Every word is a function of (seed, first_msg + i, word index) only, so all
+ * GPUs and the host restatement (oracle) build identical bytes without transfers.
+ *   profile 0 "flat"    -- flat-struct mix (45% small ints, 20% u32 pairs, 15% zero, 10%
+ *                          pointers, 10% ASCII text)
+ *   profile 1 "pointer" -- pointer-heavy: zero stretches of 264..336 words between short runs of
+ *                          pointers / small ints
+ *   profile 2 "text"    -- ASCII text (no zero byte)
+ *   profile 3 "mixed"   -- per-message choice of 0/1/2 by hash */
+cpk_status cpk_gen_messages(cpk_ctx* ctx, int profile, uint64_t seed, uint64_t first_msg,
+                            uint64_t nmsgs, uint32_t nseg, const uint64_t* d_msg_word_off,
+                            uint64_t* d_words, void* stream);
+/* Message sizes for the generator: message i has nseg segments of seg_words words each, or,
+ * when seg_words == 0, one segment of 2^k words with k uniform in [3, 11] by hash (config C5).
+ * Writes d_msg_word_off (nmsgs+1 entries) on the device and returns the total word count. */
+cpk_status cpk_gen_offsets(cpk_ctx* ctx, uint64_t seed, uint64_t first_msg, uint64_t nmsgs,
+                           uint32_t nseg, uint64_t seg_words, uint64_t* d_msg_word_off,
+                           uint64_t* total_words_out, void* stream);
 
 #ifdef __cplusplus
 }  /* extern "C" */
 #endif
 
-#endif  /* CPK_H_ */
+#endif /* CPK_H_ */

@@ -1,0 +1,169 @@
+"""GPU parity for PACK: libcpk_hip.so (through its C ABI) vs the CPU oracle, bit-exact.
+
+Reference behaviour being matched: PackedOutputStream::write per piece
+(serialize-packed.c++:307-431) under writeMessage's chunking (serialize.c++:332-357).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import cases
+import pyoracle as P
+from gpu_util import dev, host_u8, offsets
+
+pytestmark = pytest.mark.gpu
+G = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.fixture(scope="module")
+def codec():
+    import capnproto_amd
+
+    c = capnproto_amd.Codec(0)
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="module")
+def oracle():
+    return P.Oracle()
+
+
+def gpu_pack_chunks(codec, chunks):
+    words = np.concatenate(chunks) if chunks else np.zeros(0, "<u8")
+    off = offsets([len(c) for c in chunks])
+    out, coff = codec.pack_chunks(dev(codec, words), dev(codec, off))
+    codec.sync()
+    coff = coff.cpu().numpy()
+    data = host_u8(out)[: int(coff[-1])]
+    return data.tobytes(), coff
+
+
+def gpu_pack_messages(codec, words, off):
+    out, moff, st = codec.pack_messages(dev(codec, words), dev(codec, off))
+    codec.sync()
+    moff = moff.cpu().numpy()
+    return host_u8(out)[: int(moff[-1])].tobytes(), moff, st.cpu().numpy()
+
+
+def test_kats(codec):
+    kats = json.load(open(os.path.join(G, "kats.json")))["cases"]
+    chunks = [np.frombuffer(bytes(k["unpacked"]), "<u8") if k["unpacked"] else np.zeros(0, "<u8")
+              for k in kats]
+    data, coff = gpu_pack_chunks(codec, chunks)
+    for i, k in enumerate(kats):
+        assert data[coff[i]:coff[i + 1]] == bytes(k["packed"]), i
+
+
+def test_reference_fixtures(codec):
+    rd = lambda n: open(os.path.join(G, n), "rb").read()  # noqa: E731
+    for src, dst in (("binary", "packed"), ("segmented", "segmented-packed")):
+        w = P.words_of(rd(src))
+        data, moff, st = gpu_pack_messages(codec, w, np.array([0, len(w)], np.int64))
+        assert st[0] == P.OK and data == rd(dst) and moff[1] == len(rd(dst))
+    flat = P.words_of(rd("flat"))
+    data, _ = gpu_pack_chunks(codec, [flat])
+    assert data == rd("packedflat")
+
+
+def test_edge_chunks(codec, oracle):
+    chunks = cases.edge_chunks()
+    data, coff = gpu_pack_chunks(codec, chunks)
+    for i, c in enumerate(chunks):
+        assert data[coff[i]:coff[i + 1]] == oracle.pack_chunk(c), i
+
+
+@pytest.mark.parametrize("profile", ["mixed", "bytes", "text", "zeros"])
+def test_random_chunks(codec, oracle, profile):
+    rng = np.random.default_rng(hash(profile) & 0xFFFF)
+    lens = rng.integers(0, 3000, size=40)
+    lens[::7] = 0  # empty chunks
+    chunks = [cases.random_words(rng, int(n), profile) for n in lens]
+    data, coff = gpu_pack_chunks(codec, chunks)
+    ref = [oracle.pack_chunk(c) for c in chunks]
+    assert (coff == offsets([len(r) for r in ref])).all()
+    assert data == b"".join(ref)
+
+
+def test_long_runs_across_tiles(codec, oracle):
+    """Zero / raw / R' stretches much longer than a tile (1024 words) and a chunk boundary
+    inside them; counts must see past the tile end."""
+    F = np.frombuffer(bytes(range(1, 9)), "<u8")[0]
+    R1 = np.frombuffer(bytes([1, 2, 0, 4, 5, 6, 7, 8]), "<u8")[0]
+    chunks = [np.zeros(5000, "<u8"), np.full(3333, F, "<u8"),
+              np.concatenate([np.full(700, R1, "<u8"), np.full(2000, F, "<u8")]),
+              np.zeros(1023, "<u8"), np.zeros(1, "<u8"), np.full(1025, F, "<u8"),
+              np.concatenate([[F], np.full(4000, R1, "<u8")])]
+    for shift in (0, 1, 255, 511, 1000):  # move the structure against the tile grid
+        cc = [np.zeros(shift, "<u8")] + chunks
+        data, coff = gpu_pack_chunks(codec, cc)
+        assert data == b"".join(oracle.pack_chunk(c) for c in cc), shift
+
+
+@pytest.mark.parametrize("profile", ["mixed", "bytes", "text"])
+def test_message_batches(codec, oracle, profile):
+    rng = np.random.default_rng(99 + len(profile))
+    words, off = cases.message_batch(rng, 120, max_seg=9, max_words=900, profile=profile)
+    data, moff, st = gpu_pack_messages(codec, words, off.astype(np.int64))
+    ref, roff, rst = oracle.pack_batch(words, off)
+    assert (st == 0).all() and (moff == roff.astype(np.int64)).all()
+    assert data == ref.tobytes()
+
+
+def test_bad_framing(codec, oracle):
+    rng = np.random.default_rng(5)
+    words, off = cases.message_batch(rng, 30, max_seg=4, max_words=200)
+    w = words.copy()
+    # corrupt some tables: wrong sizes / absurd segment counts
+    for k, m in enumerate(range(0, 30, 4)):
+        t32 = w[off[m]:off[m] + 1].view("<u4")
+        if k % 2:
+            t32[1] += 1
+        else:
+            t32[0] = 0xFFFFFFFF
+        w[off[m]] = t32.view("<u8")[0]
+    data, moff, st = gpu_pack_messages(codec, w, off.astype(np.int64))
+    ref, roff, rst = oracle.pack_batch(w, off)
+    assert (st == rst).all() and (st[::4] == P.BAD_FRAMING).all()
+    assert (moff == roff.astype(np.int64)).all() and data == ref.tobytes()
+
+
+def test_generated_c2_sample(codec, oracle):
+    """The bench workload (config C2 shape, 64 KiB flat-struct messages), 64 messages."""
+    off, total = codec.gen_offsets(64, nseg=1, seg_words=8191, seed=1)
+    words = codec.gen_messages("flat", off, total, nseg=1, seed=1)
+    out, moff, st = codec.pack_messages(words, off)
+    codec.sync()
+    w = words.cpu().numpy().view(np.uint64)
+    o = off.cpu().numpy()
+    ref, roff, _ = oracle.pack_batch(w, o.astype(np.uint64))
+    moff = moff.cpu().numpy()
+    assert (moff == roff.astype(np.int64)).all()
+    assert host_u8(out)[: int(moff[-1])].tobytes() == ref.tobytes()
+    assert (st.cpu().numpy() == 0).all()
+
+
+@pytest.mark.parametrize("profile", ["pointer", "text", "mixed"])
+def test_generated_profiles(codec, oracle, profile):
+    off, total = codec.gen_offsets(24, nseg=3, seg_words=3000, seed=7)
+    words = codec.gen_messages(profile, off, total, nseg=3, seed=7)
+    out, moff, st = codec.pack_messages(words, off)
+    codec.sync()
+    ref, roff, _ = oracle.pack_batch(words.cpu().numpy().view(np.uint64),
+                                     off.cpu().numpy().astype(np.uint64))
+    moff = moff.cpu().numpy()
+    assert host_u8(out)[: int(moff[-1])].tobytes() == ref.tobytes()
+
+
+def test_capacity_error(codec):
+    import capnproto_amd
+    import torch
+
+    w = np.full(5000, np.frombuffer(bytes(range(1, 9)), "<u8")[0], "<u8")
+    out = torch.empty(100, dtype=torch.uint8, device=codec.device)
+    codec.pack_chunks(dev(codec, w), dev(codec, np.array([0, len(w)], np.int64)), out=out)
+    with pytest.raises(capnproto_amd.CpkError) as ei:
+        codec.sync()
+    assert ei.value.status == capnproto_amd.CAPACITY

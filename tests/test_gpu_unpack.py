@@ -1,0 +1,205 @@
+"""GPU parity for UNPACK: libcpk_hip.so (through its C ABI) vs the CPU oracle.
+
+Reference behaviour being matched: PackedMessageReader over an array (serialize-packed.c++:437-440
+-> InputStreamMessageReader serialize.c++:202-302 -> PackedInputStream::tryRead :34-183), the
+flat-packed read (capnp.c++:1066-1071) and computeUnpackedSizeInWords (:482-508).  Words are
+compared bit-exactly for every message the reference accepts; statuses for every message.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import cases
+import pyoracle as P
+from gpu_util import concat_bytes, dev, host_u64
+
+pytestmark = pytest.mark.gpu
+G = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.fixture(scope="module")
+def codec():
+    import capnproto_amd
+
+    c = capnproto_amd.Codec(0)
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="module")
+def oracle():
+    return P.Oracle()
+
+
+def gpu_unpack(codec, msgs, limit=None):
+    """msgs: list of packed byte strings.  Returns (words per message or None, statuses)."""
+    data, off = concat_bytes(msgs)
+    cap = 300 + sum(130 * len(m) + 300 for m in msgs)
+    words, woff, st = codec.unpack_messages(dev(codec, data), dev(codec, off), cap,
+                                            nbytes=len(data), traversal_limit_words=limit)
+    codec.sync()
+    w = host_u64(words)
+    woff = woff.cpu().numpy()
+    st = st.cpu().numpy()
+    out = [w[woff[i]:woff[i + 1]].copy() if st[i] == 0 else None for i in range(len(msgs))]
+    return out, st, woff
+
+
+def check_against_oracle(codec, oracle, msgs, limit=P.DEFAULT_TRAVERSAL_LIMIT):
+    got, st, _ = gpu_unpack(codec, msgs, limit)
+    for i, m in enumerate(msgs):
+        rs, rw, used = oracle.read_message(m, limit, cap_words=300 + 260 * len(m))
+        if rs == P.OK and used != len(m):
+            rs = P.TRAILING_BYTES
+        assert st[i] == rs, (i, st[i], rs, m[:40].hex())
+        if rs == P.OK:
+            assert got[i].tobytes() == rw.tobytes(), i
+
+
+def test_reference_fixtures(codec):
+    rd = lambda n: open(os.path.join(G, n), "rb").read()  # noqa: E731
+    got, st, _ = gpu_unpack(codec, [rd("packed"), rd("segmented-packed"), rd("packed")])
+    assert (st == 0).all()
+    assert got[0].tobytes() == rd("binary") and got[2].tobytes() == rd("binary")
+    assert got[1].tobytes() == rd("segmented")
+
+
+@pytest.mark.parametrize("profile", ["mixed", "bytes", "text"])
+def test_round_trip_batches(codec, oracle, profile):
+    rng = np.random.default_rng(3 + len(profile))
+    msgs = []
+    for _ in range(150):
+        nseg = int(rng.integers(1, 9))
+        m = cases.flat_message(rng, nseg, rng.integers(0, 700, size=nseg), profile)
+        msgs.append(oracle.pack_flat(m)[0])
+    check_against_oracle(codec, oracle, msgs)
+
+
+def test_large_messages_multi_tile(codec, oracle):
+    """Messages spanning many 4 KiB tiles, incl. text (long raw runs) and long zero runs."""
+    rng = np.random.default_rng(12)
+    msgs = []
+    for prof, n in (("mixed", 30000), ("text", 20000), ("zeros", 100000), ("bytes", 25000),
+                    ("mixed", 9000)):
+        m = cases.flat_message(rng, 3, [n // 3, n // 3, n // 3], prof)
+        msgs.append(oracle.pack_flat(m)[0])
+    check_against_oracle(codec, oracle, msgs)
+
+
+def test_error_cases(codec, oracle):
+    rng = np.random.default_rng(21)
+    msgs = []
+    for _ in range(40):
+        nseg = int(rng.integers(1, 6))
+        m = cases.flat_message(rng, nseg, rng.integers(0, 300, size=nseg), "mixed")
+        pk = oracle.pack_flat(m)[0]
+        msgs.append(pk)
+        msgs.append(pk[: int(rng.integers(0, len(pk)))])            # truncated
+        bb = bytearray(pk)
+        for _ in range(int(rng.integers(1, 4))):
+            bb[int(rng.integers(0, len(bb)))] = int(rng.integers(0, 256))
+        msgs.append(bytes(bb))                                       # corrupted
+        msgs.append(pk + bytes([0x11, 0x22]))                        # trailing bytes
+    msgs += [b"", b"\x00", b"\x00\x00", b"\x00\x01", bytes([0x0f, 0xff, 0x01, 0, 0]),
+             bytes([0x03, 0xfe, 0x01]) + bytes(200), bytes([0xff]) + bytes(range(1, 9)) + b"\x05"]
+    check_against_oracle(codec, oracle, msgs)
+
+
+def test_traversal_limit(codec, oracle):
+    rng = np.random.default_rng(4)
+    msgs = [oracle.pack_flat(cases.flat_message(rng, 2, [100, 50], "mixed"))[0]
+            for _ in range(10)]
+    check_against_oracle(codec, oracle, msgs, limit=120)
+
+
+def test_non_canonical_streams(codec, oracle):
+    """The decoder must accept any valid stream (doc/encoding.md:323-329): raw runs holding
+    zero bytes, non-maximal zero runs, runs split at arbitrary points."""
+    rng = np.random.default_rng(8)
+    msgs = []
+    for _ in range(60):
+        nwords = int(rng.integers(1, 400))
+        body = bytearray()
+        w = 0
+        while w < nwords:
+            k = int(rng.integers(0, 3))
+            if k == 0:
+                c = int(rng.integers(0, min(255, nwords - w - 1) + 1))
+                body += bytes([0, c])
+                w += 1 + c
+            elif k == 1:
+                c = int(rng.integers(0, min(255, nwords - w - 1) + 1))
+                body += bytes([0xff]) + rng.integers(0, 256, 8 + 8 * c, dtype=np.uint8).tobytes()
+                body.insert(len(body) - 8 * c, c)
+                w += 1 + c
+            else:
+                tag = int(rng.integers(1, 255))
+                body += bytes([tag]) + rng.integers(1, 256, bin(tag).count("1"),
+                                                    dtype=np.uint8).tobytes()
+                w += 1
+        table = np.array([0, nwords], "<u4").tobytes()
+        head = oracle.pack_chunk(np.frombuffer(table, "<u8"))
+        msgs.append(head + bytes(body))
+    check_against_oracle(codec, oracle, msgs)
+
+
+def test_unpacked_size(codec, oracle):
+    v = np.load(os.path.join(G, "ref_vectors.npz"))
+    d, off = v["sz_in"], v["sz_in_off"]
+    bufs = [d[off[i]:off[i + 1]].tobytes() for i in range(len(off) - 1)]
+    rng = np.random.default_rng(1)
+    bufs += [oracle.pack_chunk(cases.random_words(rng, int(n), "mixed"))
+             for n in rng.integers(0, 5000, 20)]
+    bufs += [rng.integers(0, 256, int(n), dtype=np.uint8).tobytes() for n in (1, 2, 7, 33, 900)]
+    bufs += [b"", bytes([5, 1]), bytes([0xff, 1, 2, 3, 4, 5, 6, 7, 8])]
+    data, o = concat_bytes(bufs)
+    sz, st = codec.unpacked_size(dev(codec, data), dev(codec, o), nbytes=len(data))
+    codec.sync()
+    sz, st = sz.cpu().numpy(), st.cpu().numpy()
+    for i, b in enumerate(bufs):
+        rs, rw = oracle.unpacked_size(b)
+        assert st[i] == rs, (i, b[:20].hex())
+        if rs == P.OK:
+            assert sz[i] == rw, i
+
+
+def test_unpack_chunks_flat_packed(codec, oracle):
+    rng = np.random.default_rng(2)
+    chunks = [cases.random_words(rng, int(n), p) for n, p in
+              zip(rng.integers(0, 3000, 30), ["mixed", "text", "bytes", "zeros"] * 8)]
+    bufs = [oracle.pack_chunk(c) for c in chunks]
+    # error variants: expect one word more / less than encoded
+    want = [len(c) for c in chunks]
+    want[3] += 1
+    want[5] = max(0, want[5] - 1)
+    data, o = concat_bytes(bufs)
+    woff = np.zeros(len(want) + 1, np.int64)
+    woff[1:] = np.cumsum(want)
+    words, st = codec.unpack_chunks(dev(codec, data), dev(codec, o), dev(codec, woff),
+                                    nbytes=len(data))
+    codec.sync()
+    w, st = host_u64(words), st.cpu().numpy()
+    for i, b in enumerate(bufs):
+        rs, rw, pos = oracle.unpack_exact(b, want[i])
+        if rs == P.OK and pos != len(b):
+            rs = P.TRAILING_BYTES
+        assert st[i] == rs, i
+        if rs == P.OK:
+            assert w[woff[i]:woff[i + 1]].tobytes() == rw.tobytes(), i
+
+
+@pytest.mark.parametrize("profile", ["flat", "pointer", "text", "mixed"])
+def test_device_round_trip_generated(codec, profile):
+    """pack -> unpack on device reproduces the generated batch exactly (size-independent)."""
+    import torch
+
+    off, total = codec.gen_offsets(96, nseg=4, seg_words=2500, seed=3)
+    words = codec.gen_messages(profile, off, total, nseg=4, seed=3)
+    packed, moff, st = codec.pack_messages(words, off)
+    nbytes = int(moff[-1].item())
+    back, woff, st2 = codec.unpack_messages(packed, moff, total, nbytes=nbytes)
+    codec.sync()
+    assert (st2.cpu() == 0).all()
+    assert torch.equal(woff, off)
+    assert torch.equal(back[:total], words[:total])
