@@ -79,6 +79,9 @@ def load_library():
         "cpk_unpack_messages_host": (C.c_int, [vp, vp, u64, vp, u64, vp, u64, vp, vp, vp]),
         "cpk_gen_messages": (C.c_int, [vp, C.c_int, u64, u64, u64, u32, vp, vp, vp]),
         "cpk_gen_offsets": (C.c_int, [vp, u64, u64, u64, u32, u64, vp, C.POINTER(u64), vp]),
+        "cpk_timing_enable": (C.c_int, [vp, C.c_int]),
+        "cpk_timing_read": (C.c_int, [vp, C.POINTER(C.c_double), C.POINTER(u64),
+                                      C.POINTER(C.c_double), C.POINTER(u64)]),
     }
     for name, (res, args) in sigs.items():
         f = getattr(L, name)
@@ -223,6 +226,18 @@ class Codec:
                                                _ptr(status), self._stream(stream)),
                     "cpk_unpack_chunks")
         return words, status[:n]
+
+    # ------------------------------------------------------------------ measurement hooks
+    def timing(self, on: bool = True):
+        self._check(self.lib.cpk_timing_enable(self.ctx, 1 if on else 0), "cpk_timing_enable")
+
+    def timing_read(self):
+        """(pack_ms, pack_launches, unpack_ms, unpack_launches) since the last read."""
+        pm, um = C.c_double(0), C.c_double(0)
+        pl, ul = C.c_uint64(0), C.c_uint64(0)
+        self._check(self.lib.cpk_timing_read(self.ctx, C.byref(pm), C.byref(pl), C.byref(um),
+                                             C.byref(ul)), "cpk_timing_read")
+        return pm.value, pl.value, um.value, ul.value
 
     # ------------------------------------------------------------------ synthetic workloads
     def gen_offsets(self, nmsgs, nseg=1, seg_words=0, seed=0, first_msg=0, stream=None):

@@ -6,6 +6,8 @@
 #include <string.h>
 
 #include <new>
+#include <utility>
+#include <vector>
 
 #include "../../include/cpk.h"
 #include "cpk_kernels.h"
@@ -18,6 +20,10 @@ struct cpk_ctx {
   // device staging for the *_host entry points
   void* stage[4] = {nullptr, nullptr, nullptr, nullptr};
   size_t stage_size[4] = {0, 0, 0, 0};
+  // measurement hooks
+  bool timing = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[2];  // [0] pack, [1] unpack
+  std::vector<hipEvent_t> pool;
 };
 
 namespace {
@@ -49,6 +55,36 @@ struct Carve {
     T* p = (T*)(base + off);
     off = align16(off + count * sizeof(T));
     return p;
+  }
+};
+
+hipEvent_t take_event(cpk_ctx* ctx) {
+  if (!ctx->pool.empty()) {
+    hipEvent_t e = ctx->pool.back();
+    ctx->pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+// Brackets one launch with events when timing is on.
+struct TimedLaunch {
+  cpk_ctx* ctx;
+  int which;
+  hipStream_t stream;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  TimedLaunch(cpk_ctx* c, int w, hipStream_t s) : ctx(c), which(w), stream(s) {
+    if (!ctx->timing) return;
+    e0 = take_event(ctx);
+    e1 = take_event(ctx);
+    if (e0) (void)hipEventRecord(e0, stream);
+  }
+  void done() {
+    if (!ctx->timing || !e0 || !e1) return;
+    (void)hipEventRecord(e1, stream);
+    ctx->ev[which].emplace_back(e0, e1);
   }
 };
 
@@ -123,7 +159,10 @@ cpk_status pack_common(cpk_ctx* ctx, const uint64_t* d_words, uint64_t N, const 
   a.desc = s.desc;
   a.state = s.state;
   a.err = ctx->err;
-  return hip_status(cpk::launch_pack_tiles(a, stream));
+  TimedLaunch tl(ctx, 0, stream);
+  e = cpk::launch_pack_tiles(a, stream);
+  tl.done();
+  return hip_status(e);
 }
 
 struct UnpackScratch {
@@ -217,7 +256,10 @@ cpk_status unpack_common(cpk_ctx* ctx, uint32_t mode, const uint8_t* d_packed, u
   a.fail_list = s.fail_list;
   a.fail_count = s.fail_count;
   a.err = ctx->err;
-  return hip_status(cpk::launch_unpack_body(a, stream));
+  TimedLaunch tl(ctx, 1, stream);
+  e = cpk::launch_unpack_body(a, stream);
+  tl.done();
+  return hip_status(e);
 }
 
 }  // namespace
@@ -276,6 +318,12 @@ cpk_status cpk_destroy(cpk_ctx* ctx) {
   (void)hipDeviceSynchronize();
   if (ctx->scratch) (void)hipFree(ctx->scratch);
   if (ctx->err) (void)hipFree(ctx->err);
+  for (int w = 0; w < 2; w++)
+    for (auto& p : ctx->ev[w]) {
+      (void)hipEventDestroy(p.first);
+      (void)hipEventDestroy(p.second);
+    }
+  for (hipEvent_t e : ctx->pool) (void)hipEventDestroy(e);
   for (int i = 0; i < 4; i++)
     if (ctx->stage[i]) (void)hipFree(ctx->stage[i]);
   delete ctx;
@@ -427,6 +475,39 @@ cpk_status cpk_unpack_messages_host(cpk_ctx* ctx, const uint8_t* h_packed, uint6
   const uint64_t n = total < words_capacity ? total : words_capacity;
   if (n && hipMemcpy(h_words, d_words, n * 8, hipMemcpyDeviceToHost) != hipSuccess)
     return CPK_ERR_HIP;
+  return CPK_OK;
+}
+
+cpk_status cpk_timing_enable(cpk_ctx* ctx, int on) {
+  if (!ctx) return CPK_ERR_INVALID_ARGUMENT;
+  ctx->timing = on != 0;
+  return CPK_OK;
+}
+
+cpk_status cpk_timing_read(cpk_ctx* ctx, double* pack_ms, uint64_t* pack_launches,
+                           double* unpack_ms, uint64_t* unpack_launches) {
+  if (!ctx) return CPK_ERR_INVALID_ARGUMENT;
+  double ms[2] = {0, 0};
+  for (int w = 0; w < 2; w++) {
+    for (auto& p : ctx->ev[w]) {
+      float t = 0;
+      if (hipEventSynchronize(p.second) != hipSuccess ||
+          hipEventElapsedTime(&t, p.first, p.second) != hipSuccess)
+        return CPK_ERR_HIP;
+      ms[w] += t;
+    }
+  }
+  if (pack_ms) *pack_ms = ms[0];
+  if (unpack_ms) *unpack_ms = ms[1];
+  if (pack_launches) *pack_launches = ctx->ev[0].size();
+  if (unpack_launches) *unpack_launches = ctx->ev[1].size();
+  for (int w = 0; w < 2; w++) {
+    for (auto& p : ctx->ev[w]) {
+      ctx->pool.push_back(p.first);
+      ctx->pool.push_back(p.second);
+    }
+    ctx->ev[w].clear();
+  }
   return CPK_OK;
 }
 

@@ -185,6 +185,15 @@ cpk_status cpk_gen_offsets(cpk_ctx* ctx, uint64_t seed, uint64_t first_msg, uint
                            uint32_t nseg, uint64_t seg_words, uint64_t* d_msg_word_off,
                            uint64_t* total_words_out, void* stream);
 
+/* ------------------------------------------------------------------------------------------
+ * Measurement hooks (bench.py).  When enabled, every pack / unpack call brackets its main tile
+ * kernel (pack: the tile encoder; unpack: the body decoder + fallback) with HIP events on the
+ * call's stream.  cpk_timing_read synchronises those events, returns the summed milliseconds
+ * and launch counts since the last read, and clears them. */
+cpk_status cpk_timing_enable(cpk_ctx* ctx, int on);
+cpk_status cpk_timing_read(cpk_ctx* ctx, double* pack_ms, uint64_t* pack_launches,
+                           double* unpack_ms, uint64_t* unpack_launches);
+
 #ifdef __cplusplus
 }  /* extern "C" */
 #endif
