@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <new>
@@ -25,6 +26,23 @@ struct cpk_ctx {
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[2];  // [0] pack, [1] unpack
   std::vector<hipEvent_t> pool;
 };
+
+namespace cpk {
+uint32_t debug_skip() {
+  static const uint32_t v = getenv("CPK_DEBUG_SKIP") ? (uint32_t)atoi(getenv("CPK_DEBUG_SKIP")) : 0;
+  return v;
+}
+unsigned long long* debug_stamps(int which) {
+  static unsigned long long* bufs[2] = {nullptr, nullptr};
+  static const bool on = getenv("CPK_STAMPS") && atoi(getenv("CPK_STAMPS")) != 0;
+  if (!on) return nullptr;
+  if (!bufs[which]) {
+    if (hipMalloc((void**)&bufs[which], 16 * 8) != hipSuccess) return nullptr;
+    if (hipMemset(bufs[which], 0, 16 * 8) != hipSuccess) return nullptr;
+  }
+  return bufs[which];
+}
+}  // namespace cpk
 
 namespace {
 
@@ -91,6 +109,8 @@ struct TimedLaunch {
 struct PackScratch {
   uint32_t* counter;
   uint64_t* desc;
+  uint64_t* gdesc;
+  uint32_t* gcnt;
   uint32_t* state;
   uint64_t* bits;
   size_t zero_bytes;
@@ -100,8 +120,9 @@ struct PackScratch {
 
 size_t pack_scratch_bytes(uint64_t N, uint64_t ntiles) {
   const uint64_t nbitw = (N + 63) / 64;
-  return 16 + align16(8 * ntiles) + align16(4 * ntiles) + align16(8 * nbitw) +
-         align16(8 * ntiles) + 64;
+  const uint64_t ng = (ntiles + 63) / 64;
+  return 16 + align16(8 * ntiles) + align16(8 * ng) + align16(4 * ng) + align16(4 * ntiles) +
+         align16(8 * nbitw) + align16(8 * ntiles) + 64;
 }
 
 PackScratch carve_pack(void* base, uint64_t N, uint64_t ntiles) {
@@ -109,6 +130,8 @@ PackScratch carve_pack(void* base, uint64_t N, uint64_t ntiles) {
   PackScratch s;
   s.counter = c.take<uint32_t>(4);
   s.desc = c.take<uint64_t>(ntiles);
+  s.gdesc = c.take<uint64_t>((ntiles + 63) / 64);
+  s.gcnt = c.take<uint32_t>((ntiles + 63) / 64);
   s.state = c.take<uint32_t>(ntiles);
   s.bits = c.take<uint64_t>((N + 63) / 64);
   s.zero_bytes = c.off;
@@ -122,7 +145,7 @@ cpk_status pack_common(cpk_ctx* ctx, const uint64_t* d_words, uint64_t N, const 
                        uint64_t* d_out_off, int32_t* d_status, hipStream_t stream) {
   if (!ctx || (!d_off && n) || (!d_words && N) || (!d_out && cap)) return CPK_ERR_INVALID_ARGUMENT;
   if (hipSetDevice(ctx->device) != hipSuccess) return CPK_ERR_HIP;
-  const uint64_t T = cpk::kPackTileWords;
+  const uint64_t T = 64ull * cpk::pack_steps();
   const uint64_t ntiles = (N + T - 1) / T;
   cpk_status st = ensure(&ctx->scratch, &ctx->scratch_size, pack_scratch_bytes(N, ntiles));
   if (st != CPK_OK) return st;
@@ -157,8 +180,12 @@ cpk_status pack_common(cpk_ctx* ctx, const uint64_t* d_words, uint64_t N, const 
   a.total_out = nullptr;
   a.tile_counter = s.counter;
   a.desc = s.desc;
+  a.gdesc = s.gdesc;
+  a.gcnt = s.gcnt;
   a.state = s.state;
   a.err = ctx->err;
+  a.stamps = cpk::debug_stamps(0);
+  a.debug_skip = cpk::debug_skip();
   TimedLaunch tl(ctx, 0, stream);
   e = cpk::launch_pack_tiles(a, stream);
   tl.done();
@@ -168,6 +195,8 @@ cpk_status pack_common(cpk_ctx* ctx, const uint64_t* d_words, uint64_t N, const 
 struct UnpackScratch {
   uint32_t* counter;
   uint64_t* desc;
+  uint64_t* gdesc;
+  uint32_t* gcnt;
   uint32_t* state;
   uint32_t* fail_flag;
   uint32_t* fail_count;
@@ -186,6 +215,8 @@ UnpackScratch carve_unpack(void* base, uint64_t ntiles, uint64_t n) {
   UnpackScratch s;
   s.counter = c.take<uint32_t>(4);
   s.desc = c.take<uint64_t>(ntiles);
+  s.gdesc = c.take<uint64_t>((ntiles + 63) / 64);
+  s.gcnt = c.take<uint32_t>((ntiles + 63) / 64);
   s.state = c.take<uint32_t>(ntiles);
   s.fail_flag = c.take<uint32_t>(n);
   s.fail_count = c.take<uint32_t>(4);
@@ -251,11 +282,15 @@ cpk_status unpack_common(cpk_ctx* ctx, uint32_t mode, const uint8_t* d_packed, u
   a.ntiles = ntiles;
   a.tile_counter = s.counter;
   a.desc = s.desc;
+  a.gdesc = s.gdesc;
+  a.gcnt = s.gcnt;
   a.state = s.state;
   a.fail_flag = s.fail_flag;
   a.fail_list = s.fail_list;
   a.fail_count = s.fail_count;
   a.err = ctx->err;
+  a.stamps = cpk::debug_stamps(1);
+  a.debug_skip = cpk::debug_skip();
   TimedLaunch tl(ctx, 1, stream);
   e = cpk::launch_unpack_body(a, stream);
   tl.done();
@@ -334,7 +369,7 @@ cpk_status cpk_reserve(cpk_ctx* ctx, uint64_t max_words, uint64_t max_packed_byt
                        uint64_t max_items) {
   if (!ctx) return CPK_ERR_INVALID_ARGUMENT;
   if (hipSetDevice(ctx->device) != hipSuccess) return CPK_ERR_HIP;
-  const uint64_t pt = (max_words + cpk::kPackTileWords - 1) / cpk::kPackTileWords;
+  const uint64_t pt = (max_words + 63) / 64;  // covers every tile size
   size_t need = pack_scratch_bytes(max_words, pt);
   const uint64_t ut = (max_packed_bytes + cpk::kUnpackTileBytes - 1) / cpk::kUnpackTileBytes;
   const size_t un = 16 + align16(16 * ut) + align16(8 * ut) + 16 * align16(8 * (max_items + 1)) +
@@ -475,6 +510,16 @@ cpk_status cpk_unpack_messages_host(cpk_ctx* ctx, const uint8_t* h_packed, uint6
   const uint64_t n = total < words_capacity ? total : words_capacity;
   if (n && hipMemcpy(h_words, d_words, n * 8, hipMemcpyDeviceToHost) != hipSuccess)
     return CPK_ERR_HIP;
+  return CPK_OK;
+}
+
+// Diagnostic (not in include/cpk.h): copies and clears the phase-stamp sums (CPK_STAMPS=1).
+extern "C" cpk_status cpk_debug_stamps(int which, uint64_t* out16) {
+  unsigned long long* b = cpk::debug_stamps(which);
+  if (!b || !out16) return CPK_ERR_INVALID_ARGUMENT;
+  if (hipDeviceSynchronize() != hipSuccess) return CPK_ERR_HIP;
+  if (hipMemcpy(out16, b, 16 * 8, hipMemcpyDeviceToHost) != hipSuccess) return CPK_ERR_HIP;
+  if (hipMemset(b, 0, 16 * 8) != hipSuccess) return CPK_ERR_HIP;
   return CPK_OK;
 }
 

@@ -166,37 +166,234 @@ __device__ __forceinline__ uint32_t wait_nonzero32(const uint32_t* p, uint32_t* 
 // Segmented variant: when `seg_bit` is non-zero, a descriptor value carrying that bit marks a
 // tile whose aggregate restarts the scan (a message start inside it); the look-back stops there
 // and the bit is stripped from the sum.
+//
+// Window: each round reads 64*K predecessors (K per lane, all loads in flight).  The inclusive
+// prefix front can only advance one window per round-trip latency, so with thousands of small
+// tiles in flight the window width -- not the polling -- bounds throughput (64 tiles per ~1 us
+// round on MI355X is far too slow; 512 is not).  While the nearest not-ready predecessor blocks
+// progress only a single lane polls it (with s_sleep), so waiting waves do not flood L2.
+template <int K = 8>
 __device__ __forceinline__ uint64_t lookback(const uint64_t* desc, uint64_t t, uint32_t* err,
                                              uint64_t seg_bit = 0) {
   const int l = lane_id();
   uint64_t excl = 0;
-  int64_t j = (int64_t)t - 1;
+  int64_t j = (int64_t)t - 1;  // nearest predecessor not yet summed
+  uint32_t spins = 0;
   while (j >= 0) {
-    const int64_t idx = j - l;
-    uint64_t d = kDescIncl;  // lanes before tile 0 read as an inclusive zero
-    if (idx >= 0) {
-      uint32_t spins = 0;
-      for (;;) {
-        d = load_agent(desc + idx);
-        if (d & kDescFlags) break;
-        if (++spins >= kSpinLimit) {
-          raise_error(err, kErrInternal);
-          d = kDescIncl;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
+    uint64_t d[K];
+#pragma unroll
+    for (int i = 0; i < K; i++) {
+      const int64_t idx = j - (64 * i + l);
+      d[i] = idx >= 0 ? load_agent(desc + idx) : kDescIncl;  // before tile 0: inclusive zero
     }
-    const uint64_t val = d & kDescValue;
-    const bool stop = (d & kDescFlags) == kDescIncl || (seg_bit && (val & seg_bit));
-    const uint64_t stops = ballot(stop);
-    const int k = stops ? lowest_bit(stops) : 63;
-    const uint64_t contrib = (l <= k) ? (val & ~seg_bit) : 0;
+    // nearest stop (inclusive, or segment restart) in distance order 64*i + lane
+    int stop_at = 64 * K;  // distance of the nearest stop (64*K: none in this window)
+    int blocked = 64 * K;  // distance of the nearest not-ready descriptor
+#pragma unroll
+    for (int i = K - 1; i >= 0; i--) {
+      const uint64_t f = d[i] & kDescFlags;
+      const bool ready = f != 0;
+      const bool stop = f == kDescIncl || (seg_bit && ready && (d[i] & seg_bit));
+      const uint64_t sb = ballot(stop), nb = ballot(!ready);
+      if (sb) stop_at = 64 * i + lowest_bit(sb);
+      if (nb) blocked = 64 * i + lowest_bit(nb);
+    }
+    if (blocked < stop_at) {
+      // wait for the nearest blocking predecessor with one lane, then re-read the window
+      if (l == 0) {
+        const uint64_t* p = desc + (j - blocked);
+        while ((load_agent(p) & kDescFlags) == 0 && spins < kSpinLimit) {
+          __builtin_amdgcn_s_sleep(1);
+          spins++;
+        }
+      }
+      spins = uniform32(spins);
+      if (spins >= kSpinLimit) {
+        raise_error(err, kErrInternal);
+        return excl;
+      }
+      continue;
+    }
+    uint64_t contrib = 0;
+#pragma unroll
+    for (int i = 0; i < K; i++)
+      if (64 * i + l <= stop_at) contrib += (d[i] & kDescValue) & ~seg_bit;
     excl += wave_sum64(contrib);
-    if (stops) break;
-    j -= 64;
+    if (stop_at < 64 * K) break;
+    j -= 64 * K;
   }
   return excl;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Two-level decoupled look-back.
+//
+// Tiles are grouped 64 to a group.  Every tile publishes its aggregate (AGG) in desc[t]; the
+// last tile of a group to do so (ticket: atomicAdd on gcnt[g]) combines the group's 64
+// aggregates in order and publishes the group aggregate in gdesc[g]; the group's last tile
+// publishes the group's inclusive prefix there once it knows its own.  A tile then needs one
+// hop over the tiles before it in its group and, unless an inclusive prefix is found there, one
+// hop over up to 64 group descriptors (4096 tiles): with thousands of tiles in flight the
+// inclusive front no longer has to crawl one window per fabric round trip.
+//
+// Combination (segmented when seg_bit != 0): a value carrying seg_bit restarts the sum (its
+// aggregate counts only from a message start inside the tile / group).
+constexpr int kGroup = 64;
+
+__device__ __forceinline__ uint64_t seg_combine(uint64_t before, uint64_t after, uint64_t seg_bit) {
+  // value of (before ++ after)
+  if (seg_bit && (after & seg_bit)) return after;
+  return (before & seg_bit) | ((before & ~seg_bit) + (after & ~seg_bit));
+}
+
+// Each lane loads its descriptor and polls it (only lanes whose entry is not ready) until
+// ready, sleeping between polls.
+__device__ __forceinline__ uint64_t load_ready(const uint64_t* p, bool use, uint32_t* err) {
+  if (!use) return kDescIncl;
+  uint64_t d = load_agent(p);
+  uint32_t spins = 0;
+  while ((d & kDescFlags) == 0) {
+    if (++spins >= kSpinLimit) {
+      raise_error(err, kErrInternal);
+      return kDescIncl;
+    }
+    __builtin_amdgcn_s_sleep(2);
+    d = load_agent(p);
+  }
+  return d;
+}
+
+// Sum (segmented) of lanes 0..k of v, in lane order = distance order (lane 0 nearest): i.e.
+// value of entries (k, ..., 1, 0) concatenated oldest first.
+__device__ __forceinline__ uint64_t reduce_nearest(uint64_t v, int k, uint64_t seg_bit) {
+  const int l = lane_id();
+  // the nearest stop with seg bit among lanes <= k: everything farther is dropped
+  const uint64_t segs = seg_bit ? ballot(l <= k && (v & seg_bit)) : 0;
+  const int s = segs ? lowest_bit(segs) : k;  // farthest lane that contributes
+  const uint64_t contrib = (l <= s) ? (v & ~seg_bit) : 0;
+  const uint64_t sum = wave_sum64(contrib);
+  return (segs ? seg_bit : 0) | sum;
+}
+
+// Publishes tile t's aggregate and, for the group's last arriver, the group aggregate.
+__device__ __forceinline__ void publish_agg(uint64_t* desc, uint64_t* gdesc, uint32_t* gcnt,
+                                            uint64_t t, uint64_t ntiles, uint64_t agg,
+                                            uint64_t seg_bit, uint32_t* err) {
+  const int l = lane_id();
+  const uint64_t g = t / kGroup;
+  const uint64_t g0 = g * kGroup;
+  const uint32_t n_in = (uint32_t)((ntiles - g0) < (uint64_t)kGroup ? (ntiles - g0) : kGroup);
+  uint32_t old = 0;
+  if (l == 0) {
+    store_agent(desc + t, kDescAgg | agg);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    old = atomicAdd(gcnt + g, 1u);
+  }
+  old = uniform32(old);
+  if (old + 1 == n_in) {
+    // last arriver: combine the group's descriptors in order (lane i = tile g0 + n_in - 1 - i).
+    // A tile may already have replaced its AGG by its INCL: the nearest such stop makes the
+    // combination an inclusive value.
+    const int i = l;
+    const bool use = i < (int)n_in;
+    const uint64_t d = load_ready(desc + g0 + (n_in - 1 - (uint32_t)(use ? i : 0)), use, err);
+    const bool stop = use && (d & kDescFlags) == kDescIncl;
+    const uint64_t sb = ballot(stop);
+    const int k = sb ? lowest_bit(sb) : (int)n_in - 1;
+    const uint64_t v = reduce_nearest(use ? (d & kDescValue) : 0, k, seg_bit);
+    if (l == 0) {
+      const uint64_t nv = sb ? (kDescIncl | (v & ~seg_bit)) : (kDescAgg | v);
+      // never overwrite an inclusive prefix the group's last tile may have published meanwhile
+      const uint64_t cur = load_agent(gdesc + g);
+      if ((cur & kDescFlags) != kDescIncl)
+        atomicCAS((unsigned long long*)(gdesc + g), (unsigned long long)cur,
+                  (unsigned long long)nv);
+    }
+  }
+}
+
+// Exclusive prefix of tile t (after publish_agg).  Publishes nothing.
+__device__ __forceinline__ uint64_t lookback2(const uint64_t* desc, const uint64_t* gdesc,
+                                              uint64_t t, uint64_t seg_bit, uint32_t* err) {
+  const int l = lane_id();
+  const uint64_t g = t / kGroup;
+  const int j = (int)(t - g * kGroup);  // predecessors inside the group
+  uint64_t excl = 0;                    // value of everything after the stop found so far
+  {
+    const bool use = l < j;
+    const uint64_t d = load_ready(desc + (t - 1 - (uint64_t)(use ? l : 0)), use, err);
+    const bool stop = use && (((d & kDescFlags) == kDescIncl) || (seg_bit && (d & seg_bit)));
+    const uint64_t sb = ballot(stop);
+    const int k = sb ? lowest_bit(sb) : j - 1;
+    if (j > 0) excl = reduce_nearest(use ? (d & kDescValue) : 0, k, seg_bit);
+    if (sb || g == 0) return excl & ~seg_bit;
+    if (excl & seg_bit) return excl & ~seg_bit;
+  }
+  // group-level: groups g-1, g-2, ...
+  int64_t G = (int64_t)g - 1;
+  while (G >= 0) {
+    const bool use = G - l >= 0;
+    const uint64_t d = load_ready(gdesc + (use ? G - l : 0), use, err);
+    const bool stop = !use || ((d & kDescFlags) == kDescIncl) || (seg_bit && (d & seg_bit));
+    const uint64_t sb = ballot(stop);
+    const int k = sb ? lowest_bit(sb) : 63;
+    const uint64_t v = reduce_nearest(use ? (d & kDescValue) : 0, k, seg_bit);
+    excl = seg_combine(v, excl, seg_bit);
+    if (sb) break;
+    G -= 64;
+  }
+  return excl & ~seg_bit;
+}
+
+// After lookback2: publish tile t's inclusive value (and the group's, from its last tile).
+__device__ __forceinline__ void publish_incl(uint64_t* desc, uint64_t* gdesc, uint64_t t,
+                                             uint64_t ntiles, uint64_t incl) {
+  if (lane_id() != 0) return;
+  store_agent(desc + t, kDescIncl | incl);
+  const uint64_t g = t / kGroup;
+  if ((t + 1) % kGroup == 0 || t + 1 == ntiles) store_agent(gdesc + g, kDescIncl | incl);
+}
+
+// Diagnostic phase stamps (env CPK_STAMPS=1 selects a separately instantiated kernel; the
+// production kernels contain no stamp).  Lane 0 adds per-phase s_memtime deltas into its own
+// debug buffer, never into outputs.
+constexpr int kStampSlots = 16;
+__device__ __forceinline__ uint64_t stamp_now() {
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  return __builtin_amdgcn_s_memtime();
+}
+template <bool ON>
+struct Stamps {
+  unsigned long long* buf;
+  uint64_t last;
+  __device__ __forceinline__ void start(unsigned long long* b) {
+    if constexpr (ON) {
+      buf = b;
+      last = stamp_now();
+    }
+  }
+  __device__ __forceinline__ void mark(int slot) {
+    if constexpr (ON) {
+      const uint64_t now = stamp_now();
+      if (lane_id() == 0 && buf) atomicAdd(buf + slot, (unsigned long long)(now - last));
+      last = now;
+    }
+  }
+};
+
+// Blocks of `threads` threads the whole GPU keeps resident for kernel `fn` (occupancy API per
+// CU, minus `margin`, times the CU count).  Persistent kernels size their grid with it so that
+// every wave of the grid runs concurrently (a tile only ever waits on lower tiles).
+inline unsigned resident_blocks(const void* fn, int threads, int margin) {
+  int dev = 0, cus = 0, per_cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 256;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    cus = 256;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, 0) != hipSuccess)
+    per_cu = 1;
+  per_cu -= margin;
+  if (per_cu < 1) per_cu = 1;
+  return (unsigned)(per_cu * cus);
 }
 
 }  // namespace cpk

@@ -27,10 +27,15 @@ struct PackTileArgs {
   // scratch (zeroed before the launch)
   uint32_t* tile_counter;
   uint64_t* desc;              // ntiles look-back descriptors
+  uint64_t* gdesc;             // per 64-tile group look-back descriptors
+  uint32_t* gcnt;              // per group arrival tickets
   uint32_t* state;             // ntiles exit budgets (0x80000000 | budget)
   uint32_t* err;
+  unsigned long long* stamps;  // diagnostic build only (env CPK_STAMPS), else NULL
+  uint32_t debug_skip;         // timing ablations only (env CPK_DEBUG_SKIP): 1 = no look-back
 };
 
+int pack_steps();  // words per pack tile = 64 * pack_steps()
 hipError_t launch_pack_tiles(const PackTileArgs& a, hipStream_t stream);
 hipError_t launch_message_bits(const uint64_t* words, const uint64_t* off, uint64_t n,
                                uint64_t* bits, int32_t* status, hipStream_t stream);
@@ -55,12 +60,21 @@ struct UnpackArgs {
   uint64_t ntiles;
   uint32_t* tile_counter;
   uint64_t* desc;
+  uint64_t* gdesc;
+  uint32_t* gcnt;
   uint32_t* state;
   uint32_t* fail_flag;          // per message
   uint32_t* fail_list;
   uint32_t* fail_count;
   uint32_t* err;
+  unsigned long long* stamps;   // diagnostic build only (env CPK_STAMPS), else NULL
+  uint32_t debug_skip;
 };
+
+uint32_t debug_skip();
+
+// Diagnostic stamp buffers (env CPK_STAMPS=1): [0] pack, [1] unpack; kStampSlots u64 each.
+unsigned long long* debug_stamps(int which);
 
 hipError_t launch_unpack_header(const uint8_t* packed, const uint64_t* in_off, uint64_t n,
                                 uint64_t limit, uint64_t* flat, int32_t* hdr_status,

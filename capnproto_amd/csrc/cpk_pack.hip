@@ -12,18 +12,24 @@
 //   * In a Z stretch the heads sit at 0, 256, 512, ... from the stretch start; a head emits
 //     `00 n` with n = min(255, zeros left in the stretch) (:352-374).
 //   * In an R stretch an F word that is a head opens a raw run covering the next <= 255 words of
-//     the stretch (:376-426); R words that are not covered are ordinary heads.  Within any 64-word
-//     step each stretch therefore has at most one run head, which lets a wave resolve a step with
-//     64-bit ballot masks, carrying one byte of state (the run's remaining budget) between steps.
+//     the stretch (:376-426); R words that are not covered are ordinary heads.
 //   * Output bytes per word: Z head 2, Z covered 0, F head 10, covered R 8, other heads 1 + nz.
+// Inside one 64-word step a run, once opened, never closes (255 > 63), so a step is resolved by
+// a handful of 64-bit mask operations on the wave's ballots (scalar unit): raw-run coverage of
+// every segment is one carry-propagating add, `((U + G) ^ U) & U` with U = ~sync and G the F
+// words shifted by one.  The only state crossing steps is one byte: the budget of the run that
+// is open at the step's last word.
 //
-// Work decomposition: the batch of words is cut into fixed tiles of 64*S words; one wave owns a
-// tile (tile ids come from an atomic counter, so every predecessor of a running tile is already
-// resident).  A tile resolves itself locally except for the stretch that enters it from its
-// predecessor: that needs the predecessor's exit budget (published as early as possible), and
-// the byte offset of the tile comes from a single-pass decoupled look-back over tile byte
-// counts.  Output bytes are staged in a per-wave LDS ring placed at (address mod 1024) and leave
-// as aligned 16-byte stores; only the <= 15-byte partial blocks at tile edges use byte stores.
+// Work decomposition: the batch of words is cut into tiles of 64*S words, one wave per tile
+// (tile ids from an atomic counter, so every predecessor of a running tile is resident).  The
+// wave classifies its words (pass 1), publishes the budget its tile hands to the successor when
+// that does not depend on its own entry, takes its entry budget from the predecessor only when
+// word 0 continues a stretch, then encodes every step once into a per-wave LDS staging buffer
+// (pass 2, tile-relative byte offsets).  The tile's byte count feeds a single-pass decoupled
+// look-back; with the global offset known the staged bytes leave as 16-byte aligned stores
+// (realigned with v_alignbyte), only the <= 15-byte partial blocks at tile edges as byte stores.
+#include <stdlib.h>
+
 #include "cpk_device.h"
 #include "cpk_kernels.h"
 
@@ -31,357 +37,383 @@ namespace cpk {
 
 namespace {
 
-constexpr int kRing = 1024;  // per-wave LDS output ring (bytes); one step emits <= 640
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-struct StepMasks {
-  uint64_t Z, F, R, SY;  // SY: stretch starts (sync points), incl. invalid lanes
-};
+// Lane's bit of a wave-uniform 64-bit mask held in an SGPR pair: one v_cndmask.
+__device__ __forceinline__ uint32_t lanebit(uint64_t mask) {
+  uint32_t r;
+  asm("v_cndmask_b32 %0, 0, 1, %1" : "=v"(r) : "s"(mask));
+  return r;
+}
 
-// Per-lane resolution of one 64-word step.  `b` = budget entering the step (words the run that
-// is open at the previous word may still cover), meaningful when the step's word 0 continues the
-// previous stretch.  Returns head/covered for this lane and the budget leaving the step.
-struct LaneRes {
-  bool head, covered;
-};
-
-__device__ __forceinline__ LaneRes resolve_lane(const StepMasks& m, int l, int b, bool valid) {
-  const uint64_t bit = 1ull << l;
-  const uint64_t syl = m.SY & mask_le(l);
-  const int st = highest_bit(syl);
-  const int es = st >= 0 ? st : b;  // effective start of this lane's stretch in the step
-  LaneRes r{false, false};
-  if (!valid) return r;
-  if (m.Z & bit) {
-    r.head = (l == es);
-    r.covered = !r.head;
-  } else if (m.R & bit) {
-    if (l < es) {
-      r.covered = true;
-    } else {
-      const uint64_t range = mask_lt(l) & ~mask_lt(es);
-      r.covered = (m.F & range) != 0;
-      r.head = !r.covered;
+// v_perm selector compacting the set-bit bytes of nibble n to the low end (0x0c = zero byte).
+__device__ __forceinline__ uint32_t compact_sel(uint32_t n) {
+  uint32_t sel = 0x0c0c0c0cu, j = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    if ((n >> i) & 1) {
+      sel = (sel & ~(0xffu << (8 * j))) | ((uint32_t)i << (8 * j));
+      j++;
     }
-  } else {
-    r.head = true;
+  }
+  return sel;
+}
+
+struct Classes {
+  uint64_t Z, F, R, SY, V;
+};
+
+// Class masks + sync mask of one 64-word step (lane = word).  zc/rc: the word before the step
+// is a valid Z / R word of the same chunk-run (chunk starts are part of C).
+__device__ __forceinline__ Classes classify_step(uint64_t x, uint32_t tag, bool valid, uint64_t C,
+                                                 uint64_t zc, uint64_t rc) {
+  const uint32_t nz = __popc(tag);
+  Classes k;
+  k.Z = ballot(valid && x == 0);
+  k.F = ballot(valid && tag == 0xff);
+  k.R = ballot(valid && nz >= 7);
+  const uint64_t V = ballot(valid);
+  k.V = V;
+  const uint64_t O = V & ~k.Z & ~k.R;
+  const uint64_t prevZ = (k.Z << 1) | zc;
+  const uint64_t prevR = (k.R << 1) | rc;
+  k.SY = C | O | (k.Z & ~prevZ) | (k.R & ~prevR) | ~V;
+  return k;
+}
+
+// Head / coverage resolution of one step, entry budget b (words the run open before the step
+// may still cover).  All wave-uniform mask arithmetic.
+struct StepRes {
+  uint64_t covered, runheads;  // covered words; Z heads | F heads
+  int b_out;                   // budget leaving the step
+};
+
+__device__ __forceinline__ StepRes resolve_step(const Classes& k, int b, bool last_valid) {
+  const uint64_t SY = k.SY, U = ~SY;
+  const int L0 = lowest_bit(SY);  // 64 if no sync in the step
+  const bool leadZ = L0 > 0 && (k.Z & 1);
+  const bool leadR = L0 > 0 && (k.R & 1);
+  const int cb = b < L0 ? b : L0;  // words of the lead covered by the entering run
+  const uint64_t lead_cov = cb >= 64 ? ~0ull : mask_lt(cb);
+  const uint64_t zlead = (leadZ && b < L0) ? (1ull << b) : 0;
+  const uint64_t Feff = leadR ? (k.F & ~lead_cov) : k.F;
+  const uint64_t G = (Feff << 1) & U;
+  const uint64_t fill = (((U + G) ^ U) & U) | G;  // words after an F head, same segment
+  const uint64_t Rcov = k.R & (fill | (leadR ? lead_cov : 0));
+  const uint64_t Fheads = Feff & ~fill;
+  const uint64_t Zheads = (k.Z & SY) | zlead;
+  StepRes r;
+  r.covered = Rcov | (k.Z & ~Zheads);
+  r.runheads = Zheads | Fheads;
+  r.b_out = 0;
+  if (last_valid && (((k.Z | k.R) >> 63) & 1)) {
+    const int st63 = highest_bit(SY);
+    const int h = highest_bit(r.runheads);
+    if (h >= 0 && h >= st63) r.b_out = 255 - (63 - h);
+    else if (st63 < 0 && b > 63) r.b_out = b - 64;
   }
   return r;
 }
 
-// Budget leaving a step, from the ballot of run heads (Z heads and F heads).
-__device__ __forceinline__ int exit_budget(const StepMasks& m, uint64_t runheads, int b,
-                                           bool last_is_run_family) {
-  if (!last_is_run_family) return 0;
-  const int st63 = highest_bit(m.SY);
-  const int h = highest_bit(runheads);
-  if (h >= 0 && h >= st63) return 255 - (63 - h);
-  if (st63 < 0 && b > 63) return b - 64;
-  return 0;
-}
-
-struct Klass {
-  uint64_t Z, F, R, O, V;
+// Words a tile needs, loaded one tile ahead (persistent loop prefetch).
+template <int S>
+struct TileLoad {
+  uint64_t x[S];  // word 64*s + lane
+  uint64_t cb;    // chunk-start bits of step `lane` (lanes < S)
+  uint64_t pw;    // word before the tile
+  uint64_t nx;    // first step of the next tile (look-ahead for run counts)
+  uint64_t ncb;   // its chunk-start bits
 };
 
-__device__ __forceinline__ Klass classify(uint64_t x, bool valid) {
-  const uint32_t tag = word_tag(x);
-  const int nz = __popc(tag);
-  Klass k;
-  k.Z = ballot(valid && x == 0);
-  k.F = ballot(valid && tag == 0xff);
-  k.R = ballot(valid && nz >= 7);
-  k.O = ballot(valid && x != 0 && nz < 7);
-  k.V = ballot(valid);
-  return k;
-}
-
-// Sync mask of a step given its class masks, chunk-start bits and the carried class of the word
-// before the step (zc/rc: previous word was Z / R and valid).
-__device__ __forceinline__ uint64_t sync_mask(const Klass& k, uint64_t C, uint64_t zc,
-                                              uint64_t rc) {
-  const uint64_t prevZ = (k.Z << 1) | zc;
-  const uint64_t prevR = (k.R << 1) | rc;
-  return C | k.O | (k.Z & ~prevZ) | (k.R & ~prevR) | ~k.V;
-}
-
 template <int S>
-__global__ __launch_bounds__(256) void pack_tiles_kernel(PackTileArgs a) {
-  static_assert(S >= 1 && S <= 64, "S steps per tile");
+__device__ __forceinline__ void load_tile(const PackTileArgs& a, uint64_t t, TileLoad<S>& L) {
   constexpr int T = 64 * S;
-  __shared__ uint64_t lds_words[4][T];
+  const int l = lane_id();
+  const uint64_t N = a.nwords;
+  const uint64_t nbitw = (N + 63) >> 6;
+  const uint64_t tbase = t * T;
+  const uint64_t tend = tbase + T < N ? tbase + T : N;
+#pragma unroll
+  for (int s = 0; s < S; s++) {
+    const uint64_t g = tbase + 64 * s + l;
+    L.x[s] = g < N ? a.words[g] : 0;
+  }
+  L.cb = (l < S && (tbase >> 6) + l < nbitw) ? a.chunk_bits[(tbase >> 6) + l] : 0;
+  L.pw = tbase > 0 ? a.words[tbase - 1] : 0;
+  L.nx = tend + l < N ? a.words[tend + l] : 0;
+  L.ncb = (tend >> 6) < nbitw ? a.chunk_bits[tend >> 6] : 0;
+}
+
+template <int S, bool STAMPS>
+__global__ __launch_bounds__(256) void pack_tiles_kernel(PackTileArgs a) {
+  static_assert(S >= 1 && S <= 32, "S steps per tile");
+  constexpr int T = 64 * S;
+  constexpr int kRing = 1024;  // per-wave output ring (one step emits <= 640 bytes)
   __shared__ __attribute__((aligned(16))) uint8_t lds_ring[4][kRing];
 
   const int l = lane_id();
-  const int wv = threadIdx.x >> 6;
-  uint64_t* xw = lds_words[wv];
+  const int wv = (int)uniform32(threadIdx.x >> 6);  // wave-uniform (keeps tile math scalar)
   uint8_t* ring = lds_ring[wv];
-
-  uint32_t t32 = 0;
-  if (l == 0) t32 = atomicAdd(a.tile_counter, 1u);
-  const uint64_t t = uniform32(t32);
-  if (t >= a.ntiles) return;
-
+  *(u32x4*)(ring + 16 * l) = (u32x4){0, 0, 0, 0};
+  const uint32_t csel = compact_sel((uint32_t)l & 15);
+  const uint64_t gt_mask = ~mask_le(l);  // lanes above this one
   const uint64_t N = a.nwords;
-  const uint64_t tbase = t * T;
-  const uint64_t tend = tbase + T < N ? tbase + T : N;
-
-  // ---- load the tile (coalesced, all loads in flight), then stage into LDS -------------------
-  {
-    uint64_t v[S];
-#pragma unroll
-    for (int s = 0; s < S; s++) {
-      const uint64_t g = tbase + 64 * s + l;
-      v[s] = g < N ? a.words[g] : 0;
-    }
-#pragma unroll
-    for (int s = 0; s < S; s++) xw[64 * s + l] = v[s];
-  }
   const uint64_t nbitw = (N + 63) >> 6;
-  const uint64_t cbw = (l < S && (tbase >> 6) + l < nbitw) ? a.chunk_bits[(tbase >> 6) + l] : 0;
-
-  // Class of the word before the tile (same-chunk test is the chunk bit of word 0).
-  uint64_t zc = 0, rc = 0;
-  if (tbase > 0) {
-    const uint64_t pw = a.words[tbase - 1];
-    zc = pw == 0;
-    rc = __popc(word_tag(pw)) >= 7;
-  }
-
-  // ---- pass 1: per-step class masks; lane s keeps step s's masks -----------------------------
-  uint64_t myZ = 0, myF = 0, myR = 0, mySY = 0;
-  bool any_sync_valid = false;
-  int first_sync = T;  // first sync position among valid words
-  {
-    uint64_t czc = zc, crc = rc;
-    for (int s = 0; s < S; s++) {
-      const uint64_t g = tbase + 64 * s + l;
-      const bool valid = g < N;
-      const uint64_t x = xw[64 * s + l];
-      const Klass k = classify(x, valid);
-      const uint64_t C = readlane64(cbw, s);
-      const uint64_t SY = sync_mask(k, C, czc, crc);
-      czc = k.Z >> 63;
-      crc = k.R >> 63;
-      const uint64_t syv = SY & k.V;
-      if (syv && !any_sync_valid) {
-        any_sync_valid = true;
-        first_sync = 64 * s + lowest_bit(syv);
-      }
-      if (l == s) {
-        myZ = k.Z;
-        myF = k.F;
-        myR = k.R;
-        mySY = SY;
-      }
-    }
-  }
-  const int nvalid = (int)(tend - tbase);
-  const int last = nvalid - 1;  // tile position of the last valid word
-  const bool last_Z = (readlane64(myZ, last >> 6) >> (last & 63)) & 1;
-  const bool last_R = (readlane64(myR, last >> 6) >> (last & 63)) & 1;
-
-  // ---- look-ahead: first sync position after the tile (for run counts near the end) ----------
-  // la = distance from tend to the first word that ends the trailing stretch (<= 256).
-  int la = 0;
-  if ((last_Z || last_R) && tend < N) {
-    uint64_t czc = last_Z, crc = last_R;
-    la = 256;
-    for (int k = 0; k < 4; k++) {
-      const uint64_t g = tend + 64 * k + l;
-      const bool valid = g < N;
-      const uint64_t x = valid ? a.words[g] : 0;
-      const Klass kk = classify(x, valid);
-      const uint64_t C = ((tend >> 6) + k < nbitw) ? a.chunk_bits[(tend >> 6) + k] : 0;
-      const uint64_t SY = sync_mask(kk, C, czc, crc);
-      czc = kk.Z >> 63;
-      crc = kk.R >> 63;
-      if (SY) {
-        la = 64 * k + lowest_bit(SY);
-        break;
-      }
-    }
-  }
-
-  // first sync bit per step (lane s), used for run counts
-  const int myFs = lowest_bit(mySY);
-
-  // Distance from the start of step s+1 to the first sync at or after it (capped at 256).
-  auto next_sync_after = [&](int s) -> int {
-    int d = 0;
-    for (int k = s + 1; k < S && d < 256; k++) {
-      const int fs = (int)readlane32((uint32_t)myFs, k);
-      if (fs < 64) return d + fs;
-      d += 64;
-    }
-    if (s + 1 >= S) return la;
-    return d < 256 ? d + la : 256;
-  };
-
-  auto masks_of = [&](int s) -> StepMasks {
-    StepMasks m;
-    m.Z = readlane64(myZ, s);
-    m.F = readlane64(myF, s);
-    m.R = readlane64(myR, s);
-    m.SY = readlane64(mySY, s);
-    return m;
-  };
-
-  // Byte count of steps [s0, s1) with entry budget b at step s0; lanes with tile position < lo
-  // or >= hi are not counted.  Returns the budget leaving step s1-1 in *bout.
-  auto count_steps = [&](int s0, int s1, int b, int lo, int hi, int* bout) -> uint64_t {
-    uint64_t bytes = 0;
-    for (int s = s0; s < s1; s++) {
-      const StepMasks m = masks_of(s);
-      const int pos = 64 * s + l;
-      const bool valid = pos < nvalid;
-      const LaneRes r = resolve_lane(m, l, b, valid);
-      const uint64_t bit = 1ull << l;
-      const uint32_t tag = word_tag(xw[pos]);
-      uint32_t len = 0;
-      if (r.covered) len = (m.R & bit) ? 8 : 0;
-      else if (r.head) len = (m.Z & bit) ? 2 : ((m.F & bit) ? 10 : 1 + __popc(tag));
-      if (pos < lo || pos >= hi) len = 0;
-      uint32_t tot;
-      wave_excl_sum_small(len, &tot);
-      bytes += tot;
-      const uint64_t runheads = ballot(r.head && ((m.Z | m.F) & bit));
-      const int l63 = 64 * s + 63;
-      const bool fam = l63 < nvalid && (((m.Z | m.R) >> 63) & 1);
-      b = exit_budget(m, runheads, b, fam);
-    }
-    *bout = b;
-    return bytes;
-  };
-
-  // ---- exit state (published early when independent of the entry) ---------------------------
-  uint32_t* const state = a.state;
-  uint64_t bytes_suffix = 0;
-  int exit_b = 0;
-  if (any_sync_valid) {
-    const int s0 = first_sync >> 6;
-    bytes_suffix = count_steps(s0, S, 0, first_sync, T, &exit_b);
-    if (l == 0) store_agent32(state + t, 0x80000000u | (uint32_t)exit_b);
-  }
-
-  // ---- entry budget -------------------------------------------------------------------------
-  int b_entry = 0;
-  if (first_sync > 0 && t > 0) {
-    b_entry = (int)(wait_nonzero32(state + t - 1, a.err) & 0xffu);
-  }
-  uint64_t bytes_lead = 0;
-  if (first_sync > 0) {
-    const int s1 = any_sync_valid ? (first_sync >> 6) + 1 : S;
-    int bo;
-    bytes_lead = count_steps(0, s1, b_entry, 0, first_sync, &bo);
-    if (!any_sync_valid) {
-      exit_b = bo;
-      if (l == 0) store_agent32(state + t, 0x80000000u | (uint32_t)exit_b);
-    }
-  }
-  const uint64_t agg = bytes_lead + bytes_suffix;
-
-  // ---- decoupled look-back for the tile's output offset -------------------------------------
-  uint64_t excl = 0;
-  if (t == 0) {
-    if (l == 0) store_agent(a.desc, kDescIncl | agg);
-  } else {
-    if (l == 0) store_agent(a.desc + t, kDescAgg | agg);
-    excl = lookback(a.desc, t, a.err);
-    if (l == 0) store_agent(a.desc + t, kDescIncl | (excl + agg));
-  }
-
-  // ---- emission -----------------------------------------------------------------------------
   const uint64_t base_addr = (uint64_t)(uintptr_t)a.out;
-  const uint64_t A0 = base_addr + excl;
-  const uint64_t A1 = A0 + agg;
-  const uint64_t al = (A0 + 15) & ~15ull;
-  const bool over = excl + agg > a.out_capacity;
-  if (over && l == 0) raise_error(a.err, kErrCapacity);
-  uint64_t flushed = al;  // next 16-aligned block to store
-  uint64_t hd = A0;       // next head (partial-block) byte to store
-  uint64_t A = A0;        // address of the next emitted byte
+  uint32_t* const state = a.state;
 
-  // positions whose output offset is requested (message / chunk starts)
-  uint64_t pidx = a.pos ? uniform64(a.tile_first[t]) : 0;
-  uint64_t pnext = (a.pos && pidx <= a.npos) ? uniform64(a.pos[pidx]) : ~0ull;
+  // Persistent waves, static strided tile order (grid <= guaranteed residency, see launch):
+  // a tile only waits on lower tiles, which belong to resident waves that reach them first.
+  const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  Stamps<STAMPS> stm;
+  uint64_t t = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wv;
+  TileLoad<S> cur;
+  if (t < a.ntiles) load_tile<S>(a, t, cur);
+  for (; t < a.ntiles; t += nwaves) {
+    stm.start(a.stamps);
+    const uint64_t tbase = t * T;
+    const uint64_t tend = tbase + T < N ? tbase + T : N;
+    const int nvalid = (int)(tend - tbase);
+    const int last = nvalid - 1;
+    const int nsteps = (nvalid + 63) >> 6;
+    uint64_t zc = 0, rc = 0;
+    if (tbase > 0) {
+      zc = cur.pw == 0;
+      rc = __popc(word_tag(cur.pw)) >= 7;
+    }
 
-  int b = b_entry;
-  for (int s = 0; s < S; s++) {
-    if (64 * s >= nvalid) break;
-    const StepMasks m = masks_of(s);
-    const int pos = 64 * s + l;
-    const bool valid = pos < nvalid;
-    const uint64_t bit = 1ull << l;
-    const uint64_t x = xw[pos];
-    const uint32_t tag = word_tag(x);
-    const LaneRes r = resolve_lane(m, l, b, valid);
-    const bool isZ = m.Z & bit, isF = m.F & bit, isR = m.R & bit;
-    uint32_t len = 0;
-    uint64_t lo = 0;
-    uint32_t hi = 0;
-    // run count for Z / F heads: min(255, words left in the stretch after this one)
-    const int nsa = next_sync_after(s);
-    uint32_t cnt = 0;
-    if (r.head && (isZ || isF)) {
-      const uint64_t gt = m.SY & ~mask_le(l);
-      const int ns = gt ? lowest_bit(gt) : 64 + nsa;
-      const int c = ns - l - 1;
-      cnt = (uint32_t)(c < 255 ? c : 255);
-    }
-    if (r.covered) {
-      if (isR) {
-        len = 8;
-        lo = x;
-      }
-    } else if (r.head) {
-      if (isZ) {
-        len = 2;
-        lo = (uint64_t)cnt << 8;
-      } else if (isF) {
-        len = 10;
-        lo = 0xffull | (x << 8);
-        hi = (uint32_t)(x >> 56) | (cnt << 8);
-      } else {
-        len = 1 + __popc(tag);
-        lo = (uint64_t)tag | (compact_nonzero(x) << 8);
-      }
-    }
-    uint32_t step_total;
-    const uint32_t o = wave_excl_sum_small(len, &step_total);
-    if (!over) {
+    // ---- pass 1: classes (lane s keeps step s's masks) and O-word bytes ----------------------
+    uint64_t myZ = 0, myF = 0, myR = 0, mySY = 0;
+    uint32_t myOB = 0;
+    int first_sync = T;
+    {
+      uint64_t czc = zc, crc = rc;
 #pragma unroll
-      for (int k = 0; k < 10; k++) {
-        if ((uint32_t)k < len) {
-          const uint8_t byte = k < 8 ? (uint8_t)(lo >> (8 * k)) : (uint8_t)(hi >> (8 * (k - 8)));
-          ring[(A + o + k) & (kRing - 1)] = byte;
+      for (int s = 0; s < S; s++) {
+        const bool valid = 64 * s + l < nvalid;
+        const uint32_t tag = word_tag(cur.x[s]);
+        const Classes k = classify_step(cur.x[s], tag, valid, readlane64(cur.cb, s), czc, crc);
+        czc = k.Z >> 63;
+        crc = k.R >> 63;
+        const uint64_t syv = k.SY & k.V;
+        if (first_sync == T && syv) first_sync = 64 * s + lowest_bit(syv);
+        // bytes of O words (always heads, state independent): 1 + nz <= 7
+        const uint32_t nz = __popc(tag);
+        const uint32_t ob = (valid && cur.x[s] != 0 && nz < 7) ? 1 + nz : 0;
+        const uint32_t OB = (uint32_t)(__popcll(ballot(ob & 1)) + 2 * __popcll(ballot(ob & 2)) +
+                                       4 * __popcll(ballot(ob & 4)));
+        if (l == s) {
+          myZ = k.Z;
+          myF = k.F;
+          myR = k.R;
+          mySY = k.SY;
+          myOB = OB;
         }
       }
     }
-    // requested output offsets for positions inside this step
-    const uint64_t g0 = tbase + 64 * s;
-    while (pnext < g0 + 64) {
-      const uint64_t i = pidx + l;
-      const uint64_t p = i <= a.npos ? a.pos[i] : ~0ull;
-      const bool in = p < g0 + 64;
-      const uint32_t src = in ? (uint32_t)(p - g0) : 0;
-      const uint32_t oo = shfl32(o, (int)src);
-      if (in) a.pos_out[i] = (A - base_addr) + oo;
-      const uint64_t inm = ballot(in);
-      pidx += __popcll(inm);
-      pnext = pidx <= a.npos ? uniform64(a.pos[pidx]) : ~0ull;
-      if (inm != ~0ull) break;
+    stm.mark(0);  // pass 1
+
+    // ---- look-ahead: first sync after the tile (run counts need <= 255 words) -----------------
+    int la = 0;
+    {
+      const bool lastZ = (readlane64(myZ, last >> 6) >> (last & 63)) & 1;
+      const bool lastR = (readlane64(myR, last >> 6) >> (last & 63)) & 1;
+      if ((lastZ || lastR) && tend < N) {
+        uint64_t czc = lastZ, crc = lastR;
+        la = 256;
+        for (int k = 0; k < 4; k++) {
+          const uint64_t g = tend + 64 * k + l;
+          const bool valid = g < N;
+          uint64_t xx, C;
+          if (k == 0) {
+            xx = cur.nx;
+            C = cur.ncb;
+          } else {
+            xx = valid ? a.words[g] : 0;
+            C = ((tend >> 6) + k < nbitw) ? a.chunk_bits[(tend >> 6) + k] : 0;
+          }
+          const Classes kk = classify_step(xx, word_tag(xx), valid, C, czc, crc);
+          czc = kk.Z >> 63;
+          crc = kk.R >> 63;
+          if (kk.SY) {
+            la = 64 * k + lowest_bit(kk.SY);
+            break;
+          }
+        }
+      }
     }
-    b = exit_budget(m, ballot(r.head && ((m.Z | m.F) & bit)), b,
-                    (64 * s + 63 < nvalid) && (((m.Z | m.R) >> 63) & 1));
-    const uint64_t Aend = A + step_total;
-    if (!over) {
+    int myNsa = 0;  // lane s: distance from step s+1 to the first sync at or after it (<= 256)
+    {
+      int v = la;
+      for (int s = S - 1; s >= 0; s--) {
+        if (l == s) myNsa = v;
+        const int fs = lowest_bit(readlane64(mySY, s));
+        v = s >= nsteps ? la : (fs < 64 ? fs : (v + 64 < 256 ? v + 64 : 256));
+      }
+    }
+
+    // ---- exit budget, published early when it does not depend on our own entry --------------
+    auto first_F_from = [&](int xpos) -> int {
+      for (int k = xpos >> 6; k < nsteps; k++) {
+        uint64_t m = readlane64(myF, k);
+        if (k == (xpos >> 6)) m &= ~mask_lt(xpos & 63);
+        if (m) return 64 * k + lowest_bit(m);
+      }
+      return 1 << 20;
+    };
+    if (first_sync < T) {
+      int sg = -1;
+      for (int k = last >> 6; k >= 0; k--) {
+        uint64_t m = readlane64(mySY, k);
+        if (k == (last >> 6)) m &= mask_le(last & 63);
+        if (m) {
+          sg = 64 * k + highest_bit(m);
+          break;
+        }
+      }
+      const bool sZ = (readlane64(myZ, sg >> 6) >> (sg & 63)) & 1;
+      const bool sR = (readlane64(myR, sg >> 6) >> (sg & 63)) & 1;
+      int eb = 0;
+      if (sZ) {
+        eb = 255 - ((last - sg) & 255);
+      } else if (sR) {
+        int qq = -1;
+        for (int q = first_F_from(sg); q <= last; q = first_F_from(q + 256)) qq = q;
+        eb = (qq >= 0 && last - qq <= 255) ? 255 - (last - qq) : 0;
+      }
+      if (l == 0) store_agent32(state + t, 0x80000000u | (uint32_t)eb);
+    }
+    stm.mark(1);  // look-ahead, run-count table, early exit budget
+    int b = 0;
+    if (first_sync > 0 && t > 0) b = (int)(wait_nonzero32(state + t - 1, a.err) & 0xffu);
+    stm.mark(2);  // entry wait
+
+    // ---- count pass (scalar): per-step coverage and byte offsets ------------------------------
+    //   bytes(step) = 8 |R| + 2 |Z heads + F heads| + sum over O words of (1 + nz)
+    uint64_t myCov = 0;
+    uint32_t myOff = 0;
+    uint32_t off = 0;
+    for (int s = 0; s < nsteps; s++) {
+      Classes k;
+      k.Z = readlane64(myZ, s);
+      k.F = readlane64(myF, s);
+      k.R = readlane64(myR, s);
+      k.SY = readlane64(mySY, s);
+      const StepRes r = resolve_step(k, b, 64 * s + 63 < nvalid);
+      const uint32_t bytes = readlane32(myOB, s) + 8 * (uint32_t)__popcll(k.R) +
+                             2 * (uint32_t)__popcll(r.runheads);
+      if (l == s) {
+        myCov = r.covered;
+        myOff = off;
+      }
+      off += bytes;
+      b = r.b_out;
+    }
+    if (first_sync == T && l == 0) store_agent32(state + t, 0x80000000u | (uint32_t)b);
+    const uint64_t agg = off;
+    stm.mark(3);  // count pass
+
+    // ---- publish, prefetch the next tile, look-back ------------------------------------------
+    uint64_t excl = 0;
+    if (a.debug_skip & 1) {
+      excl = t * 4096;  // timing ablation: no look-back (output meaningless)
+    } else {
+      publish_agg(a.desc, a.gdesc, a.gcnt, t, a.ntiles, agg, 0, a.err);
+    }
+    TileLoad<S> nxt;
+    if (t + nwaves < a.ntiles) load_tile<S>(a, t + nwaves, nxt);
+    if (!(a.debug_skip & 1)) {
+      excl = lookback2(a.desc, a.gdesc, t, 0, a.err);
+      publish_incl(a.desc, a.gdesc, t, a.ntiles, excl + agg);
+    }
+    stm.mark(4);  // look-back
+
+    // ---- emission: encode each step through the ring, 16-byte aligned stores ----------------
+    const uint64_t A0 = base_addr + excl;
+    const uint64_t A1 = A0 + agg;
+    const bool over = excl + agg > a.out_capacity;
+    if (over && l == 0) raise_error(a.err, kErrCapacity);
+    const uint64_t al = (A0 + 15) & ~15ull;
+    uint64_t flushed = al;  // next full block to store
+    uint64_t hd = A0;       // next head-block byte to store
+    uint64_t pidx = a.pos ? uniform64(a.tile_first[t]) : 0;
+    uint64_t pnext = (a.pos && pidx <= a.npos) ? uniform64(a.pos[pidx]) : ~0ull;
+    for (int s = 0; s < nsteps && !over; s++) {
+      const uint64_t Z = readlane64(myZ, s), F = readlane64(myF, s), R = readlane64(myR, s);
+      const uint64_t SY = readlane64(mySY, s), COV = readlane64(myCov, s);
+      const uint32_t soff = readlane32(myOff, s);
+      const int nsa = (int)readlane32((uint32_t)myNsa, s);
+      uint64_t xv = 0;
+#pragma unroll
+      for (int ss = 0; ss < S; ss++)
+        if (ss == s) xv = cur.x[ss];
+      const uint32_t tag = word_tag(xv);
+      const uint32_t isZ = lanebit(Z), isF = lanebit(F), isR = lanebit(R), cov = lanebit(COV);
+      const bool valid = 64 * s + l < nvalid;
+      // bytes of this word's record
+      const uint32_t hlen = isZ ? 2u : (isF ? 10u : 1u + (uint32_t)__popc(tag));
+      const uint32_t len = !valid ? 0u : (cov ? (isR ? 8u : 0u) : hlen);
+      // run count of Z / F heads: min(255, stretch words left after this one)
+      const uint64_t gt = SY & gt_mask;
+      const int ns = gt ? lowest_bit(gt) : 64 + nsa;
+      const uint32_t cnt = (uint32_t)min(ns - l - 1, 255);
+      // string: slo = bytes 0..7, shi = bytes 8..9 (branch-free selects)
+      const uint32_t xlo = (uint32_t)xv, xhi = (uint32_t)(xv >> 32);
+      const uint32_t tl = tag & 15, th = tag >> 4;
+      const uint32_t clo = __builtin_amdgcn_perm(0u, xlo, shfl32(csel, (int)tl));
+      const uint32_t chi = __builtin_amdgcn_perm(0u, xhi, shfl32(csel, (int)th));
+      const uint64_t comp = (uint64_t)clo | ((uint64_t)chi << (8 * __popc(tl)));
+      const uint64_t s_head = (uint64_t)tag | (comp << 8);
+      const uint64_t s_f = 0xffull | (xv << 8);
+      const uint64_t s_z = (uint64_t)cnt << 8;
+      const uint64_t slo = cov ? xv : (isZ ? s_z : (isF ? s_f : s_head));
+      const uint32_t shi = (!cov && isF) ? ((xhi >> 24) | (cnt << 8)) : 0u;
+      uint32_t total;
+      const uint32_t o = wave_excl_sum_small(len, &total);
+      const uint64_t A = A0 + soff;
+      {
+        // OR the string into the ring (zeroed), dword-aligned to its global address
+        const uint64_t at = A + o;
+        const uint32_t al4 = (uint32_t)at & 3;
+        const uint32_t w0 = (uint32_t)slo, w1 = (uint32_t)(slo >> 32), w2 = shi;
+        const uint32_t sh = 4 - al4;
+        const uint32_t e0 = w0 << (8 * al4);
+        const uint32_t e1 = al4 ? __builtin_amdgcn_alignbyte(w1, w0, sh) : w1;
+        const uint32_t e2 = al4 ? __builtin_amdgcn_alignbyte(w2, w1, sh) : w2;
+        const uint32_t e3 = al4 ? __builtin_amdgcn_alignbyte(0u, w2, sh) : 0u;
+        const uint32_t nd = len ? (al4 + len + 3) >> 2 : 0;
+        const uint32_t d0 = (uint32_t)(at >> 2);
+        uint32_t* rw = (uint32_t*)ring;
+        constexpr uint32_t M = kRing / 4 - 1;
+        if (nd > 0) atomicOr(rw + ((d0 + 0) & M), e0);
+        if (nd > 1) atomicOr(rw + ((d0 + 1) & M), e1);
+        if (nd > 2) atomicOr(rw + ((d0 + 2) & M), e2);
+        if (nd > 3) atomicOr(rw + ((d0 + 3) & M), e3);
+      }
+      // requested output offsets (message / chunk starts) inside this step
+      const uint64_t g0 = tbase + 64 * s;
+      while (pnext < g0 + 64) {
+        const uint64_t i = pidx + l;
+        const uint64_t p = i <= a.npos ? a.pos[i] : ~0ull;
+        const bool in = p < g0 + 64;
+        const uint32_t oo = shfl32(o, in ? (int)(p - g0) : 0);
+        if (in) a.pos_out[i] = excl + soff + oo;
+        const uint64_t inm = ballot(in);
+        pidx += __popcll(inm);
+        pnext = pidx <= a.npos ? uniform64(a.pos[pidx]) : ~0ull;
+        if (inm != ~0ull) break;
+      }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      const uint64_t Aend = A + total;
       // partial head block (shared with the previous tile's bytes): byte stores
       const uint64_t hlim = Aend < al ? Aend : al;
       if (hd < hlim) {
         const uint64_t p = hd + l;
-        if (l < 16 && p < hlim) *(uint8_t*)(uintptr_t)p = ring[p & (kRing - 1)];
+        if (l < 16 && p < hlim) {
+          uint8_t* rb = ring + (p & (kRing - 1));
+          *(uint8_t*)(uintptr_t)p = *rb;
+          *rb = 0;
+        }
         hd = hlim;
       }
       // full 16-byte blocks
@@ -392,29 +424,36 @@ __global__ __launch_bounds__(256) void pack_tiles_kernel(PackTileArgs a) {
           const uint32_t i = i0 + l;
           if (i < nb) {
             const uint64_t p = flushed + 16ull * i;
-            const u32x4 v = *(const u32x4*)(ring + (p & (kRing - 1)));
+            u32x4* rb = (u32x4*)(ring + (p & (kRing - 1)));
+            const u32x4 v = *rb;
+            *rb = (u32x4){0, 0, 0, 0};
             *(u32x4*)(uintptr_t)p = v;
           }
         }
         flushed = top;
       }
     }
-    A = Aend;
-  }
-  if (!over) {
-    // partial tail block
-    const uint64_t from = flushed > hd ? flushed : hd;
-    if (from < A1) {
+    if (!over) {
+      // partial tail block
+      const uint64_t from = flushed > hd ? flushed : hd;
       const uint64_t p = from + l;
-      if (l < 16 && p < A1) *(uint8_t*)(uintptr_t)p = ring[p & (kRing - 1)];
+      if (l < 16 && p < A1) {
+        uint8_t* rb = ring + (p & (kRing - 1));
+        *(uint8_t*)(uintptr_t)p = *rb;
+        *rb = 0;
+      }
     }
-  }
-  // positions at or past the end of the batch -> total
-  if (a.pos && tend == N) {
-    const uint64_t total = excl + agg;
-    for (uint64_t i = pidx + l; i <= a.npos; i += 64) a.pos_out[i] = total;
-    if (l == 0 && a.total_out) *a.total_out = total;
-  }
+    // positions at or past the end of the batch -> total
+    if (a.pos && tend == N) {
+      const uint64_t tot = excl + agg;
+      for (uint64_t i = pidx + l; i <= a.npos; i += 64) a.pos_out[i] = tot;
+      if (l == 0 && a.total_out) *a.total_out = tot;
+    }
+    stm.mark(5);  // emission
+    if (STAMPS && l == 0 && a.stamps) atomicAdd(a.stamps + 15, 1ull);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    cur = nxt;
+  }  // tile loop
 }
 
 // Chunk-start bitmap + per-message framing status for a batch of flat messages.
@@ -483,12 +522,34 @@ __global__ void tile_first_kernel(const uint64_t* __restrict__ pos, uint64_t npo
 }  // namespace
 
 // ---------------------------------------------------------------------------------------------
+int pack_steps() {
+  static int steps = [] {
+    const char* e = getenv("CPK_PACK_STEPS");  // tuning knob: 8 or 16 (default)
+    const int v = e ? atoi(e) : kPackSteps;
+    return (v == 8 || v == 16 || v == 4) ? v : kPackSteps;
+  }();
+  return steps;
+}
+
+template <int S>
+hipError_t launch_pack_s(const PackTileArgs& a, hipStream_t stream) {
+  static const unsigned cap = resident_blocks((const void*)pack_tiles_kernel<S, false>, 256, 0);
+  const uint64_t want = (a.ntiles + 3) / 4;
+  const unsigned blocks = (unsigned)(want < cap ? want : cap);
+  if (a.stamps)
+    hipLaunchKernelGGL((pack_tiles_kernel<S, true>), dim3(blocks), dim3(256), 0, stream, a);
+  else
+    hipLaunchKernelGGL((pack_tiles_kernel<S, false>), dim3(blocks), dim3(256), 0, stream, a);
+  return hipGetLastError();
+}
+
 hipError_t launch_pack_tiles(const PackTileArgs& a, hipStream_t stream) {
   if (a.ntiles == 0) return hipSuccess;
-  const uint64_t waves = a.ntiles;
-  const uint64_t blocks = (waves + 3) / 4;
-  hipLaunchKernelGGL(pack_tiles_kernel<kPackSteps>, dim3((unsigned)blocks), dim3(256), 0, stream, a);
-  return hipGetLastError();
+  switch (pack_steps()) {
+    case 4: return launch_pack_s<4>(a, stream);
+    case 8: return launch_pack_s<8>(a, stream);
+    default: return launch_pack_s<16>(a, stream);
+  }
 }
 
 hipError_t launch_message_bits(const uint64_t* words, const uint64_t* off, uint64_t n,

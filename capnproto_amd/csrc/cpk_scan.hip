@@ -34,7 +34,7 @@ __global__ __launch_bounds__(256) void scan_kernel(const uint64_t* __restrict__ 
     if (l == 0) store_agent(desc, kDescIncl | agg);
   } else {
     if (l == 0) store_agent(desc + t, kDescAgg | agg);
-    excl = lookback(desc, t, err);
+    excl = lookback<8>(desc, t, err);
     if (l == 0) store_agent(desc + t, kDescIncl | (excl + agg));
   }
   uint64_t carry = excl;
