@@ -32,8 +32,8 @@ CONFIGS = {
                workload="C3: 1 Mi x 4 KiB flat-struct messages (tag-byte dominated)"),
     "c4": dict(nmsgs=256, nseg=16, seg_words=524288, profile="pointer",
                workload="C4: 256 x 64 MiB pointer-heavy messages, 16 segments each"),
-    "c5": dict(nmsgs=(32 << 20) // 8, nseg=1, seg_words=0, profile="mixed",
-               workload="C5: 32 Mi mixed-size messages (64 B-16 KiB), 1/8 of them per GPU"),
+    "c5": dict(nmsgs=(32 << 20) // 8, nseg=1, seg_words=0, profile="mixed", shard="round_robin",
+               workload="C5: 32 Mi mixed-size messages (64 B-16 KiB), round-robin, 4 Mi per GPU"),
 }
 
 
@@ -104,6 +104,7 @@ def main():
     import torch
 
     import capnproto_amd
+    from capnproto_amd.shard import reduce_step, shard_messages
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
@@ -122,14 +123,13 @@ def main():
             dist.barrier()
 
     cfg = CONFIGS[args.config]
-    n = cfg["nmsgs"]
     codec = capnproto_amd.Codec(local)
-    # Independent message shards: rank r owns messages [r*n, (r+1)*n) of the global batch.
-    first = rank * n
+    # Independent message shards (weak scaling: nmsgs per GPU): capnproto_amd/shard.py.
+    first, stride, n = shard_messages(rank, world, cfg["nmsgs"] * world, cfg.get("shard", "block"))
     off, total = codec.gen_offsets(n, nseg=cfg["nseg"], seg_words=cfg["seg_words"],
-                                   seed=args.seed, first_msg=first)
+                                   seed=args.seed, first_msg=first, msg_stride=stride)
     words = codec.gen_messages(cfg["profile"], off, total, nseg=cfg["nseg"], seed=args.seed,
-                               first_msg=first)
+                               first_msg=first, msg_stride=stride)
     cap = codec.packed_bound(total, n * (cfg["nseg"] + 1)) + 64
     packed = torch.empty(cap, dtype=torch.uint8, device=codec.device)
     moff = torch.empty(n + 1, dtype=torch.int64, device=codec.device)
@@ -174,22 +174,11 @@ def main():
     ok = bool((pst == 0).all().item() and (ust == 0).all().item() and torch.equal(woff, off)
               and torch.equal(back, words[:total]))
 
-    tot = torch.tensor([dt, float(U), float(P), pack_ms / max(pl, 1), unpack_ms / max(ul, 1)],
-                       dtype=torch.float64, device=codec.device)
-    oks = torch.tensor([1 if ok else 0], dtype=torch.int64, device=codec.device)
-    if dist is not None:
-        tmax = tot.clone()
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        tsum = tot.clone()
-        dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
-        dist.all_reduce(oks, op=dist.ReduceOp.MIN)
-        dt_max = float(tmax[0])
-        U_all, P_all = float(tsum[1]), float(tsum[2])
-        pk_avg, up_avg = float(tmax[3]), float(tmax[4])
-    else:
-        dt_max, U_all, P_all = dt, float(U), float(P)
-        pk_avg, up_avg = float(tot[3]), float(tot[4])
-    ok_all = bool(oks.item())
+    red = reduce_step(dt, float(U), float(P), pack_ms / max(pl, 1), unpack_ms / max(ul, 1), ok,
+                      dist=dist, device=codec.device)
+    dt_max, U_all = red["dt_max"], red["unpacked_all"]
+    pk_avg, up_avg = red["pack_ms"], red["unpack_ms"]
+    ok_all = red["ok_all"]
 
     result = None
     if rank == 0:

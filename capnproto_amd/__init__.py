@@ -77,8 +77,8 @@ def load_library():
         "cpk_unpack_chunks": (C.c_int, [vp, vp, u64, vp, vp, u64, vp, u64, vp, vp]),
         "cpk_pack_messages_host": (C.c_int, [vp, vp, u64, vp, u64, vp, u64, vp, vp]),
         "cpk_unpack_messages_host": (C.c_int, [vp, vp, u64, vp, u64, vp, u64, vp, vp, vp]),
-        "cpk_gen_messages": (C.c_int, [vp, C.c_int, u64, u64, u64, u32, vp, vp, vp]),
-        "cpk_gen_offsets": (C.c_int, [vp, u64, u64, u64, u32, u64, vp, C.POINTER(u64), vp]),
+        "cpk_gen_messages": (C.c_int, [vp, C.c_int, u64, u64, u64, u64, u32, vp, vp, vp]),
+        "cpk_gen_offsets": (C.c_int, [vp, u64, u64, u64, u64, u32, u64, vp, C.POINTER(u64), vp]),
         "cpk_timing_enable": (C.c_int, [vp, C.c_int]),
         "cpk_timing_read": (C.c_int, [vp, C.POINTER(C.c_double), C.POINTER(u64),
                                       C.POINTER(C.c_double), C.POINTER(u64)]),
@@ -240,23 +240,25 @@ class Codec:
         return pm.value, pl.value, um.value, ul.value
 
     # ------------------------------------------------------------------ synthetic workloads
-    def gen_offsets(self, nmsgs, nseg=1, seg_words=0, seed=0, first_msg=0, stream=None):
+    def gen_offsets(self, nmsgs, nseg=1, seg_words=0, seed=0, first_msg=0, msg_stride=1,
+                    stream=None):
         off = self.torch.empty(nmsgs + 1, dtype=self.torch.int64, device=self.device)
         total = C.c_uint64(0)
-        self._check(self.lib.cpk_gen_offsets(self.ctx, seed, first_msg, nmsgs, nseg, seg_words,
+        self._check(self.lib.cpk_gen_offsets(self.ctx, seed, first_msg, msg_stride, nmsgs, nseg,
+                                             seg_words,
                                              _ptr(off), C.byref(total), self._stream(stream)),
                     "cpk_gen_offsets")
         return off, int(total.value)
 
     def gen_messages(self, profile, msg_word_off, total_words, nseg=1, seed=0, first_msg=0,
-                     words=None, stream=None):
+                     msg_stride=1, words=None, stream=None):
         if isinstance(profile, str):
             profile = PROFILES[profile]
         n = msg_word_off.numel() - 1
         if words is None:
             words = self.torch.empty(max(total_words, 1), dtype=self.torch.int64,
                                      device=self.device)
-        self._check(self.lib.cpk_gen_messages(self.ctx, profile, seed, first_msg, n, nseg,
+        self._check(self.lib.cpk_gen_messages(self.ctx, profile, seed, first_msg, msg_stride, n, nseg,
                                               _ptr(msg_word_off), _ptr(words),
                                               self._stream(stream)), "cpk_gen_messages")
         return words

@@ -557,16 +557,16 @@ cpk_status cpk_timing_read(cpk_ctx* ctx, double* pack_ms, uint64_t* pack_launche
 }
 
 cpk_status cpk_gen_messages(cpk_ctx* ctx, int profile, uint64_t seed, uint64_t first_msg,
-                            uint64_t nmsgs, uint32_t nseg, const uint64_t* d_msg_word_off,
-                            uint64_t* d_words, void* stream) {
+                            uint64_t msg_stride, uint64_t nmsgs, uint32_t nseg,
+                            const uint64_t* d_msg_word_off, uint64_t* d_words, void* stream) {
   if (!ctx || profile < 0 || profile > 3 || nseg == 0) return CPK_ERR_INVALID_ARGUMENT;
   if (hipSetDevice(ctx->device) != hipSuccess) return CPK_ERR_HIP;
-  return hip_status(cpk::launch_gen(profile, seed, first_msg, nmsgs, nseg, d_msg_word_off,
+  return hip_status(cpk::launch_gen(profile, seed, first_msg, msg_stride ? msg_stride : 1, nmsgs, nseg, d_msg_word_off,
                                     d_words, (hipStream_t)stream));
 }
 
-cpk_status cpk_gen_offsets(cpk_ctx* ctx, uint64_t seed, uint64_t first_msg, uint64_t nmsgs,
-                           uint32_t nseg, uint64_t seg_words, uint64_t* d_msg_word_off,
+cpk_status cpk_gen_offsets(cpk_ctx* ctx, uint64_t seed, uint64_t first_msg,
+                           uint64_t msg_stride, uint64_t nmsgs, uint32_t nseg, uint64_t seg_words, uint64_t* d_msg_word_off,
                            uint64_t* total_words_out, void* stream) {
   if (!ctx || nseg == 0 || (seg_words == 0 && nseg != 1)) return CPK_ERR_INVALID_ARGUMENT;
   if (hipSetDevice(ctx->device) != hipSuccess) return CPK_ERR_HIP;
@@ -581,7 +581,7 @@ cpk_status cpk_gen_offsets(cpk_ctx* ctx, uint64_t seed, uint64_t first_msg, uint
   const size_t zero = c.off;
   uint64_t* sizes = c.take<uint64_t>(nmsgs + 1);
   if (hipMemsetAsync(ctx->scratch, 0, zero, s) != hipSuccess) return CPK_ERR_HIP;
-  if (cpk::launch_gen_sizes(seed, first_msg, nmsgs, nseg, seg_words, sizes, s) != hipSuccess)
+  if (cpk::launch_gen_sizes(seed, first_msg, msg_stride ? msg_stride : 1, nmsgs, nseg, seg_words, sizes, s) != hipSuccess)
     return CPK_ERR_HIP;
   if (cpk::launch_exclusive_scan(sizes, nmsgs, d_msg_word_off, counter, desc, ctx->err, s) !=
       hipSuccess)

@@ -69,32 +69,41 @@ __device__ __forceinline__ uint32_t wave_excl_sum_small(uint32_t v, uint32_t* to
   return mbcnt64(b0) + 2 * mbcnt64(b1) + 4 * mbcnt64(b2) + 8 * mbcnt64(b3);
 }
 
-// Inclusive wave scans (Hillis-Steele over ds_bpermute / DPP-free; 6 steps).
-__device__ __forceinline__ uint32_t wave_incl_sum32(uint32_t v) {
-  const int l = lane_id();
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    uint32_t o = shfl32(v, l >= d ? l - d : l);
-    if (l >= d) v += o;
-  }
+// Inclusive wave scans by DPP: row_shr 1/2/4/8 inside each 16-lane row, then row_bcast:15 and
+// row_bcast:31 carry row totals upward.  Lanes whose DPP source does not exist read 0 (the
+// identity of every scan below: sums and unsigned max).
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint32_t dpp_src(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWS, 0xf, true);
+}
+template <class Op>
+__device__ __forceinline__ uint32_t wave_scan32(uint32_t v, Op op) {
+  v = op(v, dpp_src<0x111, 0xf>(v));
+  v = op(v, dpp_src<0x112, 0xf>(v));
+  v = op(v, dpp_src<0x114, 0xf>(v));
+  v = op(v, dpp_src<0x118, 0xf>(v));
+  v = op(v, dpp_src<0x142, 0xa>(v));
+  v = op(v, dpp_src<0x143, 0xc>(v));
   return v;
 }
-__device__ __forceinline__ uint64_t wave_incl_sum64(uint64_t v) {
-  const int l = lane_id();
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    uint64_t o = shfl64(v, l >= d ? l - d : l);
-    if (l >= d) v += o;
-  }
-  return v;
+__device__ __forceinline__ uint32_t wave_incl_sum32(uint32_t v) {
+  return wave_scan32(v, [](uint32_t a, uint32_t b) { return a + b; });
 }
 __device__ __forceinline__ uint32_t wave_incl_max32(uint32_t v) {
-  const int l = lane_id();
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    uint32_t o = shfl32(v, l >= d ? l - d : l);
-    if (l >= d) v = v > o ? v : o;
-  }
+  return wave_scan32(v, [](uint32_t a, uint32_t b) { return a > b ? a : b; });
+}
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint64_t dpp_src64(uint64_t v) {
+  return ((uint64_t)dpp_src<CTRL, ROWS>((uint32_t)(v >> 32)) << 32) |
+         dpp_src<CTRL, ROWS>((uint32_t)v);
+}
+__device__ __forceinline__ uint64_t wave_incl_sum64(uint64_t v) {
+  v += dpp_src64<0x111, 0xf>(v);
+  v += dpp_src64<0x112, 0xf>(v);
+  v += dpp_src64<0x114, 0xf>(v);
+  v += dpp_src64<0x118, 0xf>(v);
+  v += dpp_src64<0x142, 0xa>(v);
+  v += dpp_src64<0x143, 0xc>(v);
   return v;
 }
 __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {

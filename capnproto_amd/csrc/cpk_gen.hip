@@ -50,7 +50,7 @@ namespace {
 
 // One wave per message: table words, then the segment words (coalesced stores).
 __global__ __launch_bounds__(256) void gen_kernel(int profile, uint64_t seed, uint64_t first_msg,
-                                                  uint64_t nmsgs, uint32_t nseg,
+                                                  uint64_t stride, uint64_t nmsgs, uint32_t nseg,
                                                   const uint64_t* __restrict__ off,
                                                   uint64_t* __restrict__ words) {
   const uint64_t m = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -74,11 +74,12 @@ __global__ __launch_bounds__(256) void gen_kernel(int profile, uint64_t seed, ui
     words[w0 + i] = ((uint64_t)hi << 32) | lo;
   }
   for (uint64_t i = l; i < body; i += 64)
-    words[w0 + tw + i] = gen_word(profile, seed, first_msg + m, i);
+    words[w0 + tw + i] = gen_word(profile, seed, first_msg + m * stride, i);
 }
 
 // Offsets: fixed nseg x seg_words, or (seg_words == 0) one segment of 2^k words, k in [3, 11].
-__global__ void gen_sizes_kernel(uint64_t seed, uint64_t first_msg, uint64_t nmsgs, uint32_t nseg,
+__global__ void gen_sizes_kernel(uint64_t seed, uint64_t first_msg, uint64_t stride, uint64_t nmsgs,
+                                 uint32_t nseg,
                                  uint64_t seg_words, uint64_t* __restrict__ sizes) {
   const uint64_t m = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= nmsgs) return;
@@ -86,27 +87,29 @@ __global__ void gen_sizes_kernel(uint64_t seed, uint64_t first_msg, uint64_t nms
   if (seg_words) {
     sizes[m] = tw + (uint64_t)nseg * seg_words;
   } else {
-    const uint64_t k = 3 + splitmix64(seed ^ ((first_msg + m) * 0x94D049BB133111EBull)) % 9;
+    const uint64_t k = 3 + splitmix64(seed ^ ((first_msg + m * stride) * 0x94D049BB133111EBull)) % 9;
     sizes[m] = tw + (1ull << k);
   }
 }
 
 }  // namespace
 
-hipError_t launch_gen(int profile, uint64_t seed, uint64_t first_msg, uint64_t nmsgs,
+hipError_t launch_gen(int profile, uint64_t seed, uint64_t first_msg, uint64_t stride,
+                      uint64_t nmsgs,
                       uint32_t nseg, const uint64_t* off, uint64_t* words, hipStream_t stream) {
   if (nmsgs == 0) return hipSuccess;
   const uint64_t threads = nmsgs * 64;
   hipLaunchKernelGGL(gen_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, stream,
-                     profile, seed, first_msg, nmsgs, nseg, off, words);
+                     profile, seed, first_msg, stride, nmsgs, nseg, off, words);
   return hipGetLastError();
 }
 
-hipError_t launch_gen_sizes(uint64_t seed, uint64_t first_msg, uint64_t nmsgs, uint32_t nseg,
+hipError_t launch_gen_sizes(uint64_t seed, uint64_t first_msg, uint64_t stride, uint64_t nmsgs,
+                            uint32_t nseg,
                             uint64_t seg_words, uint64_t* sizes, hipStream_t stream) {
   if (nmsgs == 0) return hipSuccess;
   hipLaunchKernelGGL(gen_sizes_kernel, dim3((unsigned)((nmsgs + 255) / 256)), dim3(256), 0,
-                     stream, seed, first_msg, nmsgs, nseg, seg_words, sizes);
+                     stream, seed, first_msg, stride, nmsgs, nseg, seg_words, sizes);
   return hipGetLastError();
 }
 

@@ -7,7 +7,7 @@
 
 namespace cpk {
 
-constexpr int kPackSteps = 16;                  // words per pack tile = 64 * kPackSteps
+constexpr int kPackSteps = 8;                   // words per pack tile = 64 * kPackSteps
 constexpr uint64_t kPackTileWords = 64 * kPackSteps;
 constexpr uint64_t kUnpackTileBytes = 4096;     // packed bytes per unpack tile (>= 2050)
 
@@ -83,9 +83,11 @@ hipError_t launch_unpack_body(const UnpackArgs& a, hipStream_t stream);
 hipError_t launch_unpack_init(uint32_t mode, const uint64_t* in_off, const uint64_t* word_off,
                               uint64_t n, int32_t* status, uint64_t* size_out, hipStream_t stream);
 
-hipError_t launch_gen(int profile, uint64_t seed, uint64_t first_msg, uint64_t nmsgs,
+hipError_t launch_gen(int profile, uint64_t seed, uint64_t first_msg, uint64_t stride,
+                      uint64_t nmsgs,
                       uint32_t nseg, const uint64_t* off, uint64_t* words, hipStream_t stream);
-hipError_t launch_gen_sizes(uint64_t seed, uint64_t first_msg, uint64_t nmsgs, uint32_t nseg,
+hipError_t launch_gen_sizes(uint64_t seed, uint64_t first_msg, uint64_t stride, uint64_t nmsgs,
+                            uint32_t nseg,
                             uint64_t seg_words, uint64_t* sizes, hipStream_t stream);
 
 uint64_t scan_tiles(uint64_t n);

@@ -20,15 +20,11 @@
 // words shifted by one.  The only state crossing steps is one byte: the budget of the run that
 // is open at the step's last word.
 //
-// Work decomposition: the batch of words is cut into tiles of 64*S words, one wave per tile
-// (tile ids from an atomic counter, so every predecessor of a running tile is resident).  The
-// wave classifies its words (pass 1), publishes the budget its tile hands to the successor when
-// that does not depend on its own entry, takes its entry budget from the predecessor only when
-// word 0 continues a stretch, then encodes every step once into a per-wave LDS staging buffer
-// (pass 2, tile-relative byte offsets).  The tile's byte count feeds a single-pass decoupled
-// look-back; with the global offset known the staged bytes leave as 16-byte aligned stores
-// (realigned with v_alignbyte), only the <= 15-byte partial blocks at tile edges as byte stores.
+// Work decomposition: the batch of words is cut into tiles of 64*S words, one wave per tile,
+// persistent waves over a static strided tile order (pack_tiles_kernel below).
 #include <stdlib.h>
+
+#include <type_traits>
 
 #include "cpk_device.h"
 #include "cpk_kernels.h"
@@ -39,90 +35,108 @@ namespace {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-// Lane's bit of a wave-uniform 64-bit mask held in an SGPR pair: one v_cndmask.
-__device__ __forceinline__ uint32_t lanebit(uint64_t mask) {
+// v_writelane: lane `s` (compile-time) of `dst` takes the wave-uniform value `v`.
+template <int L>
+__device__ __forceinline__ uint32_t setlane(uint32_t dst, uint32_t v) {
+  asm("v_writelane_b32 %0, %1, %2" : "+v"(dst) : "s"(v), "i"(L));
+  return dst;
+}
+
+// Compile-time loop: f(std::integral_constant<int, I>) for I in [B, E).
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
+// Tag byte of a word (bit i <=> byte i non-zero), SWAR on the two dwords.
+__device__ __forceinline__ uint32_t tag_of(uint32_t lo, uint32_t hi) {
+  const uint32_t m7 = 0x7f7f7f7fu;
+  const uint32_t a = ((lo & m7) + m7) | lo;  // bit 7 of a byte <=> byte non-zero
+  const uint32_t b = ((hi & m7) + m7) | hi;
+  const uint32_t c = ((a >> 7) & 0x01010101u) | ((b >> 3) & 0x10101010u);  // bits 8k, 8k+4
+  const uint32_t d = c | (c >> 14);
+  return (d | (d >> 7)) & 0xffu;
+}
+
+// Per-lane select by a wave-uniform 64-bit mask held in SGPRs: one v_cndmask.
+__device__ __forceinline__ uint32_t msel(uint64_t mask, uint32_t if_set, uint32_t if_clear) {
   uint32_t r;
-  asm("v_cndmask_b32 %0, 0, 1, %1" : "=v"(r) : "s"(mask));
+  asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(r) : "v"(if_clear), "v"(if_set), "s"(mask));
   return r;
 }
 
-// v_perm selector compacting the set-bit bytes of nibble n to the low end (0x0c = zero byte).
-__device__ __forceinline__ uint32_t compact_sel(uint32_t n) {
-  uint32_t sel = 0x0c0c0c0cu, j = 0;
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    if ((n >> i) & 1) {
-      sel = (sel & ~(0xffu << (8 * j))) | ((uint32_t)i << (8 * j));
+// Index of the lowest set bit, ~0u for 0 (v_ffbl_b32).
+__device__ __forceinline__ uint32_t ffbl32(uint32_t v) {
+  uint32_t r;
+  asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(v));
+  return r;
+}
+
+// v_perm selectors placing the non-zero bytes of a word with tag `tag` after a zero byte 0:
+// dword 0 = [0, c0, c1, c2], dword 1 = [c3 .. c6] (c7 only exists for tag 0xff).
+__device__ __forceinline__ uint64_t make_sel(uint32_t tag) {
+  uint64_t sel = 0x0c0c0c0c0c0c0c0cull;
+  int j = 1;
+  for (int i = 0; i < 8; i++) {
+    if ((tag >> i) & 1) {
+      if (j < 8) sel = (sel & ~(0xffull << (8 * j))) | ((uint64_t)i << (8 * j));
       j++;
     }
   }
   return sel;
 }
 
-struct Classes {
-  uint64_t Z, F, R, SY, V;
-};
-
-// Class masks + sync mask of one 64-word step (lane = word).  zc/rc: the word before the step
-// is a valid Z / R word of the same chunk-run (chunk starts are part of C).
-__device__ __forceinline__ Classes classify_step(uint64_t x, uint32_t tag, bool valid, uint64_t C,
-                                                 uint64_t zc, uint64_t rc) {
-  const uint32_t nz = __popc(tag);
-  Classes k;
-  k.Z = ballot(valid && x == 0);
-  k.F = ballot(valid && tag == 0xff);
-  k.R = ballot(valid && nz >= 7);
-  const uint64_t V = ballot(valid);
-  k.V = V;
-  const uint64_t O = V & ~k.Z & ~k.R;
-  const uint64_t prevZ = (k.Z << 1) | zc;
-  const uint64_t prevR = (k.R << 1) | rc;
-  k.SY = C | O | (k.Z & ~prevZ) | (k.R & ~prevR) | ~V;
-  return k;
-}
-
 // Head / coverage resolution of one step, entry budget b (words the run open before the step
 // may still cover).  All wave-uniform mask arithmetic.
 struct StepRes {
   uint64_t covered, runheads;  // covered words; Z heads | F heads
+  uint64_t Zheads, Fheads;
   int b_out;                   // budget leaving the step
 };
 
-__device__ __forceinline__ StepRes resolve_step(const Classes& k, int b, bool last_valid) {
-  const uint64_t SY = k.SY, U = ~SY;
-  const int L0 = lowest_bit(SY);  // 64 if no sync in the step
-  const bool leadZ = L0 > 0 && (k.Z & 1);
-  const bool leadR = L0 > 0 && (k.R & 1);
-  const int cb = b < L0 ? b : L0;  // words of the lead covered by the entering run
-  const uint64_t lead_cov = cb >= 64 ? ~0ull : mask_lt(cb);
-  const uint64_t zlead = (leadZ && b < L0) ? (1ull << b) : 0;
-  const uint64_t Feff = leadR ? (k.F & ~lead_cov) : k.F;
-  const uint64_t G = (Feff << 1) & U;
-  const uint64_t fill = (((U + G) ^ U) & U) | G;  // words after an F head, same segment
-  const uint64_t Rcov = k.R & (fill | (leadR ? lead_cov : 0));
+__device__ __forceinline__ StepRes resolve_step(uint64_t Z, uint64_t F, uint64_t R, uint64_t SY,
+                                                int b, bool last_valid) {
+  const uint64_t LM = ~SY & (SY - 1);                     // lead: words before the first sync
+  const uint64_t BM = b >= 64 ? ~0ull : mask_lt(b);       // words the entering run covers
+  const uint64_t lead_cov = BM & LM;
+  const uint64_t zlead = (BM + 1) & LM & Z;               // Z lead: next head at word b
+  const uint64_t Feff = F & ~lead_cov;
+  const uint64_t G = (Feff << 1) & ~SY;
+  const uint64_t fill = (((~SY + G) ^ ~SY) & ~SY) | G;    // words after an F head, same segment
   const uint64_t Fheads = Feff & ~fill;
-  const uint64_t Zheads = (k.Z & SY) | zlead;
+  const uint64_t Zheads = (Z & SY) | zlead;
   StepRes r;
-  r.covered = Rcov | (k.Z & ~Zheads);
+  r.covered = (R & (fill | lead_cov)) | (Z & ~Zheads);
   r.runheads = Zheads | Fheads;
+  r.Zheads = Zheads;
+  r.Fheads = Fheads;
+  // budget for the next step: the last run head of the last segment, or the entering run when
+  // the whole step is its lead; a last word of class O ends with a sync and a zero budget
   r.b_out = 0;
-  if (last_valid && (((k.Z | k.R) >> 63) & 1)) {
-    const int st63 = highest_bit(SY);
-    const int h = highest_bit(r.runheads);
-    if (h >= 0 && h >= st63) r.b_out = 255 - (63 - h);
-    else if (st63 < 0 && b > 63) r.b_out = b - 64;
+  if (last_valid) {
+    const int st = highest_bit(SY);         // -1: no sync
+    const int h = highest_bit(r.runheads);  // -1: no head
+    if (h >= 0 && h >= st) r.b_out = 192 + h;
+    else if (SY == 0 && b > 63) r.b_out = b - 64;
   }
   return r;
 }
 
-// Words a tile needs, loaded one tile ahead (persistent loop prefetch).
+// Valid-lane mask of step s of a tile with n valid words.
+__device__ __forceinline__ uint64_t valid_mask(int n, int s) {
+  const int k = n - 64 * s;
+  return k >= 64 ? ~0ull : (k <= 0 ? 0ull : mask_lt(k));
+}
+
 template <int S>
 struct TileLoad {
   uint64_t x[S];  // word 64*s + lane
-  uint64_t cb;    // chunk-start bits of step `lane` (lanes < S)
-  uint64_t pw;    // word before the tile
-  uint64_t nx;    // first step of the next tile (look-ahead for run counts)
-  uint64_t ncb;   // its chunk-start bits
+  uint64_t nx;    // word tend + lane (look-ahead)
+  uint64_t cb;    // lanes < S: chunk-start bits of step `lane`; lane S: those of the next step
+  uint64_t pw;    // word before the tile (0 for tile 0)
 };
 
 template <int S>
@@ -130,7 +144,6 @@ __device__ __forceinline__ void load_tile(const PackTileArgs& a, uint64_t t, Til
   constexpr int T = 64 * S;
   const int l = lane_id();
   const uint64_t N = a.nwords;
-  const uint64_t nbitw = (N + 63) >> 6;
   const uint64_t tbase = t * T;
   const uint64_t tend = tbase + T < N ? tbase + T : N;
 #pragma unroll
@@ -138,321 +151,311 @@ __device__ __forceinline__ void load_tile(const PackTileArgs& a, uint64_t t, Til
     const uint64_t g = tbase + 64 * s + l;
     L.x[s] = g < N ? a.words[g] : 0;
   }
-  L.cb = (l < S && (tbase >> 6) + l < nbitw) ? a.chunk_bits[(tbase >> 6) + l] : 0;
-  L.pw = tbase > 0 ? a.words[tbase - 1] : 0;
   L.nx = tend + l < N ? a.words[tend + l] : 0;
-  L.ncb = (tend >> 6) < nbitw ? a.chunk_bits[tend >> 6] : 0;
+  const uint64_t nbitw = (N + 63) >> 6;
+  L.cb = (l <= S && (tbase >> 6) + l < nbitw) ? a.chunk_bits[(tbase >> 6) + l] : 0;
+  L.pw = tbase > 0 ? a.words[tbase - 1] : 0;
 }
 
-template <int S, bool STAMPS>
+// One wave per tile of 64*S words, persistent waves over a static strided tile order.
+//   pass A   classes + sync masks of every step (wave-uniform SGPR masks), packed tags;
+//            the tile's exit budget is published at once when it does not depend on the entry
+//   entry    the predecessor's exit budget, only when word 0 continues a stretch
+//   pass B   per step: resolve heads / coverage (scalar), record lengths, DPP prefix sum,
+//            v_perm compaction through a 256-entry selector table, records OR-ed into the
+//            wave's LDS staging area at tile-relative byte offsets
+//   look-back  two-level decoupled look-back on the tile's byte count
+//   flush    staged bytes -> global: 16-byte aligned stores (realigned by v_alignbyte), byte
+//            stores for the partial blocks at both ends; the staging area is re-zeroed.
+template <int S, bool PF, bool STAMPS>
 __global__ __launch_bounds__(256) void pack_tiles_kernel(PackTileArgs a) {
-  static_assert(S >= 1 && S <= 32, "S steps per tile");
+  static_assert(S >= 2 && S <= 16 && (S % 2) == 0, "S steps per tile");
   constexpr int T = 64 * S;
-  constexpr int kRing = 1024;  // per-wave output ring (one step emits <= 640 bytes)
-  __shared__ __attribute__((aligned(16))) uint8_t lds_ring[4][kRing];
+  constexpr int kStg = 32 + 640 * S;  // 16 B lead pad + <= 640 B per step + 16 B tail pad
+  __shared__ __attribute__((aligned(16))) uint8_t stg_all[4][kStg];
+  __shared__ uint64_t sel_tab[256];
 
   const int l = lane_id();
-  const int wv = (int)uniform32(threadIdx.x >> 6);  // wave-uniform (keeps tile math scalar)
-  uint8_t* ring = lds_ring[wv];
-  *(u32x4*)(ring + 16 * l) = (u32x4){0, 0, 0, 0};
-  const uint32_t csel = compact_sel((uint32_t)l & 15);
+  const int wv = (int)uniform32(threadIdx.x >> 6);
+  uint8_t* const stg = stg_all[wv];
+  uint32_t* const stg32 = (uint32_t*)stg;
+  sel_tab[threadIdx.x] = make_sel(threadIdx.x);
+  for (int i = l; i < kStg / 16; i += 64) ((u32x4*)stg)[i] = (u32x4){0, 0, 0, 0};
+  __syncthreads();
+
   const uint64_t gt_mask = ~mask_le(l);  // lanes above this one
+  const uint32_t gt_lo = (uint32_t)gt_mask, gt_hi = (uint32_t)(gt_mask >> 32);
+  const uint32_t lp1 = (uint32_t)l + 1u;
   const uint64_t N = a.nwords;
   const uint64_t nbitw = (N + 63) >> 6;
-  const uint64_t base_addr = (uint64_t)(uintptr_t)a.out;
   uint32_t* const state = a.state;
-
-  // Persistent waves, static strided tile order (grid <= guaranteed residency, see launch):
-  // a tile only waits on lower tiles, which belong to resident waves that reach them first.
   const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
   Stamps<STAMPS> stm;
   uint64_t t = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wv;
   TileLoad<S> cur;
   if (t < a.ntiles) load_tile<S>(a, t, cur);
   for (; t < a.ntiles; t += nwaves) {
+    TileLoad<S> nxt;
+    auto tile = [&](auto full_c) {
+    constexpr bool FULL = decltype(full_c)::value;
     stm.start(a.stamps);
     const uint64_t tbase = t * T;
     const uint64_t tend = tbase + T < N ? tbase + T : N;
-    const int nvalid = (int)(tend - tbase);
+    const int nvalid = FULL ? T : (int)(tend - tbase);
     const int last = nvalid - 1;
-    const int nsteps = (nvalid + 63) >> 6;
     uint64_t zc = 0, rc = 0;
     if (tbase > 0) {
-      zc = cur.pw == 0;
-      rc = __popc(word_tag(cur.pw)) >= 7;
+      const uint64_t pw = uniform64(cur.pw);
+      zc = pw == 0;
+      rc = __popc(tag_of((uint32_t)pw, (uint32_t)(pw >> 32))) >= 7;
     }
 
-    // ---- pass 1: classes (lane s keeps step s's masks) and O-word bytes ----------------------
-    uint64_t myZ = 0, myF = 0, myR = 0, mySY = 0;
-    uint32_t myOB = 0;
-    int first_sync = T;
-    {
-      uint64_t czc = zc, crc = rc;
-#pragma unroll
-      for (int s = 0; s < S; s++) {
-        const bool valid = 64 * s + l < nvalid;
-        const uint32_t tag = word_tag(cur.x[s]);
-        const Classes k = classify_step(cur.x[s], tag, valid, readlane64(cur.cb, s), czc, crc);
-        czc = k.Z >> 63;
-        crc = k.R >> 63;
-        const uint64_t syv = k.SY & k.V;
-        if (first_sync == T && syv) first_sync = 64 * s + lowest_bit(syv);
-        // bytes of O words (always heads, state independent): 1 + nz <= 7
-        const uint32_t nz = __popc(tag);
-        const uint32_t ob = (valid && cur.x[s] != 0 && nz < 7) ? 1 + nz : 0;
-        const uint32_t OB = (uint32_t)(__popcll(ballot(ob & 1)) + 2 * __popcll(ballot(ob & 2)) +
-                                       4 * __popcll(ballot(ob & 4)));
-        if (l == s) {
-          myZ = k.Z;
-          myF = k.F;
-          myR = k.R;
-          mySY = k.SY;
-          myOB = OB;
-        }
+    // ---- pass A --------------------------------------------------------------------------
+    // per-step masks parked in VGPR lanes (lane s = step s) to keep SGPR pressure low
+    uint32_t vSYlo = 0, vSYhi = 0, vFlo = 0, vFhi = 0, vNsa = 0;
+    uint32_t tagpk[S / 2];
+    bool lastZ = false, lastR = false;
+    int first_sync = T, sg = -1;
+    static_for<0, S>([&](auto sc) {
+      constexpr int s = decltype(sc)::value;
+      const uint64_t x = cur.x[s];
+      const uint32_t tag = tag_of((uint32_t)x, (uint32_t)(x >> 32));
+      if (s & 1) {
+        tagpk[s >> 1] |= tag << 16;
+        asm volatile("" : "+v"(tagpk[s >> 1]));  // keep the packed form (VGPR pressure)
+      } else {
+        tagpk[s >> 1] = tag;
       }
-    }
-    stm.mark(0);  // pass 1
+      const uint64_t V = valid_mask(nvalid, s);
+      const uint64_t C = readlane64(cur.cb, s);
+      const uint64_t Z = ballot(x == 0) & V;
+      const uint64_t R = ballot(__popc(tag) >= 7) & V;
+      const uint64_t Fs = ballot(tag == 0xff) & V;
+      const uint64_t O = V & ~Z & ~R;
+      const uint64_t SY = C | O | (Z & ~((Z << 1) | zc)) | (R & ~((R << 1) | rc)) | ~V;
+      vSYlo = setlane<s>(vSYlo, (int)(uint32_t)SY);
+      vSYhi = setlane<s>(vSYhi, (int)(uint32_t)(SY >> 32));
+      vFlo = setlane<s>(vFlo, (int)(uint32_t)Fs);
+      vFhi = setlane<s>(vFhi, (int)(uint32_t)(Fs >> 32));
+      const uint64_t m = SY & V;
+      if (m) {
+        if (first_sync == T) first_sync = 64 * s + lowest_bit(m);
+        sg = 64 * s + highest_bit(m);
+      }
+      zc = Z >> 63;
+      rc = R >> 63;
+      if (s == (last >> 6)) {
+        lastZ = (Z >> (last & 63)) & 1;
+        lastR = (R >> (last & 63)) & 1;
+      }
+    });
+    stm.mark(0);
 
-    // ---- look-ahead: first sync after the tile (run counts need <= 255 words) -----------------
+    // ---- look-ahead: distance from tend to the first sync at / after it (<= 256) ------------
     int la = 0;
-    {
-      const bool lastZ = (readlane64(myZ, last >> 6) >> (last & 63)) & 1;
-      const bool lastR = (readlane64(myR, last >> 6) >> (last & 63)) & 1;
-      if ((lastZ || lastR) && tend < N) {
-        uint64_t czc = lastZ, crc = lastR;
-        la = 256;
-        for (int k = 0; k < 4; k++) {
-          const uint64_t g = tend + 64 * k + l;
-          const bool valid = g < N;
-          uint64_t xx, C;
-          if (k == 0) {
-            xx = cur.nx;
-            C = cur.ncb;
-          } else {
-            xx = valid ? a.words[g] : 0;
-            C = ((tend >> 6) + k < nbitw) ? a.chunk_bits[(tend >> 6) + k] : 0;
-          }
-          const Classes kk = classify_step(xx, word_tag(xx), valid, C, czc, crc);
-          czc = kk.Z >> 63;
-          crc = kk.R >> 63;
-          if (kk.SY) {
-            la = 64 * k + lowest_bit(kk.SY);
-            break;
-          }
-        }
-      }
-    }
-    int myNsa = 0;  // lane s: distance from step s+1 to the first sync at or after it (<= 256)
-    {
-      int v = la;
-      for (int s = S - 1; s >= 0; s--) {
-        if (l == s) myNsa = v;
-        const int fs = lowest_bit(readlane64(mySY, s));
-        v = s >= nsteps ? la : (fs < 64 ? fs : (v + 64 < 256 ? v + 64 : 256));
-      }
-    }
-
-    // ---- exit budget, published early when it does not depend on our own entry --------------
-    auto first_F_from = [&](int xpos) -> int {
-      for (int k = xpos >> 6; k < nsteps; k++) {
-        uint64_t m = readlane64(myF, k);
-        if (k == (xpos >> 6)) m &= ~mask_lt(xpos & 63);
-        if (m) return 64 * k + lowest_bit(m);
-      }
-      return 1 << 20;
-    };
-    if (first_sync < T) {
-      int sg = -1;
-      for (int k = last >> 6; k >= 0; k--) {
-        uint64_t m = readlane64(mySY, k);
-        if (k == (last >> 6)) m &= mask_le(last & 63);
-        if (m) {
-          sg = 64 * k + highest_bit(m);
+    if ((lastZ || lastR) && tend < N) {
+      uint64_t czc = lastZ, crc = lastR;
+      la = 256;
+      for (int k = 0; k < 4; k++) {
+        const uint64_t g = tend + 64 * k + l;
+        const uint64_t xx = k == 0 ? cur.nx : (g < N ? a.words[g] : 0);
+        const uint32_t tg = tag_of((uint32_t)xx, (uint32_t)(xx >> 32));
+        const uint64_t V = ballot(g < N);
+        const uint64_t C = k == 0 ? readlane64(cur.cb, S)
+                                  : (((tend >> 6) + k < nbitw) ? a.chunk_bits[(tend >> 6) + k] : 0);
+        const uint64_t Z = ballot(xx == 0) & V;
+        const uint64_t R = ballot(__popc(tg) >= 7) & V;
+        const uint64_t O = V & ~Z & ~R;
+        const uint64_t SY = C | O | (Z & ~((Z << 1) | czc)) | (R & ~((R << 1) | crc)) | ~V;
+        if (SY) {
+          la = 64 * k + lowest_bit(SY);
           break;
         }
+        czc = Z >> 63;
+        crc = R >> 63;
       }
-      const bool sZ = (readlane64(myZ, sg >> 6) >> (sg & 63)) & 1;
-      const bool sR = (readlane64(myR, sg >> 6) >> (sg & 63)) & 1;
+    }
+    // lane s: distance from step s+1's first word to the first sync at / after it
+    {
+      int v = la;
+      static_for<0, S>([&](auto sc) {
+        constexpr int s = S - 1 - decltype(sc)::value;
+        vNsa = setlane<s>(vNsa, v);
+        const int fs = lowest_bit(readlane64(((uint64_t)vSYhi << 32) | vSYlo, s));
+        v = fs < 64 ? fs : (v + 64 < 256 ? v + 64 : 256);
+      });
+    }
+
+    // ---- exit budget, published early when it does not depend on the entry ----------------
+    if (first_sync < T) {
       int eb = 0;
-      if (sZ) {
+      if (lastZ) {
         eb = 255 - ((last - sg) & 255);
-      } else if (sR) {
-        int qq = -1;
-        for (int q = first_F_from(sg); q <= last; q = first_F_from(q + 256)) qq = q;
+      } else if (lastR) {
+        int na = sg, qq = -1;
+#pragma unroll
+        for (int s = 0; s < S; s++) {
+          if (64 * s + 63 >= na && 64 * s <= last) {
+            uint64_t m = readlane64(((uint64_t)vFhi << 32) | vFlo, s);
+            if (na > 64 * s) m &= ~mask_lt(na - 64 * s);
+            if (m) {
+              qq = 64 * s + lowest_bit(m);
+              na = qq + 256;
+            }
+          }
+        }
         eb = (qq >= 0 && last - qq <= 255) ? 255 - (last - qq) : 0;
       }
       if (l == 0) store_agent32(state + t, 0x80000000u | (uint32_t)eb);
     }
-    stm.mark(1);  // look-ahead, run-count table, early exit budget
+
+    // prefetch the next tile (lands during pass B and the look-back)
+    if (PF && t + nwaves < a.ntiles) load_tile<S>(a, t + nwaves, nxt);
+    stm.mark(1);
+
     int b = 0;
     if (first_sync > 0 && t > 0) b = (int)(wait_nonzero32(state + t - 1, a.err) & 0xffu);
-    stm.mark(2);  // entry wait
+    stm.mark(2);
 
-    // ---- count pass (scalar): per-step coverage and byte offsets ------------------------------
-    //   bytes(step) = 8 |R| + 2 |Z heads + F heads| + sum over O words of (1 + nz)
-    uint64_t myCov = 0;
-    uint32_t myOff = 0;
-    uint32_t off = 0;
-    for (int s = 0; s < nsteps; s++) {
-      Classes k;
-      k.Z = readlane64(myZ, s);
-      k.F = readlane64(myF, s);
-      k.R = readlane64(myR, s);
-      k.SY = readlane64(mySY, s);
-      const StepRes r = resolve_step(k, b, 64 * s + 63 < nvalid);
-      const uint32_t bytes = readlane32(myOB, s) + 8 * (uint32_t)__popcll(k.R) +
-                             2 * (uint32_t)__popcll(r.runheads);
-      if (l == s) {
-        myCov = r.covered;
-        myOff = off;
+    // ---- pass B ----------------------------------------------------------------------------
+    uint32_t soff = 0;  // tile-relative byte offset of the step
+    const uint64_t pidx0 = a.pos ? uniform64(a.tile_first[t]) : 0;
+    uint64_t pidx = pidx0;
+    uint32_t prel = ~0u;  // next requested position, tile-relative (~0: none in this tile)
+    if (a.pos && pidx <= a.npos) {
+      const uint64_t pn = uniform64(a.pos[pidx]);
+      if (pn - tbase < (uint64_t)T) prel = (uint32_t)(pn - tbase);
+    }
+#pragma unroll
+    for (int s = 0; s < S; s++) {
+      if (64 * s < nvalid) {
+        uint64_t x = cur.x[s];
+        asm volatile("" : "+v"(x));  // recompute the class ballots here instead of keeping pass A's
+        const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+        const uint32_t tag = (tagpk[s >> 1] >> (16 * (s & 1))) & 0xffu;
+        const uint32_t nz = __popc(tag);
+        const uint64_t V = valid_mask(nvalid, s);
+        const uint64_t Z = ballot(x == 0) & V;
+        const uint64_t R = ballot(nz >= 7) & V;
+        const uint64_t F = readlane64(((uint64_t)vFhi << 32) | vFlo, s);
+        const uint64_t SY = readlane64(((uint64_t)vSYhi << 32) | vSYlo, s);
+        const StepRes r = resolve_step(Z, F, R, SY, b, 64 * s + 63 < nvalid);
+        b = r.b_out;
+        const uint64_t COV = r.covered | ~V;
+        const uint64_t ZH = r.Zheads, FH = r.Fheads;
+        // record length: head 1 + nz (+1 count byte for run heads), covered R 8, covered Z 0
+        const uint32_t n1 = nz + 1;
+        const uint32_t len = msel(COV, n1 & 8u, n1 + msel(r.runheads, 1u, 0u));
+        const uint32_t inc = wave_incl_sum32(len);
+        const uint32_t o = inc - len;
+        const uint32_t tot = readlane32(inc, 63);
+        // run count: stretch words after this one (<= 255); ffbl of 0 is ~0u
+        const uint32_t f_lo = ffbl32((uint32_t)SY & gt_lo);
+        const uint32_t f_hi = __builtin_elementwise_add_sat(
+            ffbl32((uint32_t)(SY >> 32) & gt_hi), 32u);
+        const uint32_t ns = min(min(f_lo, f_hi), 64u + readlane32(vNsa, s));
+        const uint32_t cnt = min(ns - lp1, 255u);
+        // record bytes: [tag, non-zero bytes..., count] for heads, the raw word when covered
+        const uint64_t sel = sel_tab[tag];
+        const uint32_t c8 = cnt << 8;
+        uint32_t w0 = __builtin_amdgcn_perm(hi, lo, (uint32_t)sel) | tag | msel(ZH, c8, 0u);
+        uint32_t w1 = __builtin_amdgcn_perm(hi, lo, (uint32_t)(sel >> 32));
+        const uint32_t w2 = msel(FH, (hi >> 24) | c8, 0u);
+        w0 = msel(COV, lo, w0);
+        w1 = msel(COV, hi, w1);
+        // OR into the staging area at byte 16 + soff + o: four dwords from (at - 1) & ~3
+        const uint32_t at = 16u + soff + o;
+        const uint32_t rr = (0u - at) & 3u;
+        uint32_t* dp = (uint32_t*)(stg + ((at - 1u) & ~3u));
+        atomicOr(dp + 0, __builtin_amdgcn_alignbyte(w0, 0u, rr));
+        atomicOr(dp + 1, __builtin_amdgcn_alignbyte(w1, w0, rr));
+        atomicOr(dp + 2, __builtin_amdgcn_alignbyte(w2, w1, rr));
+        atomicOr(dp + 3, __builtin_amdgcn_alignbyte(0u, w2, rr));
+        // requested positions inside this step: tile-relative offsets (excl added later)
+        if (prel < 64u * s + 64u) {
+          const uint64_t g0 = tbase + 64 * s;
+          while (true) {
+            const uint64_t i = pidx + l;
+            const uint64_t p = i <= a.npos ? a.pos[i] : ~0ull;
+            const bool in = p < g0 + 64;
+            const uint32_t oo = shfl32(o, in ? (int)(p - g0) : 0);
+            if (in) a.pos_out[i] = soff + oo;
+            const uint64_t inm = ballot(in);
+            pidx += __popcll(inm);
+            const uint64_t pn = pidx <= a.npos ? uniform64(a.pos[pidx]) : ~0ull;
+            prel = pn - tbase < (uint64_t)T ? (uint32_t)(pn - tbase) : ~0u;
+            if (inm != ~0ull) break;
+          }
+        }
+        soff += tot;
       }
-      off += bytes;
-      b = r.b_out;
     }
     if (first_sync == T && l == 0) store_agent32(state + t, 0x80000000u | (uint32_t)b);
-    const uint64_t agg = off;
-    stm.mark(3);  // count pass
+    const uint64_t agg = soff;
+    stm.mark(3);
 
-    // ---- publish, prefetch the next tile, look-back ------------------------------------------
+    // ---- look-back -------------------------------------------------------------------------
     uint64_t excl = 0;
     if (a.debug_skip & 1) {
       excl = t * 4096;  // timing ablation: no look-back (output meaningless)
     } else {
       publish_agg(a.desc, a.gdesc, a.gcnt, t, a.ntiles, agg, 0, a.err);
-    }
-    TileLoad<S> nxt;
-    if (t + nwaves < a.ntiles) load_tile<S>(a, t + nwaves, nxt);
-    if (!(a.debug_skip & 1)) {
       excl = lookback2(a.desc, a.gdesc, t, 0, a.err);
       publish_incl(a.desc, a.gdesc, t, a.ntiles, excl + agg);
     }
-    stm.mark(4);  // look-back
+    stm.mark(4);
 
-    // ---- emission: encode each step through the ring, 16-byte aligned stores ----------------
-    const uint64_t A0 = base_addr + excl;
-    const uint64_t A1 = A0 + agg;
+    // ---- flush ----------------------------------------------------------------------------
     const bool over = excl + agg > a.out_capacity;
     if (over && l == 0) raise_error(a.err, kErrCapacity);
-    const uint64_t al = (A0 + 15) & ~15ull;
-    uint64_t flushed = al;  // next full block to store
-    uint64_t hd = A0;       // next head-block byte to store
-    uint64_t pidx = a.pos ? uniform64(a.tile_first[t]) : 0;
-    uint64_t pnext = (a.pos && pidx <= a.npos) ? uniform64(a.pos[pidx]) : ~0ull;
-    for (int s = 0; s < nsteps && !over; s++) {
-      const uint64_t Z = readlane64(myZ, s), F = readlane64(myF, s), R = readlane64(myR, s);
-      const uint64_t SY = readlane64(mySY, s), COV = readlane64(myCov, s);
-      const uint32_t soff = readlane32(myOff, s);
-      const int nsa = (int)readlane32((uint32_t)myNsa, s);
-      uint64_t xv = 0;
-#pragma unroll
-      for (int ss = 0; ss < S; ss++)
-        if (ss == s) xv = cur.x[ss];
-      const uint32_t tag = word_tag(xv);
-      const uint32_t isZ = lanebit(Z), isF = lanebit(F), isR = lanebit(R), cov = lanebit(COV);
-      const bool valid = 64 * s + l < nvalid;
-      // bytes of this word's record
-      const uint32_t hlen = isZ ? 2u : (isF ? 10u : 1u + (uint32_t)__popc(tag));
-      const uint32_t len = !valid ? 0u : (cov ? (isR ? 8u : 0u) : hlen);
-      // run count of Z / F heads: min(255, stretch words left after this one)
-      const uint64_t gt = SY & gt_mask;
-      const int ns = gt ? lowest_bit(gt) : 64 + nsa;
-      const uint32_t cnt = (uint32_t)min(ns - l - 1, 255);
-      // string: slo = bytes 0..7, shi = bytes 8..9 (branch-free selects)
-      const uint32_t xlo = (uint32_t)xv, xhi = (uint32_t)(xv >> 32);
-      const uint32_t tl = tag & 15, th = tag >> 4;
-      const uint32_t clo = __builtin_amdgcn_perm(0u, xlo, shfl32(csel, (int)tl));
-      const uint32_t chi = __builtin_amdgcn_perm(0u, xhi, shfl32(csel, (int)th));
-      const uint64_t comp = (uint64_t)clo | ((uint64_t)chi << (8 * __popc(tl)));
-      const uint64_t s_head = (uint64_t)tag | (comp << 8);
-      const uint64_t s_f = 0xffull | (xv << 8);
-      const uint64_t s_z = (uint64_t)cnt << 8;
-      const uint64_t slo = cov ? xv : (isZ ? s_z : (isF ? s_f : s_head));
-      const uint32_t shi = (!cov && isF) ? ((xhi >> 24) | (cnt << 8)) : 0u;
-      uint32_t total;
-      const uint32_t o = wave_excl_sum_small(len, &total);
-      const uint64_t A = A0 + soff;
-      {
-        // OR the string into the ring (zeroed), dword-aligned to its global address
-        const uint64_t at = A + o;
-        const uint32_t al4 = (uint32_t)at & 3;
-        const uint32_t w0 = (uint32_t)slo, w1 = (uint32_t)(slo >> 32), w2 = shi;
-        const uint32_t sh = 4 - al4;
-        const uint32_t e0 = w0 << (8 * al4);
-        const uint32_t e1 = al4 ? __builtin_amdgcn_alignbyte(w1, w0, sh) : w1;
-        const uint32_t e2 = al4 ? __builtin_amdgcn_alignbyte(w2, w1, sh) : w2;
-        const uint32_t e3 = al4 ? __builtin_amdgcn_alignbyte(0u, w2, sh) : 0u;
-        const uint32_t nd = len ? (al4 + len + 3) >> 2 : 0;
-        const uint32_t d0 = (uint32_t)(at >> 2);
-        uint32_t* rw = (uint32_t*)ring;
-        constexpr uint32_t M = kRing / 4 - 1;
-        if (nd > 0) atomicOr(rw + ((d0 + 0) & M), e0);
-        if (nd > 1) atomicOr(rw + ((d0 + 1) & M), e1);
-        if (nd > 2) atomicOr(rw + ((d0 + 2) & M), e2);
-        if (nd > 3) atomicOr(rw + ((d0 + 3) & M), e3);
-      }
-      // requested output offsets (message / chunk starts) inside this step
-      const uint64_t g0 = tbase + 64 * s;
-      while (pnext < g0 + 64) {
-        const uint64_t i = pidx + l;
-        const uint64_t p = i <= a.npos ? a.pos[i] : ~0ull;
-        const bool in = p < g0 + 64;
-        const uint32_t oo = shfl32(o, in ? (int)(p - g0) : 0);
-        if (in) a.pos_out[i] = excl + soff + oo;
-        const uint64_t inm = ballot(in);
-        pidx += __popcll(inm);
-        pnext = pidx <= a.npos ? uniform64(a.pos[pidx]) : ~0ull;
-        if (inm != ~0ull) break;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (!over && agg) {
+      uint8_t* const out = a.out;
+      const uint64_t A0 = (uint64_t)(uintptr_t)out + excl;
+      const uint64_t A1 = A0 + agg;
+      const uint64_t al = (A0 + 15) & ~15ull;
+      const uint64_t hl = al < A1 ? al : A1;
+      if (A0 + l < hl) *(uint8_t*)(uintptr_t)(A0 + l) = stg[16 + l];
+      if (A1 > al) {
+        const uint64_t top = A1 & ~15ull;
+        const uint32_t nb = (uint32_t)((top - al) >> 4);
+        const uint32_t so0 = 16u + (uint32_t)(al - A0);
+        const uint32_t rr = so0 & 3u;
+        for (uint32_t i = l; i < nb; i += 64) {
+          const uint32_t d = (so0 >> 2) + 4 * i;
+          const uint32_t v0 = stg32[d], v1 = stg32[d + 1], v2 = stg32[d + 2], v3 = stg32[d + 3],
+                         v4 = stg32[d + 4];
+          u32x4 v;
+          v.x = __builtin_amdgcn_alignbyte(v1, v0, rr);
+          v.y = __builtin_amdgcn_alignbyte(v2, v1, rr);
+          v.z = __builtin_amdgcn_alignbyte(v3, v2, rr);
+          v.w = __builtin_amdgcn_alignbyte(v4, v3, rr);
+          *(u32x4*)(uintptr_t)(al + 16ull * i) = v;
+        }
+        if (top + l < A1) *(uint8_t*)(uintptr_t)(top + l) = stg[16 + (uint32_t)(top - A0) + l];
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      const uint64_t Aend = A + total;
-      // partial head block (shared with the previous tile's bytes): byte stores
-      const uint64_t hlim = Aend < al ? Aend : al;
-      if (hd < hlim) {
-        const uint64_t p = hd + l;
-        if (l < 16 && p < hlim) {
-          uint8_t* rb = ring + (p & (kRing - 1));
-          *(uint8_t*)(uintptr_t)p = *rb;
-          *rb = 0;
-        }
-        hd = hlim;
-      }
-      // full 16-byte blocks
-      const uint64_t top = Aend & ~15ull;
-      if (top > flushed) {
-        const uint32_t nb = (uint32_t)((top - flushed) >> 4);
-        for (uint32_t i0 = 0; i0 < nb; i0 += 64) {
-          const uint32_t i = i0 + l;
-          if (i < nb) {
-            const uint64_t p = flushed + 16ull * i;
-            u32x4* rb = (u32x4*)(ring + (p & (kRing - 1)));
-            const u32x4 v = *rb;
-            *rb = (u32x4){0, 0, 0, 0};
-            *(u32x4*)(uintptr_t)p = v;
-          }
-        }
-        flushed = top;
+      const uint32_t nz16 = (uint32_t)((agg + 15) >> 4) + 1;
+      for (uint32_t i = l; i < nz16; i += 64) ((u32x4*)(stg + 16))[i] = (u32x4){0, 0, 0, 0};
+    }
+    // positions: add the tile's global offset (own stores, read back past L1)
+    if (a.pos) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      for (uint64_t i = pidx0 + l; i < pidx; i += 64)
+        a.pos_out[i] = load_agent(a.pos_out + i) + excl;
+      if (tend == N) {
+        const uint64_t tot = excl + agg;
+        for (uint64_t i = pidx + l; i <= a.npos; i += 64) a.pos_out[i] = tot;
       }
     }
-    if (!over) {
-      // partial tail block
-      const uint64_t from = flushed > hd ? flushed : hd;
-      const uint64_t p = from + l;
-      if (l < 16 && p < A1) {
-        uint8_t* rb = ring + (p & (kRing - 1));
-        *(uint8_t*)(uintptr_t)p = *rb;
-        *rb = 0;
-      }
-    }
-    // positions at or past the end of the batch -> total
-    if (a.pos && tend == N) {
-      const uint64_t tot = excl + agg;
-      for (uint64_t i = pidx + l; i <= a.npos; i += 64) a.pos_out[i] = tot;
-      if (l == 0 && a.total_out) *a.total_out = tot;
-    }
-    stm.mark(5);  // emission
-    if (STAMPS && l == 0 && a.stamps) atomicAdd(a.stamps + 15, 1ull);
+    if (tend == N && l == 0 && a.total_out) *a.total_out = excl + agg;
+    stm.mark(5);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    cur = nxt;
+    };
+    if (t * T + T <= N) tile(std::true_type{});
+    else tile(std::false_type{});
+    if (PF) cur = nxt;
+    else if (t + nwaves < a.ntiles) load_tile<S>(a, t + nwaves, cur);
   }  // tile loop
 }
 
@@ -531,24 +534,35 @@ int pack_steps() {
   return steps;
 }
 
-template <int S>
+template <int S, bool PF>
 hipError_t launch_pack_s(const PackTileArgs& a, hipStream_t stream) {
-  static const unsigned cap = resident_blocks((const void*)pack_tiles_kernel<S, false>, 256, 0);
+  static const unsigned cap =
+      resident_blocks((const void*)pack_tiles_kernel<S, PF, false>, 256, 0);
   const uint64_t want = (a.ntiles + 3) / 4;
   const unsigned blocks = (unsigned)(want < cap ? want : cap);
   if (a.stamps)
-    hipLaunchKernelGGL((pack_tiles_kernel<S, true>), dim3(blocks), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL((pack_tiles_kernel<S, PF, true>), dim3(blocks), dim3(256), 0, stream, a);
   else
-    hipLaunchKernelGGL((pack_tiles_kernel<S, false>), dim3(blocks), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL((pack_tiles_kernel<S, PF, false>), dim3(blocks), dim3(256), 0, stream, a);
   return hipGetLastError();
+}
+
+// Tuning knob (env CPK_PACK_PF=1): prefetch the next tile into registers during the current one.
+static bool pack_prefetch() {
+  static const bool on = [] {
+    const char* e = getenv("CPK_PACK_PF");
+    return e && atoi(e) != 0;
+  }();
+  return on;
 }
 
 hipError_t launch_pack_tiles(const PackTileArgs& a, hipStream_t stream) {
   if (a.ntiles == 0) return hipSuccess;
+  const bool pf = pack_prefetch();
   switch (pack_steps()) {
-    case 4: return launch_pack_s<4>(a, stream);
-    case 8: return launch_pack_s<8>(a, stream);
-    default: return launch_pack_s<16>(a, stream);
+    case 4: return pf ? launch_pack_s<4, true>(a, stream) : launch_pack_s<4, false>(a, stream);
+    case 16: return pf ? launch_pack_s<16, true>(a, stream) : launch_pack_s<16, false>(a, stream);
+    default: return pf ? launch_pack_s<8, true>(a, stream) : launch_pack_s<8, false>(a, stream);
   }
 }
 

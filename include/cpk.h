@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define CPK_ABI_VERSION 1
+#define CPK_ABI_VERSION 2
 
 typedef enum cpk_status {
   CPK_OK = 0,
@@ -167,7 +167,9 @@ cpk_status cpk_unpack_messages_host(cpk_ctx* ctx, const uint8_t* h_packed, uint6
 /* ------------------------------------------------------------------------------------------
  * Synthetic workloads (benchmarks and tests).  Fills d_words with nmsgs flat
  * messages whose word offsets are given in d_msg_word_off (nmsgs+1 entries, e.g. from
- * cpk_gen_offsets).  Every word is a function of (seed, first_msg + i, word index) only, so all
+ * cpk_gen_offsets).  Message i of the call is global message first_msg + i * msg_stride
+ * (msg_stride 0 is taken as 1; round-robin sharding passes first_msg = rank, msg_stride =
+ * world).  Every word is a function of (seed, global message id, word index) only, so all
  * GPUs and the host restatement (oracle) build identical bytes without transfers.
  *   profile 0 "flat"    -- flat-struct mix (45% small ints, 20% u32 pairs, 15% zero, 10%
  *                          pointers, 10% ASCII text)
@@ -176,13 +178,14 @@ cpk_status cpk_unpack_messages_host(cpk_ctx* ctx, const uint8_t* h_packed, uint6
  *   profile 2 "text"    -- ASCII text (no zero byte)
  *   profile 3 "mixed"   -- per-message choice of 0/1/2 by hash */
 cpk_status cpk_gen_messages(cpk_ctx* ctx, int profile, uint64_t seed, uint64_t first_msg,
-                            uint64_t nmsgs, uint32_t nseg, const uint64_t* d_msg_word_off,
+                            uint64_t msg_stride, uint64_t nmsgs, uint32_t nseg,
+                            const uint64_t* d_msg_word_off,
                             uint64_t* d_words, void* stream);
 /* Message sizes for the generator: message i has nseg segments of seg_words words each, or,
  * when seg_words == 0, one segment of 2^k words with k uniform in [3, 11] by hash (config C5).
  * Writes d_msg_word_off (nmsgs+1 entries) on the device and returns the total word count. */
-cpk_status cpk_gen_offsets(cpk_ctx* ctx, uint64_t seed, uint64_t first_msg, uint64_t nmsgs,
-                           uint32_t nseg, uint64_t seg_words, uint64_t* d_msg_word_off,
+cpk_status cpk_gen_offsets(cpk_ctx* ctx, uint64_t seed, uint64_t first_msg,
+                           uint64_t msg_stride, uint64_t nmsgs, uint32_t nseg, uint64_t seg_words, uint64_t* d_msg_word_off,
                            uint64_t* total_words_out, void* stream);
 
 /* ------------------------------------------------------------------------------------------

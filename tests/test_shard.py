@@ -1,0 +1,82 @@
+"""Multi-GPU path on the CPU: message shards (capnproto_amd/shard.py) and the bench's whole-job
+reductions, with world_size-2 gloo process groups (no GPU).  The data path has no collective:
+each rank packs / unpacks its own messages, and a message's packed bytes do not depend on which
+rank packs it -- checked against the oracle."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from capnproto_amd.shard import reduce_step, shard_messages
+
+
+@pytest.mark.parametrize("mode", ["block", "round_robin"])
+@pytest.mark.parametrize("world,n", [(1, 10), (2, 10), (2, 11), (8, 4096), (8, 13), (3, 2)])
+def test_shards_partition_the_batch(mode, world, n):
+    seen = []
+    for r in range(world):
+        first, stride, count = shard_messages(r, world, n, mode)
+        seen += [first + stride * i for i in range(count)]
+    assert sorted(seen) == list(range(n))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import pyoracle
+
+        o = pyoracle.Oracle()
+        rng = np.random.default_rng(7)
+        # the global batch: 12 flat messages (table word + one segment) known to every rank
+        sizes = rng.integers(1, 300, 12)
+        msgs = []
+        for s in sizes:
+            body = rng.integers(0, 2**63, int(s), dtype=np.uint64)
+            body[rng.random(int(s)) < 0.4] = 0
+            msgs.append(np.concatenate([np.array([int(s) << 32], dtype=np.uint64), body]))
+        first, stride, count = shard_messages(rank, world, len(msgs), "round_robin")
+        mine = [msgs[first + stride * i] for i in range(count)]
+        off = np.cumsum([0] + [len(m) for m in mine]).astype(np.uint64)
+        packed, poff, st = o.pack_batch(np.concatenate(mine), off)
+        per_msg = [bytes(packed[int(poff[i]):int(poff[i + 1])]) for i in range(count)]
+        alone = [o.pack_flat(m)[0] for m in mine]
+        same = per_msg == alone
+        red = reduce_step(0.5 + rank, float(off[-1] * 8), float(poff[-1]), 1.0 + rank, 2.0,
+                          same, dist=dist)
+        q.put((rank, red, same, [first + stride * i for i in range(count)]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_shards_and_reduction():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    out.sort()
+    ids = sorted(out[0][3] + out[1][3])
+    assert ids == list(range(12))
+    for rank, red, same, _ in out:
+        assert same, "per-message packed bytes depend on the shard"
+        assert red["dt_max"] == 1.5 and red["pack_ms"] == 2.0
+        assert red["ok_all"]
+    assert out[0][1]["unpacked_all"] == out[1][1]["unpacked_all"] > 0
