@@ -235,7 +235,7 @@ cpk_status unpack_common(cpk_ctx* ctx, uint32_t mode, const uint8_t* d_packed, u
                          const uint64_t* d_in_off, uint64_t n, const uint64_t* d_word_off_in,
                          uint64_t* d_words, uint64_t cap, uint64_t* d_word_off_out,
                          int32_t* d_status, uint64_t* d_size_out, uint64_t limit,
-                         hipStream_t stream) {
+                         hipStream_t stream, uint64_t* d_in_end = nullptr) {
   if (!ctx || (!d_in_off && n) || (!d_packed && P) || (!d_status && n))
     return CPK_ERR_INVALID_ARGUMENT;
   if (hipSetDevice(ctx->device) != hipSuccess) return CPK_ERR_HIP;
@@ -278,6 +278,7 @@ cpk_status unpack_common(cpk_ctx* ctx, uint32_t mode, const uint8_t* d_packed, u
   a.words_capacity = d_words ? cap : 0;
   a.status = d_status;
   a.size_out = d_size_out;
+  a.in_end = d_in_end;
   a.mode = mode;
   a.ntiles = ntiles;
   a.tile_counter = s.counter;
@@ -454,6 +455,19 @@ cpk_status cpk_unpack_messages(cpk_ctx* ctx, const uint8_t* d_packed, uint64_t t
                        (hipStream_t)stream);
 }
 
+cpk_status cpk_read_packed_messages(cpk_ctx* ctx, const uint8_t* d_packed, uint64_t total_bytes,
+                                   const uint64_t* d_msg_in_off, uint64_t nmsgs,
+                                   uint64_t* d_words, uint64_t words_capacity,
+                                   uint64_t* d_msg_word_off, int32_t* d_status,
+                                   uint64_t* d_msg_in_end, const cpk_limits* limits,
+                                   void* stream) {
+  if (!d_msg_in_end && nmsgs) return CPK_ERR_INVALID_ARGUMENT;
+  const uint64_t limit = limits ? limits->traversal_limit_words : 8ull * 1024 * 1024;
+  return unpack_common(ctx, 0, d_packed, total_bytes, d_msg_in_off, nmsgs, nullptr, d_words,
+                       words_capacity, d_msg_word_off, d_status, nullptr, limit,
+                       (hipStream_t)stream, d_msg_in_end);
+}
+
 cpk_status cpk_unpacked_size(cpk_ctx* ctx, const uint8_t* d_packed, uint64_t total_bytes,
                              const uint64_t* d_in_off, uint64_t n, uint64_t* d_words_out,
                              int32_t* d_status, void* stream) {
@@ -511,6 +525,116 @@ cpk_status cpk_unpack_messages_host(cpk_ctx* ctx, const uint8_t* h_packed, uint6
   if (n && hipMemcpy(h_words, d_words, n * 8, hipMemcpyDeviceToHost) != hipSuccess)
     return CPK_ERR_HIP;
   return CPK_OK;
+}
+
+cpk_status cpk_read_packed_message_host(cpk_ctx* ctx, const uint8_t* h_packed,
+                                       uint64_t avail_bytes, uint64_t* h_words,
+                                       uint64_t words_capacity, uint64_t* words_out,
+                                       uint64_t* consumed_out, const cpk_limits* limits) {
+  if (!ctx || (!h_packed && avail_bytes) || (!h_words && words_capacity))
+    return CPK_ERR_INVALID_ARGUMENT;
+  if (hipSetDevice(ctx->device) != hipSuccess) return CPK_ERR_HIP;
+  if (words_out) *words_out = 0;
+  if (consumed_out) *consumed_out = 0;
+  if (avail_bytes == 0) return CPK_ERR_PREMATURE_EOF;
+  cpk_status st;
+  if ((st = ensure(&ctx->stage[0], &ctx->stage_size[0], words_capacity * 8 + 16)) != CPK_OK)
+    return st;
+  if ((st = ensure(&ctx->stage[1], &ctx->stage_size[1], avail_bytes + 16)) != CPK_OK) return st;
+  if ((st = ensure(&ctx->stage[2], &ctx->stage_size[2], 64)) != CPK_OK) return st;
+  uint64_t* d_words = (uint64_t*)ctx->stage[0];
+  uint8_t* d_packed = (uint8_t*)ctx->stage[1];
+  uint64_t* d_in_off = (uint64_t*)ctx->stage[2];  // [2]
+  uint64_t* d_word_off = d_in_off + 2;            // [2]
+  uint64_t* d_in_end = d_word_off + 2;            // [1]
+  int32_t* d_status = (int32_t*)(d_in_end + 1);
+  const uint64_t in_off[2] = {0, avail_bytes};
+  hipStream_t s = nullptr;
+  if (hipMemcpyAsync(d_packed, h_packed, avail_bytes, hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipMemcpyAsync(d_in_off, in_off, 16, hipMemcpyHostToDevice, s) != hipSuccess)
+    return CPK_ERR_HIP;
+  st = cpk_read_packed_messages(ctx, d_packed, avail_bytes, d_in_off, 1, d_words, words_capacity,
+                                d_word_off, d_status, d_in_end, limits, s);
+  if (st != CPK_OK) return st;
+  if ((st = cpk_sync(ctx, s)) != CPK_OK) return st;
+  uint64_t wo[2] = {0, 0}, end = 0;
+  int32_t ms = 0;
+  if (hipMemcpy(wo, d_word_off, 16, hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemcpy(&end, d_in_end, 8, hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemcpy(&ms, d_status, 4, hipMemcpyDeviceToHost) != hipSuccess)
+    return CPK_ERR_HIP;
+  // more bytes in the buffer than the message uses: the rest is the next message's
+  if (ms == CPK_ERR_TRAILING_BYTES) ms = CPK_OK;
+  if (words_out) *words_out = wo[1];
+  if (ms != CPK_OK) return (cpk_status)ms;
+  if (consumed_out) *consumed_out = end;
+  if (wo[1] > words_capacity) return CPK_ERR_CAPACITY;
+  if (wo[1] && hipMemcpy(h_words, d_words, wo[1] * 8, hipMemcpyDeviceToHost) != hipSuccess)
+    return CPK_ERR_HIP;
+  return CPK_OK;
+}
+
+cpk_status cpk_pack_chunks_host(cpk_ctx* ctx, const uint64_t* h_words, uint64_t total_words,
+                                const uint64_t* h_chunk_word_off, uint64_t nchunks, uint8_t* h_out,
+                                uint64_t out_capacity, uint64_t* h_chunk_out_off) {
+  if (!ctx || (!h_chunk_word_off && nchunks) || (!h_words && total_words))
+    return CPK_ERR_INVALID_ARGUMENT;
+  if (hipSetDevice(ctx->device) != hipSuccess) return CPK_ERR_HIP;
+  const size_t wbytes = total_words * 8, obytes = (nchunks + 1) * 8;
+  cpk_status st;
+  if ((st = ensure(&ctx->stage[0], &ctx->stage_size[0], wbytes + 16)) != CPK_OK) return st;
+  if ((st = ensure(&ctx->stage[1], &ctx->stage_size[1], out_capacity + 16)) != CPK_OK) return st;
+  if ((st = ensure(&ctx->stage[2], &ctx->stage_size[2], 2 * obytes + 64)) != CPK_OK) return st;
+  uint64_t* d_words = (uint64_t*)ctx->stage[0];
+  uint8_t* d_out = (uint8_t*)ctx->stage[1];
+  uint64_t* d_off = (uint64_t*)ctx->stage[2];
+  uint64_t* d_out_off = d_off + (nchunks + 1);
+  hipStream_t s = nullptr;
+  if ((wbytes && hipMemcpyAsync(d_words, h_words, wbytes, hipMemcpyHostToDevice, s)) ||
+      hipMemcpyAsync(d_off, h_chunk_word_off, obytes, hipMemcpyHostToDevice, s) != hipSuccess)
+    return CPK_ERR_HIP;
+  st = cpk_pack_chunks(ctx, d_words, total_words, d_off, nchunks, d_out, out_capacity, d_out_off,
+                       s);
+  if (st != CPK_OK) return st;
+  st = cpk_sync(ctx, s);
+  uint64_t total = 0;
+  if (hipMemcpy(&total, d_out_off + nchunks, 8, hipMemcpyDeviceToHost) != hipSuccess)
+    return CPK_ERR_HIP;
+  if (h_chunk_out_off && hipMemcpy(h_chunk_out_off, d_out_off, obytes, hipMemcpyDeviceToHost))
+    return CPK_ERR_HIP;
+  if (st != CPK_OK) return st;
+  if (total > out_capacity) return CPK_ERR_CAPACITY;
+  if (total && hipMemcpy(h_out, d_out, total, hipMemcpyDeviceToHost) != hipSuccess)
+    return CPK_ERR_HIP;
+  return CPK_OK;
+}
+
+cpk_status cpk_unpacked_size_host(cpk_ctx* ctx, const uint8_t* h_packed, uint64_t nbytes,
+                                  uint64_t* words_out) {
+  if (!ctx || (!h_packed && nbytes) || !words_out) return CPK_ERR_INVALID_ARGUMENT;
+  if (hipSetDevice(ctx->device) != hipSuccess) return CPK_ERR_HIP;
+  *words_out = 0;
+  if (nbytes == 0) return CPK_OK;
+  cpk_status st;
+  if ((st = ensure(&ctx->stage[1], &ctx->stage_size[1], nbytes + 16)) != CPK_OK) return st;
+  if ((st = ensure(&ctx->stage[2], &ctx->stage_size[2], 64)) != CPK_OK) return st;
+  uint8_t* d_packed = (uint8_t*)ctx->stage[1];
+  uint64_t* d_in_off = (uint64_t*)ctx->stage[2];
+  uint64_t* d_size = d_in_off + 2;
+  int32_t* d_status = (int32_t*)(d_size + 1);
+  const uint64_t in_off[2] = {0, nbytes};
+  hipStream_t s = nullptr;
+  if (hipMemcpyAsync(d_packed, h_packed, nbytes, hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipMemcpyAsync(d_in_off, in_off, 16, hipMemcpyHostToDevice, s) != hipSuccess)
+    return CPK_ERR_HIP;
+  st = cpk_unpacked_size(ctx, d_packed, nbytes, d_in_off, 1, d_size, d_status, s);
+  if (st != CPK_OK) return st;
+  if ((st = cpk_sync(ctx, s)) != CPK_OK) return st;
+  int32_t ms = 0;
+  if (hipMemcpy(words_out, d_size, 8, hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemcpy(&ms, d_status, 4, hipMemcpyDeviceToHost) != hipSuccess)
+    return CPK_ERR_HIP;
+  return (cpk_status)ms;
 }
 
 // Diagnostic (not in include/cpk.h): copies and clears the phase-stamp sums (CPK_STAMPS=1).

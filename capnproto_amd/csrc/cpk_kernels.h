@@ -56,6 +56,7 @@ struct UnpackArgs {
   uint64_t words_capacity;
   int32_t* status;
   uint64_t* size_out;           // mode 2
+  uint64_t* in_end;             // optional: packed byte where each message actually ends
   uint32_t mode;                // 0 messages, 1 exact-size chunks (flat-packed), 2 size only
   uint64_t ntiles;
   uint32_t* tile_counter;

@@ -312,6 +312,7 @@ struct RunJob {
   uint64_t dst, src;
   uint32_t n;
   bool raw;
+  uint64_t end;  // absolute packed byte after this record (terminal records: message end)
 };
 
 __device__ __forceinline__ int32_t handle_record(const UnpackArgs& a, const uint8_t* d, int p,
@@ -359,6 +360,7 @@ __device__ __forceinline__ int32_t handle_record(const UnpackArgs& a, const uint
       }
     }
   }
+  job->end = end;
   if (st < 0) {
     if (wb + 1 + cnt == mi.total) st = end < mend ? kTrailing : kOK;
     else if (end >= mend) st = kEOF;
@@ -697,6 +699,7 @@ __global__ __launch_bounds__(256) void body_kernel(UnpackArgs a) {
         }
       } else if (s >= 0) {
         a.status[m] = s;
+        if (a.in_end && (s == kOK || s == kTrailing || s == kCap)) a.in_end[m] = job.end;
       }
     }
     run_jobs(a, job);
@@ -771,6 +774,7 @@ __global__ __launch_bounds__(64) void fallback_kernel(UnpackArgs a) {
             const int32_t s = handle_record(a, d, p, pos + p, w0, mi, &job, word);
             if (s >= 0) {
               a.status[m] = s;
+              if (a.in_end && (s == kOK || s == kTrailing || s == kCap)) a.in_end[m] = job.end;
               done = true;
             }
           }

@@ -165,6 +165,38 @@ cpk_status cpk_unpack_messages_host(cpk_ctx* ctx, const uint8_t* h_packed, uint6
                                     const cpk_limits* limits);
 
 /* ------------------------------------------------------------------------------------------
+ * Stream readers (serialize-packed.c++:437-458 PackedMessageReader over a BufferedInputStream;
+ * serialize-packed-test.c++:348-371 reads two messages from one stream).
+ * Like cpk_unpack_messages, plus d_msg_in_end[i] = the absolute packed byte offset where
+ * message i actually ends -- the bytes the reader consumed from its stream.  A message whose
+ * [in_off[i], in_off[i+1]) range holds more bytes than it uses still reports
+ * CPK_ERR_TRAILING_BYTES in d_status (with d_msg_in_end set): for a stream reader that is
+ * success, the remaining bytes belong to the next message. */
+cpk_status cpk_read_packed_messages(cpk_ctx* ctx, const uint8_t* d_packed, uint64_t total_bytes,
+                                   const uint64_t* d_msg_in_off, uint64_t nmsgs,
+                                   uint64_t* d_words, uint64_t words_capacity,
+                                   uint64_t* d_msg_word_off, int32_t* d_status,
+                                   uint64_t* d_msg_in_end, const cpk_limits* limits,
+                                   void* stream);
+/* One message from the front of a host buffer (what PackedMessageReader's constructor reads):
+ * decodes on the device, returns the flat words (table + segments) in h_words, their count in
+ * *words_out and the packed bytes used in *consumed_out.  CPK_ERR_PREMATURE_EOF when the buffer
+ * ends inside the message (a stream caller reads more and retries); CPK_ERR_CAPACITY (with
+ * *words_out set) when h_words is too small. */
+cpk_status cpk_read_packed_message_host(cpk_ctx* ctx, const uint8_t* h_packed,
+                                       uint64_t avail_bytes, uint64_t* h_words,
+                                       uint64_t words_capacity, uint64_t* words_out,
+                                       uint64_t* consumed_out, const cpk_limits* limits);
+/* PackedOutputStream::write (serialize-packed.c++:307-431) of host chunks: chunk i =
+ * h_words[h_chunk_word_off[i] .. h_chunk_word_off[i+1]), each packed on its own. */
+cpk_status cpk_pack_chunks_host(cpk_ctx* ctx, const uint64_t* h_words, uint64_t total_words,
+                                const uint64_t* h_chunk_word_off, uint64_t nchunks, uint8_t* h_out,
+                                uint64_t out_capacity, uint64_t* h_chunk_out_off);
+/* computeUnpackedSizeInWords (serialize-packed.c++:482-508) of one host buffer. */
+cpk_status cpk_unpacked_size_host(cpk_ctx* ctx, const uint8_t* h_packed, uint64_t nbytes,
+                                  uint64_t* words_out);
+
+/* ------------------------------------------------------------------------------------------
  * Synthetic workloads (benchmarks and tests).  Fills d_words with nmsgs flat
  * messages whose word offsets are given in d_msg_word_off (nmsgs+1 entries, e.g. from
  * cpk_gen_offsets).  Message i of the call is global message first_msg + i * msg_stride

@@ -1,0 +1,231 @@
+// cpk_capnp.h -- the reference's packed-serialization API (capnproto c++/src/capnp/
+// serialize-packed.h:32-124 and the kj/io.h stream contracts it is written against), over the
+// MI355X codec's C ABI (cpk.h).  Same class / function names, argument meaning and failure
+// behaviour: the reference throws kj::Exception with a fixed description; this façade throws
+// cpk_capnp::Exception carrying the same description (cpk_status_string) and the cpk_status.
+//
+// Everything here is host C++; every byte of packing / unpacking runs in the HIP kernels behind
+// libcpk_hip.so.  There is no CPU fallback: without a GPU the first call throws
+// Exception(CPK_ERR_NO_DEVICE).
+//
+// Namespace cpk_capnp stands in for capnp (and the few kj types the API names).  A code base
+// that uses capnp::writePackedMessage / capnp::PackedMessageReader switches by including this
+// header and replacing the namespace.
+#ifndef CPK_CAPNP_H_
+#define CPK_CAPNP_H_
+
+#include <cstddef>
+#include <cstdint>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "cpk.h"
+
+namespace cpk_capnp {
+
+typedef unsigned char byte;
+
+// capnp::word (common.h:344): eight opaque bytes.
+struct word {
+  uint64_t content;
+};
+static_assert(sizeof(word) == 8, "word is 8 bytes");
+
+// kj::ArrayPtr subset.
+template <typename T>
+class ArrayPtr {
+ public:
+  ArrayPtr() : ptr_(nullptr), size_(0) {}
+  ArrayPtr(decltype(nullptr)) : ptr_(nullptr), size_(0) {}
+  ArrayPtr(T* p, size_t n) : ptr_(p), size_(n) {}
+  template <typename U>
+  ArrayPtr(const ArrayPtr<U>& o) : ptr_(o.begin()), size_(o.size()) {}
+  ArrayPtr(std::vector<typename std::remove_const<T>::type>& v) : ptr_(v.data()), size_(v.size()) {}
+  T* begin() const { return ptr_; }
+  T* end() const { return ptr_ + size_; }
+  size_t size() const { return size_; }
+  T& operator[](size_t i) const { return ptr_[i]; }
+  ArrayPtr slice(size_t a, size_t b) const { return ArrayPtr(ptr_ + a, b - a); }
+
+ private:
+  T* ptr_;
+  size_t size_;
+};
+
+// kj::Exception (FAILED) as thrown by KJ_REQUIRE / KJ_FAIL_REQUIRE on the packed path.
+class Exception : public std::runtime_error {
+ public:
+  Exception(cpk_status status, const std::string& where);
+  cpk_status status() const { return status_; }
+
+ private:
+  cpk_status status_;
+};
+
+// ---- kj/io.h stream contracts ----------------------------------------------------------------
+class OutputStream {
+ public:
+  virtual ~OutputStream() = default;
+  virtual void write(const void* buffer, size_t size) = 0;
+  void write(ArrayPtr<const byte> bytes) { write(bytes.begin(), bytes.size()); }
+  // kj/io.c++:109-113: one write() per piece (PackedOutputStream does not override it, so runs
+  // never cross a piece).
+  virtual void write(ArrayPtr<const ArrayPtr<const byte>> pieces);
+};
+
+class BufferedOutputStream : public OutputStream {
+ public:
+  virtual ArrayPtr<byte> getWriteBuffer() = 0;
+};
+
+class InputStream {
+ public:
+  virtual ~InputStream() = default;
+  virtual size_t tryRead(void* buffer, size_t minBytes, size_t maxBytes) = 0;
+  // kj/io.c++:53: "Premature EOF" when fewer than `bytes` arrive.
+  void read(void* buffer, size_t bytes);
+  virtual void skip(size_t bytes);
+};
+
+class BufferedInputStream : public InputStream {
+ public:
+  // Whatever is buffered (empty = end of stream); refills when the buffer is exhausted.
+  virtual ArrayPtr<const byte> tryGetReadBuffer() = 0;
+};
+
+// kj/io.h:210-230, io.c++:267-286: writes into a caller-owned array; "backing array was not large enough for
+// the data" (CPK_ERR_CAPACITY) when it overflows.
+class ArrayOutputStream : public BufferedOutputStream {
+ public:
+  explicit ArrayOutputStream(ArrayPtr<byte> array) : array_(array), fill_(0) {}
+  ArrayPtr<byte> getArray() { return array_.slice(0, fill_); }
+  ArrayPtr<byte> getWriteBuffer() override { return array_.slice(fill_, array_.size()); }
+  void write(const void* buffer, size_t size) override;
+  using OutputStream::write;
+
+ private:
+  ArrayPtr<byte> array_;
+  size_t fill_;
+};
+
+// kj/io.h:232-254, io.c++:290-326: growing vector.
+class VectorOutputStream : public BufferedOutputStream {
+ public:
+  explicit VectorOutputStream(size_t initialCapacity = 4096) { bytes_.reserve(initialCapacity); }
+  ArrayPtr<const byte> getArray() const { return ArrayPtr<const byte>(bytes_.data(), bytes_.size()); }
+  void clear() { bytes_.clear(); }
+  ArrayPtr<byte> getWriteBuffer() override;
+  void write(const void* buffer, size_t size) override;
+  using OutputStream::write;
+
+ private:
+  std::vector<byte> bytes_;
+  std::vector<byte> spare_;
+};
+
+// kj/io.h:195-208, io.c++:243-263.
+class ArrayInputStream : public BufferedInputStream {
+ public:
+  explicit ArrayInputStream(ArrayPtr<const byte> array) : array_(array) {}
+  ArrayPtr<const byte> tryGetReadBuffer() override { return array_; }
+  size_t tryRead(void* buffer, size_t minBytes, size_t maxBytes) override;
+  void skip(size_t bytes) override;
+
+ private:
+  ArrayPtr<const byte> array_;
+};
+
+// File descriptors (kj::FdInputStream / FdOutputStream + the buffered wrappers of kj/io.c++:
+// 145-239), used by PackedFdMessageReader / writePackedMessageToFd.
+class FdBufferedInputStream : public BufferedInputStream {
+ public:
+  explicit FdBufferedInputStream(int fd, size_t bufferSize = 65536);
+  ArrayPtr<const byte> tryGetReadBuffer() override;
+  size_t tryRead(void* buffer, size_t minBytes, size_t maxBytes) override;
+  void skip(size_t bytes) override;
+
+ private:
+  int fd_;
+  std::vector<byte> buf_;
+  size_t begin_ = 0, end_ = 0;
+};
+
+class FdOutputStream : public OutputStream {
+ public:
+  explicit FdOutputStream(int fd) : fd_(fd) {}
+  void write(const void* buffer, size_t size) override;
+  using OutputStream::write;
+
+ private:
+  int fd_;
+};
+
+// ---- capnp ----------------------------------------------------------------------------------
+// message.h:54-73 (the limits the packed reader enforces).
+struct ReaderOptions {
+  uint64_t traversalLimitInWords = 8 * 1024 * 1024;
+  int nestingLimit = 64;
+};
+
+// Device the calling thread's codec context uses (default 0; env CPK_DEVICE).  Each thread owns
+// one cpk_ctx, created on first use (a cpk_ctx is single-threaded, cpk.h).
+void setDevice(int device);
+cpk_ctx* threadContext();
+
+namespace _ {  // private
+
+// serialize-packed.h:49-63.  Each write() is one chunk, packed by the device.
+class PackedOutputStream : public OutputStream {
+ public:
+  explicit PackedOutputStream(BufferedOutputStream& inner) : inner_(inner) {}
+  void write(const void* buffer, size_t size) override;
+  using OutputStream::write;
+
+ private:
+  BufferedOutputStream& inner_;
+};
+
+}  // namespace _
+
+// serialize-packed.h:65-71 / serialize.h InputStreamMessageReader: reads one packed message
+// (segment table, then the segments) from the stream, leaving the stream positioned after it.
+class PackedMessageReader {
+ public:
+  PackedMessageReader(BufferedInputStream& inputStream, ReaderOptions options = ReaderOptions(),
+                      ArrayPtr<word> scratchSpace = nullptr);
+  virtual ~PackedMessageReader() = default;
+  size_t segmentCount() const { return segments_.size(); }
+  // MessageReader::getSegment (message.h:100): null past the last segment.
+  ArrayPtr<const word> getSegment(unsigned id) const;
+  const ReaderOptions& getOptions() const { return options_; }
+  // The flat message (table + segments) the reader decoded, for callers that want it whole.
+  ArrayPtr<const word> getFlat() const { return flat_; }
+
+ private:
+  ReaderOptions options_;
+  std::vector<word> owned_;
+  ArrayPtr<const word> flat_;
+  std::vector<ArrayPtr<const word>> segments_;
+};
+
+// serialize-packed.h:73-89: reads from a file descriptor.
+class PackedFdMessageReader : private FdBufferedInputStream, public PackedMessageReader {
+ public:
+  PackedFdMessageReader(int fd, ReaderOptions options = ReaderOptions(),
+                        ArrayPtr<word> scratchSpace = nullptr);
+};
+
+// serialize-packed.h:91-104 (MessageBuilder overloads :114-124 pass getSegmentsForOutput()).
+void writePackedMessage(BufferedOutputStream& output,
+                        ArrayPtr<const ArrayPtr<const word>> segments);
+void writePackedMessage(OutputStream& output, ArrayPtr<const ArrayPtr<const word>> segments);
+void writePackedMessageToFd(int fd, ArrayPtr<const ArrayPtr<const word>> segments);
+
+// serialize-packed.h:107.
+size_t computeUnpackedSizeInWords(ArrayPtr<const byte> packedBytes);
+
+}  // namespace cpk_capnp
+
+#endif  // CPK_CAPNP_H_

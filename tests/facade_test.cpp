@@ -1,0 +1,248 @@
+// facade_test.cpp -- the reference's packed-serialization tests (capnproto c++/src/capnp/
+// serialize-packed-test.c++) restated against the cpk_capnp façade (include/cpk_capnp.h), i.e.
+// the reference API running on the MI355X codec.  Fixtures are the reference's own testdata
+// files and KATs, committed under tests/golden/.
+//
+//   cpk_facade_test <tests/golden dir>        exit 0 = all checks passed
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
+
+#include <fstream>
+#include <iterator>
+#include <string>
+#include <vector>
+
+#include "cpk_capnp.h"
+
+using namespace cpk_capnp;
+
+static int g_fail = 0, g_pass = 0;
+#define CHECK(cond, ...)                                   \
+  do {                                                     \
+    if (cond) {                                            \
+      g_pass++;                                            \
+    } else {                                               \
+      g_fail++;                                            \
+      fprintf(stderr, "FAIL %s:%d: ", __FILE__, __LINE__); \
+      fprintf(stderr, __VA_ARGS__);                        \
+      fprintf(stderr, "\n");                               \
+    }                                                      \
+  } while (0)
+
+static std::vector<byte> read_file(const std::string& path) {
+  std::ifstream f(path, std::ios::binary);
+  return std::vector<byte>(std::istreambuf_iterator<char>(f), {});
+}
+
+// Unpacked message file (stream framing) -> segments over its words.
+static std::vector<ArrayPtr<const word>> segments_of(const std::vector<byte>& msg) {
+  const uint32_t* t = reinterpret_cast<const uint32_t*>(msg.data());
+  const uint32_t n = t[0] + 1;
+  const word* w = reinterpret_cast<const word*>(msg.data());
+  size_t at = n / 2 + 1;
+  std::vector<ArrayPtr<const word>> segs;
+  for (uint32_t i = 0; i < n; i++) {
+    segs.push_back(ArrayPtr<const word>(w + at, t[i + 1]));
+    at += t[i + 1];
+  }
+  return segs;
+}
+
+static bool same(ArrayPtr<const byte> a, const std::vector<byte>& b) {
+  return a.size() == b.size() && (a.size() == 0 || memcmp(a.begin(), b.data(), a.size()) == 0);
+}
+
+static std::vector<byte> hex(const char* s) {
+  std::vector<byte> v;
+  for (; s[0] && s[1]; s += 2) {
+    unsigned x;
+    sscanf(s, "%2x", &x);
+    v.push_back((byte)x);
+  }
+  return v;
+}
+
+// serialize-packed-test.c++:203-220 style: one chunk through PackedOutputStream, and back.
+static void kat_chunks(const std::string& dir) {
+  std::ifstream f(dir + "/kats.txt");
+  std::string u, p;
+  int n = 0;
+  while (f >> u >> p) {
+    if (u == "-") u.clear();
+    if (p == "-") p.clear();
+    std::vector<byte> unpacked = hex(u.c_str()), packed = hex(p.c_str());
+    VectorOutputStream out;
+    _::PackedOutputStream pk(out);
+    pk.write(unpacked.data(), unpacked.size());
+    CHECK(same(out.getArray(), packed), "KAT %d pack", n);
+    n++;
+  }
+  CHECK(n >= 10, "KATs read: %d", n);
+}
+
+// testdata/binary <-> testdata/packed, testdata/segmented <-> testdata/segmented-packed
+// (capnp-test.sh golden files).
+static void fixtures(const std::string& dir, const char* unpacked_name, const char* packed_name) {
+  std::vector<byte> msg = read_file(dir + "/" + unpacked_name);
+  std::vector<byte> packed = read_file(dir + "/" + packed_name);
+  auto segs = segments_of(msg);
+  VectorOutputStream out;
+  writePackedMessage(out, ArrayPtr<const ArrayPtr<const word>>(segs.data(), segs.size()));
+  CHECK(same(out.getArray(), packed), "%s: writePackedMessage bytes (%zu vs %zu)", packed_name,
+        out.getArray().size(), packed.size());
+
+  ArrayInputStream in(ArrayPtr<const byte>(packed.data(), packed.size()));
+  PackedMessageReader reader(in);
+  CHECK(reader.segmentCount() == segs.size(), "%s: segment count", packed_name);
+  bool eq = true;
+  for (size_t i = 0; i < segs.size(); i++) {
+    auto s = reader.getSegment((unsigned)i);
+    eq = eq && s.size() == segs[i].size() && memcmp(s.begin(), segs[i].begin(), 8 * s.size()) == 0;
+  }
+  CHECK(eq, "%s: PackedMessageReader segments", packed_name);
+  CHECK(in.tryGetReadBuffer().size() == 0, "%s: reader consumed the whole message", packed_name);
+  CHECK(computeUnpackedSizeInWords(ArrayPtr<const byte>(packed.data(), packed.size())) ==
+            msg.size() / 8,
+        "%s: computeUnpackedSizeInWords", packed_name);
+}
+
+// serialize-packed-test.c++:348-371: two messages back to back in one stream, the second read
+// after the first; also with a scratch space and through a file descriptor.
+static void two_messages(const std::string& dir) {
+  std::vector<byte> a = read_file(dir + "/binary"), b = read_file(dir + "/segmented");
+  auto sa = segments_of(a), sb = segments_of(b);
+  VectorOutputStream out;
+  writePackedMessage(out, ArrayPtr<const ArrayPtr<const word>>(sa.data(), sa.size()));
+  writePackedMessage(out, ArrayPtr<const ArrayPtr<const word>>(sb.data(), sb.size()));
+  auto all = out.getArray();
+  ArrayInputStream in(all);
+  {
+    std::vector<word> scratch(8);
+    PackedMessageReader r1(in, ReaderOptions(), ArrayPtr<word>(scratch.data(), scratch.size()));
+    CHECK(r1.getFlat().size() * 8 == a.size() &&
+              memcmp(r1.getFlat().begin(), a.data(), a.size()) == 0,
+          "first message");
+  }
+  {
+    PackedMessageReader r2(in);
+    CHECK(r2.getFlat().size() * 8 == b.size() &&
+              memcmp(r2.getFlat().begin(), b.data(), b.size()) == 0,
+          "second message");
+    CHECK(r2.segmentCount() == sb.size(), "second message segments");
+  }
+  CHECK(in.tryGetReadBuffer().size() == 0, "stream drained");
+
+  // through a pipe: the reader refills across small buffers
+  int fds[2];
+  if (pipe(fds) == 0) {
+    writePackedMessageToFd(fds[1], ArrayPtr<const ArrayPtr<const word>>(sb.data(), sb.size()));
+    writePackedMessageToFd(fds[1], ArrayPtr<const ArrayPtr<const word>>(sa.data(), sa.size()));
+    close(fds[1]);
+    PackedFdMessageReader f1(fds[0]);
+    CHECK(f1.getFlat().size() * 8 == b.size() &&
+              memcmp(f1.getFlat().begin(), b.data(), b.size()) == 0,
+          "fd: first message");
+    close(fds[0]);
+  }
+}
+
+// Error behaviour: the reference's exceptions (serialize-packed-test.c++:297-346).
+static void errors(const std::string& dir) {
+  std::vector<byte> packed = read_file(dir + "/packed");
+  for (size_t cut : {(size_t)0, (size_t)1, packed.size() / 2, packed.size() - 1}) {
+    ArrayInputStream in(ArrayPtr<const byte>(packed.data(), cut));
+    bool threw = false;
+    cpk_status st = CPK_OK;
+    try {
+      PackedMessageReader r(in);
+    } catch (const Exception& e) {
+      threw = true;
+      st = e.status();
+    }
+    CHECK(threw && st == CPK_ERR_PREMATURE_EOF, "truncated at %zu -> premature EOF (got %d)",
+          cut, (int)st);
+  }
+  // a zero run that overshoots the message (table says 1 word, the run says 3)
+  {
+    std::vector<byte> bad = {0x10, 0x01, 0x00, 0x02};  // table: 1 segment of 1 word; then 00 02
+    ArrayInputStream in(ArrayPtr<const byte>(bad.data(), bad.size()));
+    cpk_status st = CPK_OK;
+    try {
+      PackedMessageReader r(in);
+    } catch (const Exception& e) {
+      st = e.status();
+    }
+    CHECK(st == CPK_ERR_RUN_OVERSHOOT, "run overshoot (got %d)", (int)st);
+  }
+  // traversal limit (serialize.c++:235)
+  {
+    std::vector<byte> msg = read_file(dir + "/binary");
+    auto segs = segments_of(msg);
+    VectorOutputStream out;
+    writePackedMessage(out, ArrayPtr<const ArrayPtr<const word>>(segs.data(), segs.size()));
+    ArrayInputStream in(out.getArray());
+    ReaderOptions opt;
+    opt.traversalLimitInWords = 4;
+    cpk_status st = CPK_OK;
+    try {
+      PackedMessageReader r(in, opt);
+    } catch (const Exception& e) {
+      st = e.status();
+    }
+    CHECK(st == CPK_ERR_MESSAGE_TOO_LARGE, "traversal limit (got %d)", (int)st);
+  }
+  // writing an empty message
+  {
+    VectorOutputStream out;
+    cpk_status st = CPK_OK;
+    try {
+      writePackedMessage(out, ArrayPtr<const ArrayPtr<const word>>());
+    } catch (const Exception& e) {
+      st = e.status();
+    }
+    CHECK(st == CPK_ERR_EMPTY_MESSAGE, "empty message (got %d)", (int)st);
+  }
+  // computeUnpackedSizeInWords on truncated input: "invalid packed data"
+  {
+    std::vector<byte> t = {0xff, 1, 2, 3};
+    cpk_status st = CPK_OK;
+    try {
+      computeUnpackedSizeInWords(ArrayPtr<const byte>(t.data(), t.size()));
+    } catch (const Exception& e) {
+      st = e.status();
+    }
+    CHECK(st == CPK_ERR_INVALID_PACKED, "invalid packed data (got %d)", (int)st);
+  }
+  // ArrayOutputStream capacity
+  {
+    std::vector<byte> small(4);
+    ArrayOutputStream out(ArrayPtr<byte>(small.data(), small.size()));
+    std::vector<byte> msg = read_file(dir + "/binary");
+    auto segs = segments_of(msg);
+    cpk_status st = CPK_OK;
+    try {
+      writePackedMessage(out, ArrayPtr<const ArrayPtr<const word>>(segs.data(), segs.size()));
+    } catch (const Exception& e) {
+      st = e.status();
+    }
+    CHECK(st == CPK_ERR_CAPACITY, "ArrayOutputStream capacity (got %d)", (int)st);
+  }
+}
+
+int main(int argc, char** argv) {
+  const std::string dir = argc > 1 ? argv[1] : "tests/golden";
+  try {
+    kat_chunks(dir);
+    fixtures(dir, "binary", "packed");
+    fixtures(dir, "segmented", "segmented-packed");
+    two_messages(dir);
+    errors(dir);
+  } catch (const Exception& e) {
+    fprintf(stderr, "unexpected exception: %s\n", e.what());
+    return 2;
+  }
+  printf("facade: %d passed, %d failed\n", g_pass, g_fail);
+  return g_fail ? 1 : 0;
+}
