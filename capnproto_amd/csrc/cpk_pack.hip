@@ -212,7 +212,8 @@ __global__ __launch_bounds__(256) void pack_tiles_kernel(PackTileArgs a) {
 
     // ---- pass A --------------------------------------------------------------------------
     // per-step masks parked in VGPR lanes (lane s = step s) to keep SGPR pressure low
-    uint32_t vSYlo = 0, vSYhi = 0, vFlo = 0, vFhi = 0, vNsa = 0;
+    uint32_t vSYlo = 0, vSYhi = 0, vFlo = 0, vFhi = 0, vZlo = 0, vZhi = 0, vRlo = 0, vRhi = 0;
+    uint32_t vNsa = 0, vBase = 0;
     uint32_t tagpk[S / 2];
     bool lastZ = false, lastR = false;
     int first_sync = T, sg = -1;
@@ -237,6 +238,16 @@ __global__ __launch_bounds__(256) void pack_tiles_kernel(PackTileArgs a) {
       vSYhi = setlane<s>(vSYhi, (int)(uint32_t)(SY >> 32));
       vFlo = setlane<s>(vFlo, (int)(uint32_t)Fs);
       vFhi = setlane<s>(vFhi, (int)(uint32_t)(Fs >> 32));
+      vZlo = setlane<s>(vZlo, (int)(uint32_t)Z);
+      vZhi = setlane<s>(vZhi, (int)(uint32_t)(Z >> 32));
+      vRlo = setlane<s>(vRlo, (int)(uint32_t)R);
+      vRhi = setlane<s>(vRhi, (int)(uint32_t)(R >> 32));
+      // state-independent bytes of the step: 1 + nz per O word, 8 per R word
+      const uint32_t nz = __popc(tag);
+      const uint32_t ob = (x != 0 && nz < 7) ? nz : 0;  // O words: 1 + nz = |O| + sum nz
+      const uint32_t base = (uint32_t)(__popcll(O) + 8 * __popcll(R) + __popcll(ballot(ob & 1)) +
+                                       2 * __popcll(ballot(ob & 2)) + 4 * __popcll(ballot(ob & 4)));
+      vBase = setlane<s>(vBase, base);
       const uint64_t m = SY & V;
       if (m) {
         if (first_sync == T) first_sync = 64 * s + lowest_bit(m);
@@ -317,8 +328,36 @@ __global__ __launch_bounds__(256) void pack_tiles_kernel(PackTileArgs a) {
     if (first_sync > 0 && t > 0) b = (int)(wait_nonzero32(state + t - 1, a.err) & 0xffu);
     stm.mark(2);
 
+    // ---- count pass (scalar): heads / coverage of every step, byte offsets -----------------
+    //   bytes(step) = sum over O words of (1 + nz) + 8 |R| + 2 |Z heads + F heads|
+    uint32_t vCOVlo = 0, vCOVhi = 0, vZHlo = 0, vZHhi = 0, vFHlo = 0, vFHhi = 0, vSoff = 0;
+    uint32_t agg32 = 0;
+    static_for<0, S>([&](auto sc) {
+      constexpr int s = decltype(sc)::value;
+      if (64 * s < nvalid) {
+        const uint64_t Z = readlane64(((uint64_t)vZhi << 32) | vZlo, s);
+        const uint64_t F = readlane64(((uint64_t)vFhi << 32) | vFlo, s);
+        const uint64_t R = readlane64(((uint64_t)vRhi << 32) | vRlo, s);
+        const uint64_t SY = readlane64(((uint64_t)vSYhi << 32) | vSYlo, s);
+        const StepRes r = resolve_step(Z, F, R, SY, b, 64 * s + 63 < nvalid);
+        b = r.b_out;
+        const uint64_t COV = r.covered | ~valid_mask(nvalid, s);
+        vCOVlo = setlane<s>(vCOVlo, (uint32_t)COV);
+        vCOVhi = setlane<s>(vCOVhi, (uint32_t)(COV >> 32));
+        vZHlo = setlane<s>(vZHlo, (uint32_t)r.Zheads);
+        vZHhi = setlane<s>(vZHhi, (uint32_t)(r.Zheads >> 32));
+        vFHlo = setlane<s>(vFHlo, (uint32_t)r.Fheads);
+        vFHhi = setlane<s>(vFHhi, (uint32_t)(r.Fheads >> 32));
+        vSoff = setlane<s>(vSoff, agg32);
+        agg32 += readlane32(vBase, s) + 2 * (uint32_t)__popcll(r.runheads);
+      }
+    });
+    if (first_sync == T && l == 0) store_agent32(state + t, 0x80000000u | (uint32_t)b);
+    const uint64_t agg = agg32;
+    if (!(a.debug_skip & 1)) publish_agg(a.desc, a.gdesc, a.gcnt, t, a.ntiles, agg, 0, a.err);
+    stm.mark(3);
+
     // ---- pass B ----------------------------------------------------------------------------
-    uint32_t soff = 0;  // tile-relative byte offset of the step
     const uint64_t pidx0 = a.pos ? uniform64(a.tile_first[t]) : 0;
     uint64_t pidx = pidx0;
     uint32_t prel = ~0u;  // next requested position, tile-relative (~0: none in this tile)
@@ -329,26 +368,20 @@ __global__ __launch_bounds__(256) void pack_tiles_kernel(PackTileArgs a) {
 #pragma unroll
     for (int s = 0; s < S; s++) {
       if (64 * s < nvalid) {
-        uint64_t x = cur.x[s];
-        asm volatile("" : "+v"(x));  // recompute the class ballots here instead of keeping pass A's
+        const uint64_t x = cur.x[s];
         const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
         const uint32_t tag = (tagpk[s >> 1] >> (16 * (s & 1))) & 0xffu;
         const uint32_t nz = __popc(tag);
-        const uint64_t V = valid_mask(nvalid, s);
-        const uint64_t Z = ballot(x == 0) & V;
-        const uint64_t R = ballot(nz >= 7) & V;
-        const uint64_t F = readlane64(((uint64_t)vFhi << 32) | vFlo, s);
         const uint64_t SY = readlane64(((uint64_t)vSYhi << 32) | vSYlo, s);
-        const StepRes r = resolve_step(Z, F, R, SY, b, 64 * s + 63 < nvalid);
-        b = r.b_out;
-        const uint64_t COV = r.covered | ~V;
-        const uint64_t ZH = r.Zheads, FH = r.Fheads;
+        const uint64_t COV = readlane64(((uint64_t)vCOVhi << 32) | vCOVlo, s);
+        const uint64_t ZH = readlane64(((uint64_t)vZHhi << 32) | vZHlo, s);
+        const uint64_t FH = readlane64(((uint64_t)vFHhi << 32) | vFHlo, s);
+        const uint32_t soff = readlane32(vSoff, s);
         // record length: head 1 + nz (+1 count byte for run heads), covered R 8, covered Z 0
         const uint32_t n1 = nz + 1;
-        const uint32_t len = msel(COV, n1 & 8u, n1 + msel(r.runheads, 1u, 0u));
+        const uint32_t len = msel(COV, n1 & 8u, n1 + msel(ZH | FH, 1u, 0u));
         const uint32_t inc = wave_incl_sum32(len);
         const uint32_t o = inc - len;
-        const uint32_t tot = readlane32(inc, 63);
         // run count: stretch words after this one (<= 255); ffbl of 0 is ~0u
         const uint32_t f_lo = ffbl32((uint32_t)SY & gt_lo);
         const uint32_t f_hi = __builtin_elementwise_add_sat(
@@ -387,23 +420,19 @@ __global__ __launch_bounds__(256) void pack_tiles_kernel(PackTileArgs a) {
             if (inm != ~0ull) break;
           }
         }
-        soff += tot;
       }
     }
-    if (first_sync == T && l == 0) store_agent32(state + t, 0x80000000u | (uint32_t)b);
-    const uint64_t agg = soff;
-    stm.mark(3);
+    stm.mark(4);
 
     // ---- look-back -------------------------------------------------------------------------
     uint64_t excl = 0;
     if (a.debug_skip & 1) {
       excl = t * 4096;  // timing ablation: no look-back (output meaningless)
     } else {
-      publish_agg(a.desc, a.gdesc, a.gcnt, t, a.ntiles, agg, 0, a.err);
       excl = lookback2(a.desc, a.gdesc, t, 0, a.err);
       publish_incl(a.desc, a.gdesc, t, a.ntiles, excl + agg);
     }
-    stm.mark(4);
+    stm.mark(5);
 
     // ---- flush ----------------------------------------------------------------------------
     const bool over = excl + agg > a.out_capacity;
@@ -449,7 +478,7 @@ __global__ __launch_bounds__(256) void pack_tiles_kernel(PackTileArgs a) {
       }
     }
     if (tend == N && l == 0 && a.total_out) *a.total_out = excl + agg;
-    stm.mark(5);
+    stm.mark(6);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     };
     if (t * T + T <= N) tile(std::true_type{});
