@@ -284,40 +284,32 @@ __device__ __forceinline__ uint64_t reduce_nearest(uint64_t v, int k, uint64_t s
   return (segs ? seg_bit : 0) | sum;
 }
 
-// Publishes tile t's aggregate and, for the group's last arriver, the group aggregate.
+// Publishes tile t's aggregate; the group's last tile also combines the group's aggregates (it
+// waits for its in-group predecessors, all running in the same round of the persistent order)
+// and publishes the group aggregate.  gdesc[g] has that single writer (AGG here, then INCL in
+// publish_incl), so no ticket atomics or CAS are needed.
 __device__ __forceinline__ void publish_agg(uint64_t* desc, uint64_t* gdesc, uint32_t* gcnt,
                                             uint64_t t, uint64_t ntiles, uint64_t agg,
                                             uint64_t seg_bit, uint32_t* err) {
+  (void)gcnt;
   const int l = lane_id();
+  if (l == 0) store_agent(desc + t, kDescAgg | agg);
   const uint64_t g = t / kGroup;
   const uint64_t g0 = g * kGroup;
-  const uint32_t n_in = (uint32_t)((ntiles - g0) < (uint64_t)kGroup ? (ntiles - g0) : kGroup);
-  uint32_t old = 0;
+  const bool last_of_group = (t + 1) % kGroup == 0 || t + 1 == ntiles;
+  if (!last_of_group) return;
+  const uint32_t n_in = (uint32_t)(t - g0 + 1);
+  // lane i = tile t - i (lane 0: this tile's own aggregate)
+  const bool use = l > 0 && (uint32_t)l < n_in;
+  const uint64_t d = l == 0 ? (kDescAgg | agg) : load_ready(desc + (t - (uint64_t)(use ? l : 0)),
+                                                            use, err);
+  const bool stop = use && (d & kDescFlags) == kDescIncl;
+  const uint64_t sb = ballot(stop);
+  const int k = sb ? lowest_bit(sb) : (int)n_in - 1;
+  const uint64_t v = reduce_nearest((l == 0 || use) ? (d & kDescValue) : 0, k, seg_bit);
   if (l == 0) {
-    store_agent(desc + t, kDescAgg | agg);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    old = atomicAdd(gcnt + g, 1u);
-  }
-  old = uniform32(old);
-  if (old + 1 == n_in) {
-    // last arriver: combine the group's descriptors in order (lane i = tile g0 + n_in - 1 - i).
-    // A tile may already have replaced its AGG by its INCL: the nearest such stop makes the
-    // combination an inclusive value.
-    const int i = l;
-    const bool use = i < (int)n_in;
-    const uint64_t d = load_ready(desc + g0 + (n_in - 1 - (uint32_t)(use ? i : 0)), use, err);
-    const bool stop = use && (d & kDescFlags) == kDescIncl;
-    const uint64_t sb = ballot(stop);
-    const int k = sb ? lowest_bit(sb) : (int)n_in - 1;
-    const uint64_t v = reduce_nearest(use ? (d & kDescValue) : 0, k, seg_bit);
-    if (l == 0) {
-      const uint64_t nv = sb ? (kDescIncl | (v & ~seg_bit)) : (kDescAgg | v);
-      // never overwrite an inclusive prefix the group's last tile may have published meanwhile
-      const uint64_t cur = load_agent(gdesc + g);
-      if ((cur & kDescFlags) != kDescIncl)
-        atomicCAS((unsigned long long*)(gdesc + g), (unsigned long long)cur,
-                  (unsigned long long)nv);
-    }
+    const uint64_t nv = sb ? (kDescIncl | (v & ~seg_bit)) : (kDescAgg | v);
+    store_agent(gdesc + g, nv);
   }
 }
 

@@ -38,7 +38,9 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // v_writelane: lane `s` (compile-time) of `dst` takes the wave-uniform value `v`.
 template <int L>
 __device__ __forceinline__ uint32_t setlane(uint32_t dst, uint32_t v) {
-  asm("v_writelane_b32 %0, %1, %2" : "+v"(dst) : "s"(v), "i"(L));
+  asm("v_writelane_b32 %0, %1, %2"
+      : "+v"(dst)
+      : "s"((uint32_t)__builtin_amdgcn_readfirstlane((int)v)), "i"(L));
   return dst;
 }
 
@@ -171,14 +173,17 @@ template <int S, bool PF, bool STAMPS>
 __global__ __launch_bounds__(256) void pack_tiles_kernel(PackTileArgs a) {
   static_assert(S >= 2 && S <= 16 && (S % 2) == 0, "S steps per tile");
   constexpr int T = 64 * S;
-  constexpr int kStg = 32 + 640 * S;  // 16 B lead pad + <= 640 B per step + 16 B tail pad
+  // Per-wave staging ring: a tile's records occupy [base, base + 32 + bytes) (16 B pads at both
+  // ends), at most 32 + 640 * S bytes; the ring holds the tile being encoded and the previous
+  // one, whose look-back and flush are deferred until after this tile's emission pass.
+  constexpr int kMaxRegion = 32 + 640 * S;
+  constexpr int kStg = ((kMaxRegion * 6 / 5) + 15) & ~15;
   __shared__ __attribute__((aligned(16))) uint8_t stg_all[4][kStg];
   __shared__ uint64_t sel_tab[256];
 
   const int l = lane_id();
   const int wv = (int)uniform32(threadIdx.x >> 6);
   uint8_t* const stg = stg_all[wv];
-  uint32_t* const stg32 = (uint32_t*)stg;
   sel_tab[threadIdx.x] = make_sel(threadIdx.x);
   for (int i = l; i < kStg / 16; i += 64) ((u32x4*)stg)[i] = (u32x4){0, 0, 0, 0};
   __syncthreads();
@@ -194,6 +199,74 @@ __global__ __launch_bounds__(256) void pack_tiles_kernel(PackTileArgs a) {
   uint64_t t = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wv;
   TileLoad<S> cur;
   if (t < a.ntiles) load_tile<S>(a, t, cur);
+
+  // A tile whose look-back and flush are still to be done.
+  struct Pending {
+    uint64_t t, agg, tend, pidx0, pidx;
+    uint32_t base;
+    bool on;
+  };
+  Pending pend;
+  pend.on = false;
+  auto region = [](uint64_t agg) -> uint32_t { return ((uint32_t)agg + 32u + 15u) & ~15u; };
+  // look-back, inclusive publish, flush of the staged bytes, positions
+  auto finish = [&](const Pending& p) {
+    uint64_t excl = 0;
+    if (a.debug_skip & 1) {
+      excl = p.t * 4096;  // timing ablation: no look-back (output meaningless)
+    } else {
+      excl = lookback2(a.desc, a.gdesc, p.t, 0, a.err);
+      publish_incl(a.desc, a.gdesc, p.t, a.ntiles, excl + p.agg);
+    }
+    const uint64_t agg = p.agg;
+    uint8_t* const sb = stg + p.base;
+    const uint32_t* const sb32 = (const uint32_t*)sb;
+    const bool over = excl + agg > a.out_capacity;
+    if (over && l == 0) raise_error(a.err, kErrCapacity);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (!over && agg) {
+      uint8_t* const out = a.out;
+      const uint64_t A0 = (uint64_t)(uintptr_t)out + excl;
+      const uint64_t A1 = A0 + agg;
+      const uint64_t al = (A0 + 15) & ~15ull;
+      const uint64_t hl = al < A1 ? al : A1;
+      if (A0 + l < hl) *(uint8_t*)(uintptr_t)(A0 + l) = sb[16 + l];
+      if (A1 > al) {
+        const uint64_t top = A1 & ~15ull;
+        const uint32_t nb = (uint32_t)((top - al) >> 4);
+        const uint32_t so0 = 16u + (uint32_t)(al - A0);
+        const uint32_t rr = so0 & 3u;
+        for (uint32_t i = l; i < nb; i += 64) {
+          const uint32_t d = (so0 >> 2) + 4 * i;
+          const uint32_t v0 = sb32[d], v1 = sb32[d + 1], v2 = sb32[d + 2], v3 = sb32[d + 3],
+                         v4 = sb32[d + 4];
+          u32x4 v;
+          v.x = __builtin_amdgcn_alignbyte(v1, v0, rr);
+          v.y = __builtin_amdgcn_alignbyte(v2, v1, rr);
+          v.z = __builtin_amdgcn_alignbyte(v3, v2, rr);
+          v.w = __builtin_amdgcn_alignbyte(v4, v3, rr);
+          *(u32x4*)(uintptr_t)(al + 16ull * i) = v;
+        }
+        if (top + l < A1) *(uint8_t*)(uintptr_t)(top + l) = sb[16 + (uint32_t)(top - A0) + l];
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const uint32_t nz16 = (uint32_t)((agg + 15) >> 4) + 1;
+    for (uint32_t i = l; i < nz16; i += 64) ((u32x4*)(sb + 16))[i] = (u32x4){0, 0, 0, 0};
+    // positions: add the tile's global offset (own stores, read back past L1)
+    if (a.pos) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      for (uint64_t i = p.pidx0 + l; i < p.pidx; i += 64)
+        a.pos_out[i] = load_agent(a.pos_out + i) + excl;
+      if (p.tend == N) {
+        const uint64_t tot = excl + agg;
+        for (uint64_t i = p.pidx + l; i <= a.npos; i += 64) a.pos_out[i] = tot;
+      }
+    }
+    if (p.tend == N && l == 0 && a.total_out) *a.total_out = excl + agg;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  };
+
   for (; t < a.ntiles; t += nwaves) {
     TileLoad<S> nxt;
     auto tile = [&](auto full_c) {
@@ -357,6 +430,19 @@ __global__ __launch_bounds__(256) void pack_tiles_kernel(PackTileArgs a) {
     if (!(a.debug_skip & 1)) publish_agg(a.desc, a.gdesc, a.gcnt, t, a.ntiles, agg, 0, a.err);
     stm.mark(3);
 
+    // ---- staging region: after the pending tile's, else at 0 (finishing it first if needed) ---
+    const uint32_t need = region(agg);
+    uint32_t base = 0;
+    if (pend.on) {
+      const uint32_t pe = pend.base + region(pend.agg);
+      if (pe + need <= (uint32_t)kStg) {
+        base = pe;
+      } else if (need > pend.base) {
+        finish(pend);
+        pend.on = false;
+      }
+    }
+
     // ---- pass B ----------------------------------------------------------------------------
     const uint64_t pidx0 = a.pos ? uniform64(a.tile_first[t]) : 0;
     uint64_t pidx = pidx0;
@@ -397,7 +483,7 @@ __global__ __launch_bounds__(256) void pack_tiles_kernel(PackTileArgs a) {
         w0 = msel(COV, lo, w0);
         w1 = msel(COV, hi, w1);
         // OR into the staging area at byte 16 + soff + o: four dwords from (at - 1) & ~3
-        const uint32_t at = 16u + soff + o;
+        const uint32_t at = base + 16u + soff + o;
         const uint32_t rr = (0u - at) & 3u;
         uint32_t* dp = (uint32_t*)(stg + ((at - 1u) & ~3u));
         atomicOr(dp + 0, __builtin_amdgcn_alignbyte(w0, 0u, rr));
@@ -424,68 +510,23 @@ __global__ __launch_bounds__(256) void pack_tiles_kernel(PackTileArgs a) {
     }
     stm.mark(4);
 
-    // ---- look-back -------------------------------------------------------------------------
-    uint64_t excl = 0;
-    if (a.debug_skip & 1) {
-      excl = t * 4096;  // timing ablation: no look-back (output meaningless)
-    } else {
-      excl = lookback2(a.desc, a.gdesc, t, 0, a.err);
-      publish_incl(a.desc, a.gdesc, t, a.ntiles, excl + agg);
-    }
+    // ---- finish the previous tile (its look-back had this tile's passes to resolve) --------
+    if (pend.on) finish(pend);
+    pend.t = t;
+    pend.agg = agg;
+    pend.tend = tend;
+    pend.pidx0 = pidx0;
+    pend.pidx = pidx;
+    pend.base = base;
+    pend.on = true;
     stm.mark(5);
-
-    // ---- flush ----------------------------------------------------------------------------
-    const bool over = excl + agg > a.out_capacity;
-    if (over && l == 0) raise_error(a.err, kErrCapacity);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (!over && agg) {
-      uint8_t* const out = a.out;
-      const uint64_t A0 = (uint64_t)(uintptr_t)out + excl;
-      const uint64_t A1 = A0 + agg;
-      const uint64_t al = (A0 + 15) & ~15ull;
-      const uint64_t hl = al < A1 ? al : A1;
-      if (A0 + l < hl) *(uint8_t*)(uintptr_t)(A0 + l) = stg[16 + l];
-      if (A1 > al) {
-        const uint64_t top = A1 & ~15ull;
-        const uint32_t nb = (uint32_t)((top - al) >> 4);
-        const uint32_t so0 = 16u + (uint32_t)(al - A0);
-        const uint32_t rr = so0 & 3u;
-        for (uint32_t i = l; i < nb; i += 64) {
-          const uint32_t d = (so0 >> 2) + 4 * i;
-          const uint32_t v0 = stg32[d], v1 = stg32[d + 1], v2 = stg32[d + 2], v3 = stg32[d + 3],
-                         v4 = stg32[d + 4];
-          u32x4 v;
-          v.x = __builtin_amdgcn_alignbyte(v1, v0, rr);
-          v.y = __builtin_amdgcn_alignbyte(v2, v1, rr);
-          v.z = __builtin_amdgcn_alignbyte(v3, v2, rr);
-          v.w = __builtin_amdgcn_alignbyte(v4, v3, rr);
-          *(u32x4*)(uintptr_t)(al + 16ull * i) = v;
-        }
-        if (top + l < A1) *(uint8_t*)(uintptr_t)(top + l) = stg[16 + (uint32_t)(top - A0) + l];
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      const uint32_t nz16 = (uint32_t)((agg + 15) >> 4) + 1;
-      for (uint32_t i = l; i < nz16; i += 64) ((u32x4*)(stg + 16))[i] = (u32x4){0, 0, 0, 0};
-    }
-    // positions: add the tile's global offset (own stores, read back past L1)
-    if (a.pos) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      for (uint64_t i = pidx0 + l; i < pidx; i += 64)
-        a.pos_out[i] = load_agent(a.pos_out + i) + excl;
-      if (tend == N) {
-        const uint64_t tot = excl + agg;
-        for (uint64_t i = pidx + l; i <= a.npos; i += 64) a.pos_out[i] = tot;
-      }
-    }
-    if (tend == N && l == 0 && a.total_out) *a.total_out = excl + agg;
-    stm.mark(6);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     };
     if (t * T + T <= N) tile(std::true_type{});
     else tile(std::false_type{});
     if (PF) cur = nxt;
     else if (t + nwaves < a.ntiles) load_tile<S>(a, t + nwaves, cur);
   }  // tile loop
+  if (pend.on) finish(pend);
 }
 
 // Chunk-start bitmap + per-message framing status for a batch of flat messages.
