@@ -382,16 +382,23 @@ struct Stamps {
   }
 };
 
-// Blocks of `threads` threads the whole GPU keeps resident for kernel `fn` (occupancy API per
-// CU, minus `margin`, times the CU count).  Persistent kernels size their grid with it so that
-// every wave of the grid runs concurrently (a tile only ever waits on lower tiles).
-inline unsigned resident_blocks(const void* fn, int threads, int margin) {
+// Blocks of `threads` threads the whole GPU keeps resident for kernel `fn`: the occupancy API per
+// CU, capped by what the kernel's SGPR allocation allows (the API over-reports by one block per
+// CU for SGPR-heavy kernels on ROCm 7.2: MI355X_MICROARCH.md, "Occupancy API one block/CU high";
+// 800 SGPRs per SIMD, a wave holds ceil(sgprs/16)*16 + 16), minus `margin`, times the CU count.
+// Persistent kernels size their grid with it so that every wave of the grid runs concurrently
+// (a tile only ever waits on lower tiles).
+inline unsigned resident_blocks(const void* fn, int threads, int margin, int sgprs = 112) {
   int dev = 0, cus = 0, per_cu = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 256;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     cus = 256;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, 0) != hipSuccess)
     per_cu = 1;
+  const int waves_per_block = (threads + 63) / 64;
+  const int sgpr_waves = 800 / (((sgprs + 15) / 16) * 16 + 16);    // per SIMD
+  const int sgpr_blocks = sgpr_waves * 4 / waves_per_block;         // 4 SIMDs per CU
+  if (per_cu > sgpr_blocks) per_cu = sgpr_blocks;
   per_cu -= margin;
   if (per_cu < 1) per_cu = 1;
   return (unsigned)(per_cu * cus);
