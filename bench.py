@@ -155,39 +155,51 @@ def main():
     codec.sync()
     torch.cuda.synchronize()
     barrier()
-    codec.timing_read()  # discard
-    codec.timing(True)
-    torch.cuda.synchronize()
-    barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
     barrier()
     t1 = time.perf_counter()
-    codec.timing(False)
     codec.sync()
-    pack_ms, pl, unpack_ms, ul = codec.timing_read()
     dt = t1 - t0
 
     # correctness of what was timed: exact round trip + statuses
     ok = bool((pst == 0).all().item() and (ust == 0).all().item() and torch.equal(woff, off)
               and torch.equal(back, words[:total]))
 
-    red = reduce_step(dt, float(U), float(P), pack_ms / max(pl, 1), unpack_ms / max(ul, 1), ok,
+    # per-kernel durations: a second pass of the same steps with HIP events around every tile
+    # kernel, on the stream the kernels run on (kept out of the wall-clock pass above)
+    codec.timing_read_all()  # discard
+    codec.timing(True)
+    for _ in range(args.steps):
+        step()
+    codec.timing(False)
+    codec.sync()
+    kt = codec.timing_read_all()
+    kms = {k: (v[0] / v[1] if v[1] else 0.0) for k, v in kt.items()}
+
+    red = reduce_step(dt, float(U), float(P), kms["pack_tiles"], kms["unpack"], ok,
                       dist=dist, device=codec.device)
     dt_max, U_all = red["dt_max"], red["unpacked_all"]
-    pk_avg, up_avg = red["pack_ms"], red["unpack_ms"]
     ok_all = red["ok_all"]
 
     result = None
     if rank == 0:
         ms_per_step = dt_max / args.steps * 1e3
         value = U_all / (dt_max / args.steps) / 2**30
-        dom, dom_ms = ("pack_tiles", pk_avg) if pk_avg >= up_avg else ("unpack_body", up_avg)
-        algo = float(U + P)  # bytes one launch of either kernel moves (read+write), rank 0
-        achieved = algo / (dom_ms * 1e-3) / 1e9
-        rt = 2.0 * (U + P) / ((pk_avg + up_avg) * 1e-3) / 1e9
+        # algorithmic HBM bytes of one launch of each tile kernel
+        algo = {"pack_tiles": U + P, "unpack_index": P, "unpack_expand": U + P}
+        kern = {k: {"ms": round(kms[k], 4),
+                    "GBps": round(algo[k] / (kms[k] * 1e-3) / 1e9, 1) if kms[k] > 0 else None,
+                    "algorithmic_bytes": int(algo[k])} for k in algo}
+        for k in ("unpack_resolve", "unpack_fallback"):
+            kern[k] = {"ms": round(kms[k], 4)}
+        dom = max(algo, key=lambda k: kms[k])
+        dom_ms = kms[dom]
+        achieved = algo[dom] / (dom_ms * 1e-3) / 1e9
+        rt_ms = kms["pack_tiles"] + kms["unpack"]
+        rt = 2.0 * (U + P) / (rt_ms * 1e-3) / 1e9
         traffic = None
         tf = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
         if os.path.exists(tf):
@@ -226,9 +238,10 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "algorithmic_bytes_per_launch": int(algo),
-                "pack_ms": round(pk_avg, 4),
-                "unpack_ms": round(up_avg, 4),
+                "algorithmic_bytes_per_launch": int(algo[dom]),
+                "kernels": kern,
+                "pack_ms": round(kms["pack_tiles"], 4),
+                "unpack_ms": round(kms["unpack"], 4),
                 "roundtrip_GBps": round(rt, 1),
                 "roundtrip_frac": round(rt / HBM_PEAK_GBS, 4),
             },

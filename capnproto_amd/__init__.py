@@ -82,6 +82,7 @@ def load_library():
         "cpk_timing_enable": (C.c_int, [vp, C.c_int]),
         "cpk_timing_read": (C.c_int, [vp, C.POINTER(C.c_double), C.POINTER(u64),
                                       C.POINTER(C.c_double), C.POINTER(u64)]),
+        "cpk_timing_read_all": (C.c_int, [vp, C.POINTER(C.c_double), C.POINTER(u64)]),
     }
     for name, (res, args) in sigs.items():
         f = getattr(L, name)
@@ -238,6 +239,16 @@ class Codec:
         self._check(self.lib.cpk_timing_read(self.ctx, C.byref(pm), C.byref(pl), C.byref(um),
                                              C.byref(ul)), "cpk_timing_read")
         return pm.value, pl.value, um.value, ul.value
+
+    TIMERS = ("pack_tiles", "unpack", "unpack_index", "unpack_resolve", "unpack_expand",
+              "unpack_fallback")
+
+    def timing_read_all(self):
+        """{timer name: (summed ms, launches)} since the last read (include/cpk.h timers)."""
+        ms = (C.c_double * len(self.TIMERS))()
+        n = (C.c_uint64 * len(self.TIMERS))()
+        self._check(self.lib.cpk_timing_read_all(self.ctx, ms, n), "cpk_timing_read_all")
+        return {k: (ms[i], n[i]) for i, k in enumerate(self.TIMERS)}
 
     # ------------------------------------------------------------------ synthetic workloads
     def gen_offsets(self, nmsgs, nseg=1, seg_words=0, seed=0, first_msg=0, msg_stride=1,

@@ -21,9 +21,10 @@ struct cpk_ctx {
   // device staging for the *_host entry points
   void* stage[4] = {nullptr, nullptr, nullptr, nullptr};
   size_t stage_size[4] = {0, 0, 0, 0};
-  // measurement hooks
+  // measurement hooks: [0] pack tile kernel, [1] unpack (index .. fallback), [2 + stage] each
+  // unpack stage kernel (index, resolve, expand, fallback)
   bool timing = false;
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[2];  // [0] pack, [1] unpack
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[CPK_TIMERS];
   std::vector<hipEvent_t> pool;
 };
 
@@ -193,40 +194,55 @@ cpk_status pack_common(cpk_ctx* ctx, const uint64_t* d_words, uint64_t N, const 
 }
 
 struct UnpackScratch {
-  uint32_t* counter;
-  uint64_t* desc;
-  uint64_t* gdesc;
-  uint32_t* gcnt;
-  uint32_t* state;
   uint32_t* fail_flag;
   uint32_t* fail_count;
   uint32_t* scan_counter;
   uint64_t* scan_desc;
   size_t zero_bytes;
+  uint64_t* desc;
+  uint64_t* gdesc;
   uint64_t* tile_first;
   uint64_t* flat;
   int32_t* hdr_status;
   uint32_t* fail_list;
+  uint64_t* tm;
+  uint32_t* t_wex;
+  uint32_t* t_x0;
+  uint32_t* t_fms;
+  uint32_t* t_wpre;
+  uint32_t* t_wpost;
+  uint32_t* t_flags;
+  uint32_t* t_ent;
+  int32_t* t_delta;
   size_t total;
 };
 
+// Unpack scratch: per message ~40 B, per 4 KiB tile ~870 B (chain-0 masks 512 B, sub-tile word
+// prefixes 256 B, merge table 64 B, descriptors).  Only the fallback list state and the scan
+// descriptors need zeroing; every tile table is fully written before it is read.
 UnpackScratch carve_unpack(void* base, uint64_t ntiles, uint64_t n) {
   Carve c(base);
   UnpackScratch s;
-  s.counter = c.take<uint32_t>(4);
-  s.desc = c.take<uint64_t>(ntiles);
-  s.gdesc = c.take<uint64_t>((ntiles + 63) / 64);
-  s.gcnt = c.take<uint32_t>((ntiles + 63) / 64);
-  s.state = c.take<uint32_t>(ntiles);
   s.fail_flag = c.take<uint32_t>(n);
   s.fail_count = c.take<uint32_t>(4);
   s.scan_counter = c.take<uint32_t>(4);
   s.scan_desc = c.take<uint64_t>(cpk::scan_tiles(n + 1));
   s.zero_bytes = c.off;
+  s.desc = c.take<uint64_t>(ntiles);
+  s.gdesc = c.take<uint64_t>((ntiles + 63) / 64);
   s.tile_first = c.take<uint64_t>(ntiles);
   s.flat = c.take<uint64_t>(n + 1);
   s.hdr_status = c.take<int32_t>(n);
   s.fail_list = c.take<uint32_t>(n);
+  s.tm = c.take<uint64_t>(64 * ntiles);
+  s.t_wex = c.take<uint32_t>(64 * ntiles);
+  s.t_x0 = c.take<uint32_t>(ntiles);
+  s.t_fms = c.take<uint32_t>(ntiles);
+  s.t_wpre = c.take<uint32_t>(ntiles);
+  s.t_wpost = c.take<uint32_t>(ntiles);
+  s.t_flags = c.take<uint32_t>(ntiles);
+  s.t_ent = c.take<uint32_t>(ntiles);
+  s.t_delta = c.take<int32_t>(16 * ntiles);
   s.total = c.off;
   return s;
 }
@@ -281,21 +297,35 @@ cpk_status unpack_common(cpk_ctx* ctx, uint32_t mode, const uint8_t* d_packed, u
   a.in_end = d_in_end;
   a.mode = mode;
   a.ntiles = ntiles;
-  a.tile_counter = s.counter;
+  a.tile_counter = nullptr;
   a.desc = s.desc;
   a.gdesc = s.gdesc;
-  a.gcnt = s.gcnt;
-  a.state = s.state;
+  a.gcnt = nullptr;
+  a.state = nullptr;
   a.fail_flag = s.fail_flag;
   a.fail_list = s.fail_list;
   a.fail_count = s.fail_count;
   a.err = ctx->err;
-  a.stamps = cpk::debug_stamps(1);
+  a.stamps = nullptr;
   a.debug_skip = cpk::debug_skip();
+  a.tm = s.tm;
+  a.t_wex = s.t_wex;
+  a.t_x0 = s.t_x0;
+  a.t_fms = s.t_fms;
+  a.t_wpre = s.t_wpre;
+  a.t_wpost = s.t_wpost;
+  a.t_flags = s.t_flags;
+  a.t_delta = s.t_delta;
+  a.t_ent = s.t_ent;
   TimedLaunch tl(ctx, 1, stream);
-  e = cpk::launch_unpack_body(a, stream);
+  for (int stage = cpk::kUnpackIndex; stage <= cpk::kUnpackFallback; stage++) {
+    TimedLaunch tk(ctx, 2 + stage, stream);
+    e = cpk::launch_unpack_stage(stage, a, stream);
+    tk.done();
+    if (e != hipSuccess) return CPK_ERR_HIP;
+  }
   tl.done();
-  return hip_status(e);
+  return CPK_OK;
 }
 
 }  // namespace
@@ -354,7 +384,7 @@ cpk_status cpk_destroy(cpk_ctx* ctx) {
   (void)hipDeviceSynchronize();
   if (ctx->scratch) (void)hipFree(ctx->scratch);
   if (ctx->err) (void)hipFree(ctx->err);
-  for (int w = 0; w < 2; w++)
+  for (int w = 0; w < CPK_TIMERS; w++)
     for (auto& p : ctx->ev[w]) {
       (void)hipEventDestroy(p.first);
       (void)hipEventDestroy(p.second);
@@ -373,8 +403,7 @@ cpk_status cpk_reserve(cpk_ctx* ctx, uint64_t max_words, uint64_t max_packed_byt
   const uint64_t pt = (max_words + 63) / 64;  // covers every tile size
   size_t need = pack_scratch_bytes(max_words, pt);
   const uint64_t ut = (max_packed_bytes + cpk::kUnpackTileBytes - 1) / cpk::kUnpackTileBytes;
-  const size_t un = 16 + align16(16 * ut) + align16(8 * ut) + 16 * align16(8 * (max_items + 1)) +
-                    align16(8 * cpk::scan_tiles(max_items + 1)) + 64;
+  const size_t un = carve_unpack(nullptr, ut, max_items).total + 64;
   if (un > need) need = un;
   return ensure(&ctx->scratch, &ctx->scratch_size, need);
 }
@@ -653,11 +682,10 @@ cpk_status cpk_timing_enable(cpk_ctx* ctx, int on) {
   return CPK_OK;
 }
 
-cpk_status cpk_timing_read(cpk_ctx* ctx, double* pack_ms, uint64_t* pack_launches,
-                           double* unpack_ms, uint64_t* unpack_launches) {
+cpk_status cpk_timing_read_all(cpk_ctx* ctx, double* ms_out, uint64_t* launches) {
   if (!ctx) return CPK_ERR_INVALID_ARGUMENT;
-  double ms[2] = {0, 0};
-  for (int w = 0; w < 2; w++) {
+  double ms[CPK_TIMERS] = {0};
+  for (int w = 0; w < CPK_TIMERS; w++) {
     for (auto& p : ctx->ev[w]) {
       float t = 0;
       if (hipEventSynchronize(p.second) != hipSuccess ||
@@ -666,17 +694,28 @@ cpk_status cpk_timing_read(cpk_ctx* ctx, double* pack_ms, uint64_t* pack_launche
       ms[w] += t;
     }
   }
-  if (pack_ms) *pack_ms = ms[0];
-  if (unpack_ms) *unpack_ms = ms[1];
-  if (pack_launches) *pack_launches = ctx->ev[0].size();
-  if (unpack_launches) *unpack_launches = ctx->ev[1].size();
-  for (int w = 0; w < 2; w++) {
+  for (int w = 0; w < CPK_TIMERS; w++) {
+    if (ms_out) ms_out[w] = ms[w];
+    if (launches) launches[w] = ctx->ev[w].size();
     for (auto& p : ctx->ev[w]) {
       ctx->pool.push_back(p.first);
       ctx->pool.push_back(p.second);
     }
     ctx->ev[w].clear();
   }
+  return CPK_OK;
+}
+
+cpk_status cpk_timing_read(cpk_ctx* ctx, double* pack_ms, uint64_t* pack_launches,
+                           double* unpack_ms, uint64_t* unpack_launches) {
+  double ms[CPK_TIMERS];
+  uint64_t n[CPK_TIMERS];
+  const cpk_status st = cpk_timing_read_all(ctx, ms, n);
+  if (st != CPK_OK) return st;
+  if (pack_ms) *pack_ms = ms[0];
+  if (unpack_ms) *unpack_ms = ms[1];
+  if (pack_launches) *pack_launches = n[0];
+  if (unpack_launches) *unpack_launches = n[1];
   return CPK_OK;
 }
 

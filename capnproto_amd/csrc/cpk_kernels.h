@@ -70,7 +70,20 @@ struct UnpackArgs {
   uint32_t* err;
   unsigned long long* stamps;   // diagnostic build only (env CPK_STAMPS), else NULL
   uint32_t debug_skip;
+  // tile tables: index_kernel -> resolve_kernel -> expand_kernel (cpk_unpack.hip)
+  uint64_t* tm;                 // ntiles*64 chain-0 record-start masks (bit = byte of a sub-tile)
+  uint32_t* t_wex;              // ntiles*64 chain-0 words before each 64-byte sub-tile
+  uint32_t* t_x0;               // chain-0 exit (tile-relative; >= 1<<24: past the batch end)
+  uint32_t* t_fms;              // first message start (tile-relative; tile size if none)
+  uint32_t* t_wpre;             // chain-0 words before t_fms
+  uint32_t* t_wpost;            // words from the last message start on
+  uint32_t* t_flags;
+  int32_t* t_delta;             // ntiles*16: entry e's words minus chain 0's (INT32_MIN: no merge)
+  uint32_t* t_ent;              // true entry (tile-relative)
 };
+
+// Unpack stages (launch_unpack_stage), in launch order.
+constexpr int kUnpackIndex = 0, kUnpackResolve = 1, kUnpackExpand = 2, kUnpackFallback = 3;
 
 uint32_t debug_skip();
 
@@ -80,7 +93,7 @@ unsigned long long* debug_stamps(int which);
 hipError_t launch_unpack_header(const uint8_t* packed, const uint64_t* in_off, uint64_t n,
                                 uint64_t limit, uint64_t* flat, int32_t* hdr_status,
                                 int32_t* status, hipStream_t stream);
-hipError_t launch_unpack_body(const UnpackArgs& a, hipStream_t stream);
+hipError_t launch_unpack_stage(int stage, const UnpackArgs& a, hipStream_t stream);
 hipError_t launch_unpack_init(uint32_t mode, const uint64_t* in_off, const uint64_t* word_off,
                               uint64_t n, int32_t* status, uint64_t* size_out, hipStream_t stream);
 

@@ -606,10 +606,14 @@ int pack_steps() {
 
 template <int S, bool PF>
 hipError_t launch_pack_s(const PackTileArgs& a, hipStream_t stream) {
+  // persistent grid: every block resident (the stamp build has its own register footprint)
   static const unsigned cap =
       resident_blocks((const void*)pack_tiles_kernel<S, PF, false>, 256, 0);
+  static const unsigned cap_st =
+      resident_blocks((const void*)pack_tiles_kernel<S, PF, true>, 256, 0, 128);
   const uint64_t want = (a.ntiles + 3) / 4;
-  const unsigned blocks = (unsigned)(want < cap ? want : cap);
+  const unsigned c = a.stamps ? cap_st : cap;
+  const unsigned blocks = (unsigned)(want < c ? want : c);
   if (a.stamps)
     hipLaunchKernelGGL((pack_tiles_kernel<S, PF, true>), dim3(blocks), dim3(256), 0, stream, a);
   else

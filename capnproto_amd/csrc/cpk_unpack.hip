@@ -6,25 +6,33 @@
 // all segments.  A record is a tag byte, its non-zero bytes, and for tags 0x00 / 0xff a count
 // byte (plus 8*count raw bytes for 0xff); a run may not overshoot the words being read.
 //
-// Three launches per batch:
+// Record starts form a chain (next = p + record length) that restarts at every message start.
+// The batch of packed bytes is cut into 4 KiB tiles.  No kernel waits on another workgroup:
+// every hand-off is a kernel boundary.
 //   1. header_kernel    one thread per message: decodes the first word and the rest of the
 //                       segment table with the reference's checks; yields the flat size.
 //   2. scan             message word offsets (cpk_scan.hip).
-//   3. body_kernel      one wave per 4 KiB tile of the packed batch.  Record starts are a chain
-//                       (next = p + record length) that restarts at every message start.  Each
-//                       lane walks its 64-byte sub-tile speculatively from the sub-tile start;
-//                       lanes then agree on their true entries by a fixed-point iteration of
-//                       "entry = max(previous exits)", re-walking only where an entry misses the
-//                       speculative chain.  Across tiles the same idea runs optimistically: a
-//                       tile publishes the exit of the chain entered at its own first byte, the
-//                       successor uses it as its entry, and every tile verifies that its true
-//                       entry (its predecessor's published exit) leads to the exit it published.
-//                       A tile whose chains do not merge flags the message; flagged messages are
-//                       re-decoded serially by fallback_kernel (never seen on canonical input).
-//                       Word offsets come from a segmented (per message) decoupled look-back.
-//                       Records are then expanded one lane per record, 64 consecutive records at
-//                       a time, so output stores are coalesced; zero and raw runs are written
-//                       cooperatively by the whole wave.
+//   3. index_kernel     one wave per tile.  Resolves "chain 0", the chain entered at the tile's
+//                       first byte: each lane walks its 64-byte sub-tile speculatively, then a
+//                       fixed point settles every lane's true entry.  Stores chain 0's record-start
+//                       masks (512 B per tile), its exit, word counts, and for entries 1..15 whether
+//                       (and with what word difference) their chain merges into chain 0.
+//   4. resolve_kernel   one thread per tile.  The true entry is the predecessor's chain-0 exit
+//                       (exact when the predecessor's own entry merged -- which the predecessor's
+//                       thread checks -- or the predecessor holds a message start).  Checks that
+//                       this tile's entry merges (table, or a walk through global memory for an
+//                       entry past a raw run), words before the first message start, and writes
+//                       segmented tile values + 64-tile group aggregates for the word offsets.
+//                       An entry that does not merge flags its message for fallback_kernel.
+//   5. expand_kernel    one wave per tile.  Word offset by a look-back over the (final) tile
+//                       values, chain 0 patched for the true entry, then records are expanded
+//                       one lane per record, 64 consecutive records at a time (coalesced stores);
+//                       zero and raw runs are written cooperatively by the wave.
+//   6. fallback_kernel  flagged messages, decoded serially (one wave per message).  Canonical
+//                       dense streams never need it; long raw-run (text) streams whose tiles
+//                       chain 0 cannot synchronise with do.
+#include <limits.h>
+
 #include "cpk_device.h"
 #include "cpk_kernels.h"
 
@@ -36,6 +44,11 @@ constexpr int kB = (int)kUnpackTileBytes;  // 4096
 constexpr int kPad = 16;
 constexpr int kDead = 1 << 24;  // chain ran into the end of the batch
 constexpr uint64_t kSegBit = 1ull << 61;
+constexpr int kTab = 16;                    // entries 0..15 get a merge table
+constexpr int32_t kUnmerged = INT32_MIN;
+constexpr uint32_t kTileUnsettled = 1;      // lane fixed point hit its iteration cap
+constexpr uint32_t kTileHasStart = 2;       // a message starts inside the tile
+constexpr int kWalkCap = 1024;              // records a resolve thread walks before giving up
 
 // status codes (include/cpk.h)
 constexpr int32_t kOK = 0, kEOF = 1, kOvershoot = 2, kTooMany = 3, kTooLarge = 4, kInvalid = 5;
@@ -121,13 +134,15 @@ __global__ void header_kernel(const uint8_t* __restrict__ packed,
   status[m] = st;
 }
 
+// Byte length of a record from its tag and its count byte (tag 0x00: + count byte; 0xff: +
+// count byte + 8*count raw bytes).
+__device__ __forceinline__ int rec_len(uint32_t tag, uint32_t cnt) {
+  return 1 + __popc(tag) + ((tag == 0 || tag == 0xff) ? 1 : 0) + (tag == 0xff ? 8 * (int)cnt : 0);
+}
+
 // Record length at tile position p given the staged bytes (no clipping).
 __device__ __forceinline__ int record_len(const uint8_t* d, int p) {
-  const uint32_t tag = d[p];
-  int len = 1 + __popc(tag);
-  if (tag == 0) len += 1;
-  else if (tag == 0xff) len += 1 + 8 * (int)d[p + 9];
-  return len;
+  return rec_len(d[p], d[p + 9]);
 }
 
 struct SubTile {
@@ -165,14 +180,19 @@ __device__ __forceinline__ int walk(const uint8_t* d, const SubTile& st, int p, 
   return p;
 }
 
-// Lane-entry fixed point for a tile entry E.  In: spec chain (chain, sx).  In/out: e (entries).
-// Out: true record-start mask of the lane and its exit.
-__device__ __forceinline__ void resolve(const uint8_t* d, const SubTile& st, uint64_t chain,
-                                        int sx, int E, int& e, uint64_t& tm, int& out,
-                                        uint64_t& runm) {
+// Lane-entry fixed point for a tile entry E.  In: the speculative chain of the lane's sub-tile
+// (chain, exit sx).  In/out: e (entries).  Out: true record-start mask of the lane and its exit.
+// A lane's entry is the largest exit of the earlier lanes that hold a record start (a lane
+// covered by a longer record passes nothing on), never below its own start: a wrong far jump of
+// one speculative chain is then corrected in the next round instead of being carried from lane
+// to lane.  Returns false when the iteration cap is hit (the caller flags the tile).
+__device__ __forceinline__ bool settle(const uint8_t* d, const SubTile& st, uint64_t chain,
+                                       int sx, int E, int& e, uint64_t& tm, int& out,
+                                       uint64_t& runm) {
   const int l = lane_id();
-  for (int iter = 0; iter < 80; iter++) {
-    if (e >= st.end || e >= st.pend) {
+  for (int iter = 0; iter < 96; iter++) {
+    const bool pass = e >= st.end || e >= st.pend;
+    if (pass) {
       out = e >= st.pend ? kDead : e;
       tm = 0;
     } else if ((chain >> (e - st.s)) & 1) {
@@ -190,44 +210,14 @@ __device__ __forceinline__ void resolve(const uint8_t* d, const SubTile& st, uin
         tm = wm;
       }
     }
-    const uint32_t incl = wave_incl_max32((uint32_t)out);
+    const uint32_t incl = wave_incl_max32(pass ? 0u : (uint32_t)out);
     const int prev = (int)shfl32(incl, l > 0 ? l - 1 : 0);
-    const int en = l == 0 ? E : (prev > E ? prev : E);
-    if (!ballot(en != e)) break;
+    int en = l == 0 ? E : (prev > E ? prev : E);
+    if (l > 0 && en < st.s) en = st.s;
+    if (!ballot(en != e)) return true;
     e = en;
   }
-}
-
-// Position of the k-th set bit of m (k < popcount(m)).
-__device__ __forceinline__ int select_bit(uint64_t m, int k) {
-  int pos = 0;
-#pragma unroll
-  for (int w = 32; w >= 1; w >>= 1) {
-    const uint64_t low = m & ((1ull << w) - 1);
-    const int c = __popcll(low);
-    if (k >= c) {
-      k -= c;
-      m >>= w;
-      pos += w;
-    } else {
-      m = low;
-    }
-  }
-  return pos;
-}
-
-// Record r's tile position from the per-lane true masks (R = exclusive record prefix by lane).
-__device__ __forceinline__ int record_pos(uint32_t R, uint64_t tm, uint32_t r) {
-  int j = 0;
-#pragma unroll
-  for (int step = 32; step >= 1; step >>= 1) {
-    const int c = j + step;
-    const uint32_t Rc = shfl32(R, c <= 63 ? c : 63);
-    if (c <= 63 && Rc <= r) j = c;
-  }
-  const uint32_t Rj = shfl32(R, j);
-  const uint64_t mj = shfl64(tm, j);
-  return 64 * j + select_bit(mj, (int)(r - Rj));
+  return false;
 }
 
 struct Rec {
@@ -287,20 +277,22 @@ struct MsgInfo {
   bool ok, fits;
 };
 
-__device__ __forceinline__ MsgInfo msg_info(const UnpackArgs& a, uint64_t m) {
+// Message m's metadata.  check_flag: a message flagged for the fallback decoder counts as not ok
+// (the tile kernels leave it alone); the fallback itself passes false.
+__device__ __forceinline__ MsgInfo msg_info(const UnpackArgs& a, uint64_t m, bool check_flag) {
   MsgInfo mi;
   if (!a.word_off) {  // size-only mode
     mi.base = 0;
     mi.total = ~0ull >> 2;
     mi.end = a.in_off[m + 1];
-    mi.ok = true;
+    mi.ok = !(check_flag && a.fail_flag[m]);
     mi.fits = false;
     return mi;
   }
   mi.base = a.word_off[m];
   mi.total = a.word_off[m + 1] - mi.base;
   mi.end = a.in_off[m + 1];
-  mi.ok = a.hdr_status ? a.hdr_status[m] == kOK : true;
+  mi.ok = (a.hdr_status ? a.hdr_status[m] == kOK : true) && !(check_flag && a.fail_flag[m]);
   mi.fits = mi.base + mi.total <= a.words_capacity;
   return mi;
 }
@@ -428,7 +420,7 @@ struct MsgWin {
   uint64_t end;      // in_off[m + 1]
   uint64_t base;     // word_off[m]
   uint64_t total;    // word_off[m + 1] - word_off[m]
-  uint32_t ok;       // header accepted
+  uint32_t ok;       // header accepted and not left to the fallback decoder
 };
 
 __device__ __forceinline__ void load_win(const UnpackArgs& a, int64_t mw, MsgWin& w) {
@@ -444,7 +436,7 @@ __device__ __forceinline__ void load_win(const UnpackArgs& a, int64_t mw, MsgWin
       w.base = 0;
       w.total = ~0ull >> 2;
     }
-    w.ok = a.hdr_status ? a.hdr_status[m] == kOK : 1;
+    w.ok = (a.hdr_status ? a.hdr_status[m] == kOK : 1) && a.fail_flag[m] == 0;
   } else {
     w.start = ~0ull;
     w.end = ~0ull;
@@ -468,13 +460,81 @@ __device__ __forceinline__ void stage_tile(const UnpackArgs& a, uint64_t A, uint
       if (aligned && A + o + 16 <= P) {
         v = *(const u32x4*)(a.packed + A + o);
       } else {
-        uint8_t tmp[16];
-        for (int i = 0; i < 16; i++) tmp[i] = (A + o + i < P) ? a.packed[A + o + i] : 0;
-        v = *(const u32x4*)tmp;
+        uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0;
+        for (int i = 0; i < 16; i++) {
+          const uint32_t bv = (A + o + i < P) ? (uint32_t)a.packed[A + o + i] : 0u;
+          const uint32_t sv = bv << (8 * (i & 3));
+          if (i < 4) q0 |= sv;
+          else if (i < 8) q1 |= sv;
+          else if (i < 12) q2 |= sv;
+          else q3 |= sv;
+        }
+        v = (u32x4){q0, q1, q2, q3};
       }
       *(u32x4*)(d + o) = v;
     }
   }
+}
+
+// Message-start bitmap of tile [A, A + kB) into ms[64] (bit = tile-relative byte; the batch end
+// counts as a start when it falls inside the tile).  Returns one past the last message starting
+// in the tile; *nms_after = first message start at or after the tile end (tile-relative, capped
+// at the batch end).
+__device__ __forceinline__ uint64_t tile_msg_starts(const UnpackArgs& a, uint64_t A,
+                                                    uint64_t mfirst, uint64_t* ms,
+                                                    int* nms_after) {
+  const int l = lane_id();
+  const uint64_t P = a.nbytes;
+  ms[l] = 0;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  MsgWin w2;
+  load_win(a, (int64_t)mfirst - 1, w2);
+  uint64_t mlast;
+  for (;;) {
+    const bool in = l > 0 && w2.start >= A && w2.start < A + kB;
+    if (in) {
+      const uint64_t r = w2.start - A;
+      atomicOr((unsigned long long*)&ms[r >> 6], 1ull << (r & 63));
+    }
+    const uint64_t inm = ballot(in);
+    if (inm != (~0ull << 1)) {
+      mlast = (uint64_t)(w2.mw + 1 + __popcll(inm));
+      const uint64_t nx = mlast < a.nmsgs ? uniform64(a.in_off[mlast]) : P;
+      *nms_after = (int)((nx < P ? nx : P) - A);
+      break;
+    }
+    load_win(a, w2.mw + 63, w2);  // 63 starts in this window: continue with the next
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (P - A < (uint64_t)kB) {
+    const int pe = (int)(P - A);
+    atomicOr((unsigned long long*)&ms[pe >> 6], 1ull << (pe & 63));
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  return mlast;
+}
+
+// Sub-tile geometry of this lane: [64l, 64l + 64), message starts, the first message start
+// after the sub-tile (suffix minimum over the lanes).
+__device__ __forceinline__ SubTile make_subtile(uint64_t A, uint64_t P, uint64_t msw,
+                                                int nms_tile_after) {
+  const int l = lane_id();
+  SubTile st;
+  st.s = 64 * l;
+  st.end = st.s + 64;
+  st.pend = (P - A) < (uint64_t)kDead ? (int)(P - A) : kDead;
+  st.vend = st.end < st.pend ? st.end : st.pend;
+  st.msw = msw;
+  const int fs = st.msw ? st.s + lowest_bit(st.msw) : 0x7fffffff;
+  int v = fs;
+#pragma unroll
+  for (int dd = 1; dd < 64; dd <<= 1) {
+    const int o = (int)shfl32((uint32_t)v, l + dd <= 63 ? l + dd : l);
+    if (l + dd <= 63) v = o < v ? o : v;
+  }
+  const int nxt = (int)shfl32((uint32_t)v, l < 63 ? l + 1 : 63);
+  st.nms_after = (l < 63 && nxt != 0x7fffffff) ? nxt : nms_tile_after;
+  return st;
 }
 
 // v_perm selectors depositing the bytes that follow a tag into the word: byte i <- data byte
@@ -490,129 +550,385 @@ __device__ __forceinline__ uint64_t make_dep(uint32_t tag) {
   return sel;
 }
 
-// A tile whose look-back and expansion are deferred (see body_kernel).
-struct PendTile {
-  uint64_t t, A, mfirst, mlast, agg;
-  bool on, tile_has_start;
-};
-
-// 3. Body: one wave per 4 KiB tile, persistent waves over a static strided tile order.
-//   phase 1  stage, message starts, speculative walks, entries (published spec exit, the
-//            predecessor's exit), per-lane record masks, the tile's word count -> publish
-//   phase 2  (deferred until the wave's next tile has done phase 1, so the look-back has a
-//            whole phase to resolve) look-back, re-stage (L2), record list, expansion.
-template <bool STAMPS>
-__global__ __launch_bounds__(256) void body_kernel(UnpackArgs a) {
+// 3. Index: one wave per tile, chain 0 + merge table (see the file comment).
+__global__ __launch_bounds__(256) void index_kernel(UnpackArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds_data[4][kB + kPad];
   __shared__ uint64_t lds_ms[4][64];
+  __shared__ uint64_t lds_tm[4][64];
+  const int l = lane_id();
+  const int wv = (int)uniform32(threadIdx.x >> 6);
+  const uint64_t t = (uint64_t)blockIdx.x * 4 + wv;
+  if (t >= a.ntiles) return;
+  uint8_t* d = lds_data[wv];
+  const uint64_t P = a.nbytes;
+  const uint64_t A = t * kB;
+
+  stage_tile(a, A, d);
+  int nms_tile_after;
+  (void)tile_msg_starts(a, A, a.tile_first[t], lds_ms[wv], &nms_tile_after);
+  const SubTile st = make_subtile(A, P, lds_ms[wv][l], nms_tile_after);
+
+  // ---- chain 0: speculative walks, then the lane fixed point for entry 0 --------------------
+  uint64_t chain = 0, runm = 0;
+  int sx = kDead;
+  if (st.s < st.pend) sx = walk(d, st, st.s, 0, &chain, &runm);
+  int e = st.s;
+  uint64_t tm = 0;
+  int out = 0;
+  const bool settled = settle(d, st, chain, sx, 0, e, tm, out, runm);
+  const uint32_t x0 = readlane32((uint32_t)out, 63);
+
+  // first message start (the batch end counts), tile-relative; kB if none
+  const uint64_t msl = ballot(st.msw != 0);
+  const int fl = lowest_bit(msl);
+  const int fms = msl ? 64 * fl + lowest_bit(readlane64(st.msw, fl)) : kB;
+
+  // ---- words of chain 0: per lane, before fms, after the lane's last message start ----------
+  const uint64_t pre_m = fms <= st.s ? 0ull : (fms >= st.s + 64 ? ~0ull : mask_lt(fms - st.s));
+  uint32_t w_all = __popcll(tm), w_pre = __popcll(tm & pre_m), w_post = 0;
+  const uint64_t msin = tm & st.msw;
+  const int lastms = highest_bit(msin);
+  const bool has_ms = lastms >= 0;
+  if (has_ms) w_post = __popcll(tm & ~mask_lt(lastms));
+  const uint64_t rruns = tm & runm;
+  {
+    uint64_t rr = rruns;
+    while (rr) {
+      const int b = lowest_bit(rr);
+      rr &= rr - 1;
+      const int p = st.s + b;
+      const uint32_t c = d[p + 1 + __popc(d[p])];
+      w_all += c;
+      if ((pre_m >> b) & 1) w_pre += c;
+      if (has_ms && b >= lastms) w_post += c;
+    }
+  }
+  const uint32_t Wex = wave_incl_sum32(w_all) - w_all;
+  const uint32_t wpre0 = readlane32(wave_incl_sum32(w_pre), 63);
+  const uint64_t hm = ballot(has_ms);
+  const bool tile_has_start = hm != 0;
+  const int lm = highest_bit(hm);
+  const uint32_t contrib = (!tile_has_start || l > lm) ? w_all : (l == lm ? w_post : 0u);
+  const uint32_t wpost = readlane32(wave_incl_sum32(contrib), 63);
+  a.tm[t * 64 + l] = tm;
+  a.t_wex[t * 64 + l] = Wex;
+  lds_tm[wv][l] = tm;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+
+  // ---- merge table: lane e (1..15) walks the chain entered at byte e until it meets chain 0 --
+  int m = 0;
+  uint32_t ww = 0;
+  bool merged = true;
+  if (l >= 1 && l < kTab) {
+    int p = l;
+    for (int k = 0; k < kB; k++) {
+      if (p >= fms) {
+        if (fms < kB) m = fms;           // every chain restarts at the first message start
+        else if (p == (int)x0) m = kB;   // left the tile at chain 0's exit
+        else merged = false;
+        break;
+      }
+      if ((lds_tm[wv][p >> 6] >> (p & 63)) & 1) {
+        m = p;
+        break;
+      }
+      const uint32_t tag = d[p];
+      const uint32_t cnt = tag == 0 ? d[p + 1] : (tag == 0xff ? d[p + 9] : 0u);
+      ww += 1 + cnt;
+      p += rec_len(tag, cnt);
+    }
+  }
+  // chain-0 words before the merge point (all lanes take part in the shuffles)
+  const int L = (m >> 6) < 63 ? (m >> 6) : 63;
+  const uint64_t tmL = shfl64(tm, L);
+  const uint64_t rrL = shfl64(rruns, L);
+  const uint32_t WexL = shfl32(Wex, L);
+  int32_t delta = 0;
+  if (l >= 1 && l < kTab) {
+    if (!merged) {
+      delta = kUnmerged;
+    } else {
+      uint32_t w0;
+      if (m >= kB) {
+        w0 = wpre0;  // no message start in the tile: wpre0 counts every record
+      } else {
+        const int b = m & 63;
+        w0 = WexL + __popcll(tmL & mask_lt(b));
+        uint64_t r2 = rrL & mask_lt(b);
+        while (r2) {
+          const int bb = lowest_bit(r2);
+          r2 &= r2 - 1;
+          const int p = 64 * (m >> 6) + bb;
+          w0 += d[p + 1 + __popc(d[p])];
+        }
+      }
+      delta = (int32_t)(ww - w0);
+    }
+  }
+  if (l < kTab) a.t_delta[t * kTab + l] = delta;
+  if (l == 0) {
+    a.t_x0[t] = x0;
+    a.t_fms[t] = (uint32_t)fms;
+    a.t_wpre[t] = wpre0;
+    a.t_wpost[t] = wpost;
+    a.t_flags[t] = (settled ? 0u : kTileUnsettled) | (tile_has_start ? kTileHasStart : 0u);
+  }
+}
+
+// Walks the chain entered at tile-relative byte E of tile t through global memory until it meets
+// a chain-0 record start (or the first message start).  True when it merges; *wpre = words of
+// the records from E up to the first message start.
+__device__ bool walk_global(const UnpackArgs& a, uint64_t t, uint32_t E, uint32_t fms,
+                            uint32_t x0, uint32_t wpre0, uint32_t* wpre) {
+  const uint8_t* b = a.packed;
+  const uint64_t P = a.nbytes;
+  const uint64_t A = t * kB;
+  const uint64_t* tmt = a.tm + t * 64;
+  auto byte_at = [&](uint64_t q) -> uint32_t { return q < P ? (uint32_t)b[q] : 0u; };
+  uint32_t p = E, w = 0;
+  for (int k = 0; k < kWalkCap; k++) {
+    if (p >= fms) {
+      if (fms < (uint32_t)kB || p == x0) {
+        *wpre = w;
+        return true;
+      }
+      return false;
+    }
+    const uint64_t tmw = tmt[p >> 6];
+    if ((tmw >> (p & 63)) & 1) {
+      // merged at p: chain-0 words before p = sub-tile prefix + records of sub-tile p>>6 below p
+      const uint32_t L = p >> 6, bb = p & 63;
+      uint32_t w0 = a.t_wex[t * 64 + L] + (uint32_t)__popcll(tmw & mask_lt((int)bb));
+      uint64_t r = tmw & mask_lt((int)bb);
+      while (r) {
+        const int j = lowest_bit(r);
+        r &= r - 1;
+        const uint64_t q = A + 64 * L + j;
+        const uint32_t tag = byte_at(q);
+        if (tag == 0) w0 += byte_at(q + 1);
+        else if (tag == 0xff) w0 += byte_at(q + 9);
+      }
+      *wpre = w + (wpre0 - w0);
+      return true;
+    }
+    const uint64_t q = A + p;
+    const uint32_t tag = byte_at(q);
+    const uint32_t cnt = tag == 0 ? byte_at(q + 1) : (tag == 0xff ? byte_at(q + 9) : 0u);
+    w += 1 + cnt;
+    p += (uint32_t)rec_len(tag, cnt);
+  }
+  return false;
+}
+
+// 4. Resolve: one thread per tile (64 consecutive tiles per wave = one look-back group).
+__global__ __launch_bounds__(256) void resolve_kernel(UnpackArgs a) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int l = lane_id();
+  const bool valid = t < a.ntiles;
+  uint64_t v = 0;
+  if (valid) {
+    const uint32_t fms = a.t_fms[t];
+    const uint32_t flags = a.t_flags[t];
+    const uint32_t wpre0 = a.t_wpre[t];
+    uint32_t E = 0;
+    if (t > 0) {
+      const uint32_t xp = a.t_x0[t - 1];
+      E = xp >= (uint32_t)kDead ? (uint32_t)kB : xp - (uint32_t)kB;
+    }
+    if (E > fms) E = fms;
+    bool ok = true;
+    uint32_t wpre = 0;
+    if (E == 0) {
+      wpre = wpre0;
+    } else if (E >= fms) {
+      wpre = 0;
+    } else if (E < (uint32_t)kTab) {
+      const int32_t dl = a.t_delta[t * kTab + E];
+      if (dl == kUnmerged) ok = false;
+      else wpre = wpre0 + (uint32_t)dl;
+    } else {
+      ok = walk_global(a, t, E, fms, a.t_x0[t], wpre0, &wpre);
+    }
+    const uint64_t mf = a.tile_first[t];  // first message starting at or after the tile start
+    if (!ok && mf > 0) flag_message(a, mf - 1);
+    if (flags & kTileUnsettled) {
+      const uint64_t A = t * kB;
+      if (mf > 0) flag_message(a, mf - 1);
+      for (uint64_t m = mf; m < a.nmsgs && a.in_off[m] < A + kB; m++) flag_message(a, m);
+    }
+    a.t_ent[t] = E;
+    v = (flags & kTileHasStart) ? (kSegBit | a.t_wpost[t]) : (uint64_t)wpre;
+    a.desc[t] = kDescAgg | v;
+  }
+  // group aggregate (tiles 64g .. 64g+63 in lane order): words after the last restart
+  const uint64_t segm = ballot(valid && (v & kSegBit));
+  const int ls = highest_bit(segm);
+  const uint64_t c = (valid && l >= ls) ? (v & ~kSegBit) : 0;
+  const uint64_t sum = wave_sum64(c);
+  if (l == 0 && valid) a.gdesc[t / kGroup] = kDescAgg | (segm ? kSegBit : 0) | sum;
+}
+
+// 5. Expand: one wave per tile.
+__global__ __launch_bounds__(256) void expand_kernel(UnpackArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds_data[4][kB + kPad];
+  __shared__ uint64_t lds_ms[4][64];
+  __shared__ uint64_t lds_tm[4][64];
+  __shared__ uint64_t lds_fix[4][64];
   __shared__ uint16_t lds_list[4][kB / 4];  // record positions of half a tile (<= 1024)
   __shared__ uint64_t dep_tab[256];
   const int l = lane_id();
   const int wv = (int)uniform32(threadIdx.x >> 6);  // wave-uniform (keeps tile math scalar)
-  uint8_t* d = lds_data[wv];
-  uint16_t* list = lds_list[wv];
   dep_tab[threadIdx.x] = make_dep(threadIdx.x);
   __syncthreads();
+  const uint64_t t = (uint64_t)blockIdx.x * 4 + wv;
+  if (t >= a.ntiles) return;
+  uint8_t* d = lds_data[wv];
+  uint16_t* list = lds_list[wv];
   const uint32_t lut = deposit_sel((uint32_t)l & 15);
-  const uint64_t P = a.nbytes;
+  const uint64_t A = t * kB;
 
-  const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
-  Stamps<STAMPS> stm;
-  PendTile pend;
-  pend.on = false;
-  uint64_t ptm = 0, pmsw = 0;  // pending tile: this lane's record-start and message-start bits
+  stage_tile(a, A, d);
+  const uint64_t mfirst = a.tile_first[t];
+  int nms_after;
+  const uint64_t mlast = tile_msg_starts(a, A, mfirst, lds_ms[wv], &nms_after);
+  const uint64_t msw = lds_ms[wv][l];
+  uint64_t tm = a.tm[t * 64 + l];
+  const uint32_t E = a.t_ent[t];
+  const uint32_t fms = a.t_fms[t];
+  // words of the message at the tile start before this tile (tile values are final: no wait)
+  const uint64_t excl = lookback2(a.desc, a.gdesc, t, kSegBit, a.err);
+  MsgWin win;
+  load_win(a, (int64_t)mfirst - 1, win);
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 
-  // ---------------------------------------------------------------- phase 2 of a pending tile
-  auto finish = [&](const PendTile& pt, uint64_t tm, uint64_t msw) {
-    const uint64_t A = pt.A;
-    uint64_t excl = 0;
-    if (!(a.debug_skip & 1)) {
-      excl = lookback2(a.desc, a.gdesc, pt.t, kSegBit, a.err);
-      publish_incl(a.desc, a.gdesc, pt.t, a.ntiles, pt.tile_has_start ? pt.agg : excl + pt.agg);
-    }
-    stage_tile(a, A, d);
-    lds_ms[wv][l] = msw;
-    MsgWin win;
-    load_win(a, (int64_t)pt.mfirst - 1, win);
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    // Fast expansion when every message touching the tile is in the window, has a valid
-    // header, fits the output, and no two messages start at the same byte.
-    bool fast = a.mode == 0 && pt.mlast - (pt.mfirst - 1) <= 63 && a.word_off;
-    if (fast) {
-      const int64_t m = win.mw + l;
-      const bool inrange = m >= 0 && (uint64_t)m < pt.mlast;
-      const bool bad = inrange && (!win.ok || win.base + win.total > a.words_capacity);
-      const uint64_t nxs = shfl64(win.start, l < 63 ? l + 1 : 63);
-      const bool dup = inrange && l < 63 && (uint64_t)(m + 1) < pt.mlast && nxs == win.start;
-      fast = ballot(bad || dup) == 0;
-    }
-    const uint32_t cnt_all = __popcll(tm);
-    const uint32_t Rall_incl = wave_incl_sum32(cnt_all);
-    const uint32_t nrec = readlane32(Rall_incl, 63);
-    const uint32_t nfirst = readlane32(Rall_incl, 31);
-    if (nfirst > kB / 4 || nrec - nfirst > kB / 4) fast = false;  // list capacity (1-byte records)
-    if (!fast) {
-      // general path: one lane per record, record positions by binary search, message of each
-      // record from the window (see handle_record for the reference checks)
-      const uint32_t R = Rall_incl - cnt_all;
-      const uint64_t* msw_all = lds_ms[wv];
-      int64_t mcur = (int64_t)pt.mfirst - 1;
-      uint64_t nxt_start = readlane64(win.start, 1);
-      uint64_t sum = 0;
-      uint32_t base_key = 0;
-      for (uint32_t b0 = 0; b0 < nrec; b0 += 64) {
-        const uint32_t r = b0 + l;
-        const bool act = r < nrec;
-        const int rp = record_pos(R, tm, act ? r : 0);
-        const int p = act ? rp : 0;
-        const uint64_t pabs = A + p;
-        const Rec rc = read_rec(d, p);
-        const uint32_t w = act ? 1 + rc.cnt : 0;
-        const bool is_ms = act && ((msw_all[p >> 6] >> (p & 63)) & 1);
-        const uint32_t inc = wave_incl_sum32(w);
-        const uint64_t Sx = sum + inc - w;
-        const uint32_t key = is_ms ? (uint32_t)(Sx + 1) : 0;
-        uint32_t km = wave_incl_max32(key);
-        if (km < base_key) km = base_key;
-        const uint64_t wb = km ? Sx - (km - 1) : excl + Sx;
-        const uint32_t lastl = (nrec - b0 < 64 ? nrec - b0 : 64) - 1;
-        const uint64_t maxp = readlane64(pabs, (int)lastl);
-        int64_t m = mcur;
-        if (maxp >= nxt_start) {
-          bool found = false;
-          for (;;) {
-            int c = 0;
-#pragma unroll
-            for (int step = 32; step >= 1; step >>= 1) {
-              const uint64_t probe = shfl64(win.start, c + step <= 63 ? c + step : 63);
-              if (c + step <= 63 && probe <= pabs) c += step;
-            }
-            const bool beyond = act && c == 63 && readlane64(win.start, 63) <= pabs;
-            if (!found && !beyond) m = win.mw + c;
-            found = found || !beyond;
-            if (!ballot(beyond)) break;
-            load_win(a, win.mw + 63, win);
-          }
-          mcur = (int64_t)readlane64((uint64_t)m, (int)lastl);
-          if (mcur - win.mw >= 63) load_win(a, mcur, win);
-          nxt_start = readlane64(win.start, (int)(mcur - win.mw) + 1);
+  // ---- chain 0 -> the true chain: starts before the merge point come from a walk from E ----
+  if (E > 0) {
+    const bool pre_ok = readlane32(win.ok, 0) != 0;  // message holding the tile's first byte
+    int m = (int)fms;
+    lds_fix[wv][l] = 0;
+    if (pre_ok && E < fms) {
+      lds_tm[wv][l] = tm;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (l == 0) {
+        int p = (int)E;
+        uint64_t* fix = lds_fix[wv];
+        while (p < (int)fms && p < kB) {
+          if ((lds_tm[wv][p >> 6] >> (p & 63)) & 1) break;
+          fix[p >> 6] |= 1ull << (p & 63);
+          p += record_len(d, p);
         }
-        const int64_t wl64 = m - win.mw;
-        const bool inwin = wl64 >= 0 && wl64 < 64;
-        const int wl = inwin ? (int)wl64 : 0;
-        MsgInfo mi;
-        mi.base = shfl64(win.base, wl);
-        mi.total = shfl64(win.total, wl);
-        mi.end = shfl64(win.end, wl);
-        mi.ok = shfl32(win.ok, wl) != 0;
-        if (!inwin && act && m >= 0 && (uint64_t)m < a.nmsgs) mi = msg_info(a, (uint64_t)m);
-        mi.fits = a.word_off ? (mi.base + mi.total <= a.words_capacity) : false;
-        const uint64_t word = expand_word(d, p, rc.tag, lut);
-        RunJob job;
-        job.n = 0;
-        if (act && m >= 0 && (uint64_t)m < a.nmsgs) {
-          const int32_t st = handle_record(a, d, p, pabs, wb, mi, &job, word);
-          if (a.mode == 2) {
+        m = p < (int)fms ? p : (int)fms;
+      }
+      m = (int)readlane32((uint32_t)m, 0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    const int s = 64 * l;
+    const uint64_t below = m <= s ? 0ull : (m >= s + 64 ? ~0ull : mask_lt(m - s));
+    tm = (tm & ~below) | lds_fix[wv][l];
+  }
+
+  // Fast expansion when every message touching the tile is in the window, has a valid header,
+  // is not left to the fallback, fits the output, and no two messages start at the same byte.
+  bool fast = a.mode == 0 && mlast - (mfirst - 1) <= 63 && a.word_off;
+  if (fast) {
+    const int64_t m = win.mw + l;
+    const bool inrange = m >= 0 && (uint64_t)m < mlast;
+    const bool bad = inrange && (!win.ok || win.base + win.total > a.words_capacity);
+    const uint64_t nxs = shfl64(win.start, l < 63 ? l + 1 : 63);
+    const bool dup = inrange && l < 63 && (uint64_t)(m + 1) < mlast && nxs == win.start;
+    fast = ballot(bad || dup) == 0;
+  }
+  const uint32_t cnt_all = __popcll(tm);
+  const uint32_t Rall_incl = wave_incl_sum32(cnt_all);
+  const uint32_t nrec = readlane32(Rall_incl, 63);
+  const uint32_t nfirst = readlane32(Rall_incl, 31);
+  if (nfirst > kB / 4 || nrec - nfirst > kB / 4) fast = false;  // list capacity (1-byte records)
+  if (!fast) {
+    // general path: one lane per record, record positions by binary search, message of each
+    // record from the window (see handle_record for the reference checks)
+    const uint32_t R = Rall_incl - cnt_all;
+    const uint64_t* msw_all = lds_ms[wv];
+    int64_t mcur = (int64_t)mfirst - 1;
+    uint64_t nxt_start = readlane64(win.start, 1);
+    uint64_t sum = 0;
+    uint32_t base_key = 0;
+    for (uint32_t b0 = 0; b0 < nrec; b0 += 64) {
+      const uint32_t r = b0 + l;
+      const bool act = r < nrec;
+      const uint32_t rq = act ? r : 0;
+      // record position: lane j holding record r, then the (r - R_j)-th set bit of its mask
+      int j = 0;
+#pragma unroll
+      for (int step = 32; step >= 1; step >>= 1) {
+        const int c = j + step;
+        const uint32_t Rc = shfl32(R, c <= 63 ? c : 63);
+        if (c <= 63 && Rc <= rq) j = c;
+      }
+      const uint32_t Rj = shfl32(R, j);
+      uint64_t mj = shfl64(tm, j);
+      int k = (int)(rq - Rj), pos = 0;
+#pragma unroll
+      for (int w = 32; w >= 1; w >>= 1) {
+        const uint64_t low = mj & ((1ull << w) - 1);
+        const int c = __popcll(low);
+        if (k >= c) {
+          k -= c;
+          mj >>= w;
+          pos += w;
+        } else {
+          mj = low;
+        }
+      }
+      const int p = act ? 64 * j + pos : 0;
+      const uint64_t pabs = A + p;
+      const Rec rc = read_rec(d, p);
+      const uint32_t w = act ? 1 + rc.cnt : 0;
+      const bool is_ms = act && ((msw_all[p >> 6] >> (p & 63)) & 1);
+      const uint32_t inc = wave_incl_sum32(w);
+      const uint64_t Sx = sum + inc - w;
+      const uint32_t key = is_ms ? (uint32_t)(Sx + 1) : 0;
+      uint32_t km = wave_incl_max32(key);
+      if (km < base_key) km = base_key;
+      const uint64_t wb = km ? Sx - (km - 1) : excl + Sx;
+      const uint32_t lastl = (nrec - b0 < 64 ? nrec - b0 : 64) - 1;
+      const uint64_t maxp = readlane64(pabs, (int)lastl);
+      int64_t m = mcur;
+      if (maxp >= nxt_start) {
+        bool found = false;
+        for (;;) {
+          int c = 0;
+#pragma unroll
+          for (int step = 32; step >= 1; step >>= 1) {
+            const uint64_t probe = shfl64(win.start, c + step <= 63 ? c + step : 63);
+            if (c + step <= 63 && probe <= pabs) c += step;
+          }
+          const bool beyond = act && c == 63 && readlane64(win.start, 63) <= pabs;
+          if (!found && !beyond) m = win.mw + c;
+          found = found || !beyond;
+          if (!ballot(beyond)) break;
+          load_win(a, win.mw + 63, win);
+        }
+        mcur = (int64_t)readlane64((uint64_t)m, (int)lastl);
+        if (mcur - win.mw >= 63) load_win(a, mcur, win);
+        nxt_start = readlane64(win.start, (int)(mcur - win.mw) + 1);
+      }
+      const int64_t wl64 = m - win.mw;
+      const bool inwin = wl64 >= 0 && wl64 < 64;
+      const int wl = inwin ? (int)wl64 : 0;
+      MsgInfo mi;
+      mi.base = shfl64(win.base, wl);
+      mi.total = shfl64(win.total, wl);
+      mi.end = shfl64(win.end, wl);
+      mi.ok = shfl32(win.ok, wl) != 0;
+      if (!inwin && act && m >= 0 && (uint64_t)m < a.nmsgs) mi = msg_info(a, (uint64_t)m, true);
+      mi.fits = a.word_off ? (mi.base + mi.total <= a.words_capacity) : false;
+      const uint64_t word = expand_word(d, p, rc.tag, lut);
+      RunJob job;
+      job.n = 0;
+      if (act && m >= 0 && (uint64_t)m < a.nmsgs) {
+        const int32_t st = handle_record(a, d, p, pabs, wb, mi, &job, word);
+        if (a.mode == 2) {
+          if (mi.ok) {
             if (st == kInvalid) {
               a.status[m] = kInvalid;
               a.size_out[m] = 0;
@@ -620,256 +936,110 @@ __global__ __launch_bounds__(256) void body_kernel(UnpackArgs a) {
               a.status[m] = kOK;
               a.size_out[m] = wb + 1 + (rc.run ? rc.cnt : 0);
             }
-          } else if (st >= 0) {
-            a.status[m] = st;
-            if (a.in_end && (st == kOK || st == kTrailing || st == kCap)) a.in_end[m] = job.end;
           }
+        } else if (st >= 0) {
+          a.status[m] = st;
+          if (a.in_end && (st == kOK || st == kTrailing || st == kCap)) a.in_end[m] = job.end;
         }
-        run_jobs(a, job);
-        base_key = readlane32(km, 63);
-        sum += readlane32(inc, 63);
       }
-      return;
+      run_jobs(a, job);
+      base_key = readlane32(km, 63);
+      sum += readlane32(inc, 63);
     }
-    // fast path: record list per half tile (lanes 0-31, then 32-63), 64 records per batch
-    uint64_t sum = 0;        // words of the tile's records so far
-    uint32_t base_key = 0;   // key of the latest message start so far (key-max reset)
-    uint32_t mcount = 0;     // message starts so far
-    for (int h = 0; h < 2; h++) {
-      const bool mine = (l >> 5) == h;
-      uint64_t bits = mine ? tm : 0;
-      const uint32_t c = __popcll(bits);
-      const uint32_t Rin = wave_incl_sum32(c);
-      const uint32_t nh = readlane32(Rin, 63);
-      uint32_t r = Rin - c;
-      while (bits) {
-        const int b = lowest_bit(bits);
-        bits &= bits - 1;
-        const uint32_t ms = (uint32_t)((msw >> b) & 1);
-        list[r++] = (uint16_t)((64 * l + b) | (ms << 12));
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      for (uint32_t b0 = 0; b0 < nh; b0 += 64) {
-        const uint32_t rr = b0 + l;
-        const bool act = rr < nh;
-        const uint32_t e = act ? list[rr] : 0;
-        const int p = (int)(e & 0xfff);
-        const bool is_ms = act && ((e >> 12) & 1);
-        // bytes p .. p + 12: tag, up to 8 data bytes, count byte
-        const uint32_t* dw = (const uint32_t*)(d + (p & ~3));
-        const uint32_t sh = (uint32_t)p & 3;
-        const uint32_t q0 = dw[0], q1 = dw[1], q2 = dw[2], q3 = dw[3];
-        const uint32_t b0w = __builtin_amdgcn_alignbyte(q1, q0, sh);  // bytes p .. p+3
-        const uint32_t b1w = __builtin_amdgcn_alignbyte(q2, q1, sh);  // p+4 .. p+7
-        const uint32_t b2w = __builtin_amdgcn_alignbyte(q3, q2, sh);  // p+8 .. p+11
-        const uint32_t tag = b0w & 0xff;
-        const uint32_t dlo = __builtin_amdgcn_alignbyte(b1w, b0w, 1);  // data bytes 0..3
-        const uint32_t dhi = __builtin_amdgcn_alignbyte(b2w, b1w, 1);  // data bytes 4..7
-        const uint32_t nz = __popc(tag);
-        const bool z = tag == 0, f = tag == 0xff;
-        const uint32_t cnt = act ? (z ? ((b0w >> 8) & 0xff) : (f ? ((b2w >> 8) & 0xff) : 0u)) : 0u;
-        const uint32_t w = act ? 1 + cnt : 0;
-        const uint32_t inc = wave_incl_sum32(w);
-        const uint64_t Sx = sum + inc - w;
-        const uint32_t key = is_ms ? (uint32_t)(Sx + 1) : 0;
-        uint32_t km = wave_incl_max32(key);
-        if (km < base_key) km = base_key;
-        const uint64_t wb = km ? Sx - (km - 1) : excl + Sx;
-        const uint64_t msb = ballot(is_ms);
-        const int wl = (int)(mcount + (uint32_t)__popcll(msb & mask_le(l)));  // window lane
-        const uint64_t mbase = shfl64(win.base, wl);
-        const uint64_t mtotal = shfl64(win.total, wl);
-        const uint64_t mend = shfl64(win.end, wl);
-        const uint64_t sel = dep_tab[tag];
-        const uint32_t wlo = __builtin_amdgcn_perm(dhi, dlo, (uint32_t)sel);
-        const uint32_t whi = __builtin_amdgcn_perm(dhi, dlo, (uint32_t)(sel >> 32));
-        const uint64_t word = ((uint64_t)whi << 32) | wlo;
-        const uint32_t len = 1 + nz + ((z || f) ? 1 + (f ? 8 * cnt : 0) : 0);
-        const uint64_t pabs = A + p;
-        // records that end a message (or break it) go through the reference checks
-        const bool special = act && (wb + w >= mtotal || pabs + len >= mend);
-        RunJob job;
-        job.n = 0;
-        if (act && !special) {
-          a.words[mbase + wb] = word;
-          if (cnt) {
-            job.n = cnt;
-            job.dst = mbase + wb + 1;
-            job.raw = f;
-            job.src = pabs + 10;
-          }
-        } else if (special) {
-          MsgInfo mi;
-          mi.base = mbase;
-          mi.total = mtotal;
-          mi.end = mend;
-          mi.ok = true;
-          mi.fits = true;
-          const int64_t m = win.mw + wl;
-          const int32_t st = handle_record(a, d, p, pabs, wb, mi, &job, word);
-          if (st >= 0) {
-            a.status[m] = st;
-            if (a.in_end && (st == kOK || st == kTrailing || st == kCap)) a.in_end[m] = job.end;
-          }
+    return;
+  }
+  // fast path: record list per half tile (lanes 0-31, then 32-63), 64 records per batch
+  uint64_t sum = 0;        // words of the tile's records so far
+  uint32_t base_key = 0;   // key of the latest message start so far (key-max reset)
+  uint32_t mcount = 0;     // message starts so far
+  for (int h = 0; h < 2; h++) {
+    const bool mine = (l >> 5) == h;
+    uint64_t bits = mine ? tm : 0;
+    const uint32_t c = __popcll(bits);
+    const uint32_t Rin = wave_incl_sum32(c);
+    const uint32_t nh = readlane32(Rin, 63);
+    uint32_t r = Rin - c;
+    while (bits) {
+      const int b = lowest_bit(bits);
+      bits &= bits - 1;
+      const uint32_t ms = (uint32_t)((msw >> b) & 1);
+      list[r++] = (uint16_t)((64 * l + b) | (ms << 12));
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    for (uint32_t b0 = 0; b0 < nh; b0 += 64) {
+      const uint32_t rr = b0 + l;
+      const bool act = rr < nh;
+      const uint32_t e = act ? list[rr] : 0;
+      const int p = (int)(e & 0xfff);
+      const bool is_ms = act && ((e >> 12) & 1);
+      // bytes p .. p + 12: tag, up to 8 data bytes, count byte
+      const uint32_t* dw = (const uint32_t*)(d + (p & ~3));
+      const uint32_t sh = (uint32_t)p & 3;
+      const uint32_t q0 = dw[0], q1 = dw[1], q2 = dw[2], q3 = dw[3];
+      const uint32_t b0w = __builtin_amdgcn_alignbyte(q1, q0, sh);  // bytes p .. p+3
+      const uint32_t b1w = __builtin_amdgcn_alignbyte(q2, q1, sh);  // p+4 .. p+7
+      const uint32_t b2w = __builtin_amdgcn_alignbyte(q3, q2, sh);  // p+8 .. p+11
+      const uint32_t tag = b0w & 0xff;
+      const uint32_t dlo = __builtin_amdgcn_alignbyte(b1w, b0w, 1);  // data bytes 0..3
+      const uint32_t dhi = __builtin_amdgcn_alignbyte(b2w, b1w, 1);  // data bytes 4..7
+      const uint32_t nz = __popc(tag);
+      const bool z = tag == 0, f = tag == 0xff;
+      const uint32_t cnt = act ? (z ? ((b0w >> 8) & 0xff) : (f ? ((b2w >> 8) & 0xff) : 0u)) : 0u;
+      const uint32_t w = act ? 1 + cnt : 0;
+      const uint32_t inc = wave_incl_sum32(w);
+      const uint64_t Sx = sum + inc - w;
+      const uint32_t key = is_ms ? (uint32_t)(Sx + 1) : 0;
+      uint32_t km = wave_incl_max32(key);
+      if (km < base_key) km = base_key;
+      const uint64_t wb = km ? Sx - (km - 1) : excl + Sx;
+      const uint64_t msb = ballot(is_ms);
+      const int wl = (int)(mcount + (uint32_t)__popcll(msb & mask_le(l)));  // window lane
+      const uint64_t mbase = shfl64(win.base, wl);
+      const uint64_t mtotal = shfl64(win.total, wl);
+      const uint64_t mend = shfl64(win.end, wl);
+      const uint64_t sel = dep_tab[tag];
+      const uint32_t wlo = __builtin_amdgcn_perm(dhi, dlo, (uint32_t)sel);
+      const uint32_t whi = __builtin_amdgcn_perm(dhi, dlo, (uint32_t)(sel >> 32));
+      const uint64_t word = ((uint64_t)whi << 32) | wlo;
+      const uint32_t len = 1 + nz + ((z || f) ? 1 + (f ? 8 * cnt : 0) : 0);
+      const uint64_t pabs = A + p;
+      // records that end a message (or break it) go through the reference checks
+      const bool special = act && (wb + w >= mtotal || pabs + len >= mend);
+      RunJob job;
+      job.n = 0;
+      if (act && !special) {
+        a.words[mbase + wb] = word;
+        if (cnt) {
+          job.n = cnt;
+          job.dst = mbase + wb + 1;
+          job.raw = f;
+          job.src = pabs + 10;
         }
-        run_jobs(a, job);
-        base_key = readlane32(km, 63);
-        sum += readlane32(inc, 63);
-        mcount += (uint32_t)__popcll(msb);
+      } else if (special) {
+        MsgInfo mi;
+        mi.base = mbase;
+        mi.total = mtotal;
+        mi.end = mend;
+        mi.ok = true;
+        mi.fits = true;
+        const int64_t m = win.mw + wl;
+        const int32_t st = handle_record(a, d, p, pabs, wb, mi, &job, word);
+        if (st >= 0) {
+          a.status[m] = st;
+          if (a.in_end && (st == kOK || st == kTrailing || st == kCap)) a.in_end[m] = job.end;
+        }
       }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      run_jobs(a, job);
+      base_key = readlane32(km, 63);
+      sum += readlane32(inc, 63);
+      mcount += (uint32_t)__popcll(msb);
     }
-  };
-
-  for (uint64_t t = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wv; t < a.ntiles; t += nwaves) {
-  stm.start(a.stamps);
-  const uint64_t A = t * kB;
-
-  // ---- stage bytes [A, A + kB + kPad) -------------------------------------------------------
-  stage_tile(a, A, d);
-  // ---- message window (lane 0 = message holding byte A) and message-start bitmap --------------
-  const uint64_t mfirst = a.tile_first[t];
-  MsgWin win;
-  load_win(a, (int64_t)mfirst - 1, win);
-  lds_ms[wv][l] = 0;
-  uint64_t mlast;                     // one past the last message starting in [A, A + kB)
-  int nms_tile_after;                 // first message start >= A + kB (tile-relative)
-  {
-    MsgWin w2 = win;
-    for (;;) {
-      const bool in = l > 0 && w2.start >= A && w2.start < A + kB;
-      if (in) {
-        const uint64_t r = w2.start - A;
-        atomicOr((unsigned long long*)&lds_ms[wv][r >> 6], 1ull << (r & 63));
-      }
-      const uint64_t inm = ballot(in);
-      if (inm != (~0ull << 1)) {
-        const int c = __popcll(inm);
-        mlast = (uint64_t)(w2.mw + 1 + c);
-        const uint64_t nx = mlast < a.nmsgs ? uniform64(a.in_off[mlast]) : P;
-        nms_tile_after = (int)((nx < P ? nx : P) - A);
-        break;
-      }
-      load_win(a, w2.mw + 63, w2);  // 63 starts in this window: continue with the next
-    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  if (P - A < (uint64_t)kB) {
-    const int pe = (int)(P - A);
-    atomicOr((unsigned long long*)&lds_ms[wv][pe >> 6], 1ull << (pe & 63));
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-
-  stm.mark(0);  // staging + message window
-  SubTile st;
-  st.s = 64 * l;
-  st.end = st.s + 64;
-  st.pend = (int)(P - A) < kDead ? (int)(P - A) : kDead;
-  st.vend = st.end < st.pend ? st.end : st.pend;
-  st.msw = lds_ms[wv][l];
-  {
-    // first message start in a later sub-tile (suffix min over lanes)
-    const int fs = st.msw ? st.s + lowest_bit(st.msw) : 0x7fffffff;
-    int v = fs;
-#pragma unroll
-    for (int dd = 1; dd < 64; dd <<= 1) {
-      const int o = (int)shfl32((uint32_t)v, l + dd <= 63 ? l + dd : l);
-      if (l + dd <= 63) v = o < v ? o : v;
-    }
-    const int nxt = (int)shfl32((uint32_t)v, l < 63 ? l + 1 : 63);
-    st.nms_after = (l < 63 && nxt != 0x7fffffff) ? nxt : nms_tile_after;
-  }
-
-  // ---- speculative chains per sub-tile -------------------------------------------------------
-  uint64_t chain = 0, runm = 0;
-  int sx = kDead;
-  if (st.s < st.pend) sx = walk(d, st, st.s, 0, &chain, &runm);
-
-  stm.mark(1);  // speculative walks
-  // ---- tile entry: speculative (first byte) then true (predecessor's published exit) ---------
-  const bool a_is_start = lds_ms[wv][0] & 1;
-  int e = l == 0 ? 0 : st.s;
-  uint64_t tm = 0;
-  int out = 0;
-  resolve(d, st, chain, sx, 0, e, tm, out, runm);
-  const int spec_exit = (int)readlane32((uint32_t)out, 63);
-  if (l == 0) {
-    const uint32_t enc = spec_exit >= kDead ? 0xffffu : (uint32_t)(spec_exit - kB);
-    store_agent32(a.state + t, 0x80000000u | enc);
-  }
-  stm.mark(2);  // spec resolve + publish
-  if (!a_is_start && t > 0) {
-    const uint32_t v = wait_nonzero32(a.state + t - 1, a.err);
-    const int E = (v & 0xffffu) == 0xffffu ? kDead : (int)(v & 0xffffu);
-    if (E != 0) {
-      if (l == 0) e = E;
-      resolve(d, st, chain, sx, E, e, tm, out, runm);
-    }
-  }
-  {
-    // the exit published above must be the true one whenever the successor starts mid-message
-    const int true_exit = (int)readlane32((uint32_t)out, 63);
-    const bool next_is_start = nms_tile_after == kB;
-    if (true_exit != spec_exit && !next_is_start && A + kB < P) {
-      if (l == 0) flag_message(a, mlast - 1);
-    }
-  }
-
-  stm.mark(3);  // entry wait + true resolve
-  // ---- tile aggregate: words per lane, segmented by message starts ---------------------------
-  const uint32_t cnt = __popcll(tm);
-  uint64_t w_all = cnt, w_post = 0;
-  bool has_ms = false;
-  {
-    uint64_t rr = tm & runm;
-    const uint64_t msin = tm & st.msw;  // message starts that are records of this lane
-    const int lastms = highest_bit(msin);
-    has_ms = lastms >= 0;
-    if (has_ms) w_post = __popcll(tm & ~mask_lt(lastms));
-    while (rr) {
-      const int b = lowest_bit(rr);
-      rr &= rr - 1;
-      const int p = st.s + b;
-      const uint32_t tag = d[p];
-      const uint32_t c = d[p + 1 + __popc(tag)];
-      w_all += c;
-      if (has_ms && b >= lastms) w_post += c;
-    }
-  }
-  uint64_t agg;
-  bool tile_has_start;
-  {
-    const uint64_t hm = ballot(has_ms);
-    tile_has_start = hm != 0;
-    const int lm = highest_bit(hm);
-    // words after the last message start = w_post of that lane + w_all of later lanes
-    const uint64_t contrib = (!tile_has_start || l > lm) ? w_all : (l == lm ? w_post : 0);
-    agg = wave_sum64(contrib);
-  }
-  const uint64_t agg_desc = tile_has_start ? (kSegBit | agg) : agg;
-  if (!(a.debug_skip & 1))
-    publish_agg(a.desc, a.gdesc, a.gcnt, t, a.ntiles, agg_desc, kSegBit, a.err);
-  stm.mark(4);  // aggregate
-
-  // ---- phase 2 of the previous tile, then this tile becomes the pending one ----------------
-  if (pend.on) finish(pend, ptm, pmsw);
-  pend.t = t;
-  pend.A = A;
-  pend.mfirst = mfirst;
-  pend.mlast = mlast;
-  pend.agg = agg;
-  pend.tile_has_start = tile_has_start;
-  pend.on = true;
-  ptm = tm;
-  pmsw = st.msw;
-  stm.mark(5);  // deferred look-back + expansion
-  if (STAMPS && l == 0 && a.stamps) atomicAdd(a.stamps + 15, 1ull);
-  }  // tile loop
-  if (pend.on) finish(pend, ptm, pmsw);
 }
 
-// Serial re-decode of flagged messages: lane 0 walks the records of a 4 KiB window, then the
-// wave expands them with the same record handler as body_kernel.
+// 6. Serial re-decode of flagged messages: one wave per message; lane 0 walks the records of a
+// 4 KiB window, then the wave expands them with the same record handler as expand_kernel.
 __global__ __launch_bounds__(64) void fallback_kernel(UnpackArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t d[kB + kPad];
   __shared__ uint16_t rpos[kB];
@@ -880,7 +1050,7 @@ __global__ __launch_bounds__(64) void fallback_kernel(UnpackArgs a) {
   const uint32_t nfail = *a.fail_count;
   for (uint32_t fi = blockIdx.x; fi < nfail; fi += gridDim.x) {
     const uint64_t m = a.fail_list[fi];
-    const MsgInfo mi = msg_info(a, m);
+    const MsgInfo mi = msg_info(a, m, false);
     if (!mi.ok) continue;
     uint64_t pos = a.in_off[m];
     const uint64_t mend = mi.end;
@@ -986,18 +1156,24 @@ hipError_t launch_unpack_header(const uint8_t* packed, const uint64_t* in_off, u
   return hipGetLastError();
 }
 
-hipError_t launch_unpack_body(const UnpackArgs& a, hipStream_t stream) {
+hipError_t launch_unpack_stage(int stage, const UnpackArgs& a, hipStream_t stream) {
   if (a.ntiles == 0) return hipSuccess;
-  static const unsigned cap = resident_blocks((const void*)body_kernel<false>, 256, 0);
-  const uint64_t want = (a.ntiles + 3) / 4;
-  const unsigned blocks = (unsigned)(want < cap ? want : cap);
-  if (a.stamps)
-    hipLaunchKernelGGL(body_kernel<true>, dim3(blocks), dim3(256), 0, stream, a);
-  else
-    hipLaunchKernelGGL(body_kernel<false>, dim3(blocks), dim3(256), 0, stream, a);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(fallback_kernel, dim3(256), dim3(64), 0, stream, a);
+  const unsigned wave_blocks = (unsigned)((a.ntiles + 3) / 4);
+  switch (stage) {
+    case kUnpackIndex:
+      hipLaunchKernelGGL(index_kernel, dim3(wave_blocks), dim3(256), 0, stream, a);
+      break;
+    case kUnpackResolve:
+      hipLaunchKernelGGL(resolve_kernel, dim3((unsigned)((a.ntiles + 255) / 256)), dim3(256), 0,
+                         stream, a);
+      break;
+    case kUnpackExpand:
+      hipLaunchKernelGGL(expand_kernel, dim3(wave_blocks), dim3(256), 0, stream, a);
+      break;
+    default:
+      hipLaunchKernelGGL(fallback_kernel, dim3(2048), dim3(64), 0, stream, a);
+      break;
+  }
   return hipGetLastError();
 }
 

@@ -221,13 +221,18 @@ cpk_status cpk_gen_offsets(cpk_ctx* ctx, uint64_t seed, uint64_t first_msg,
                            uint64_t* total_words_out, void* stream);
 
 /* ------------------------------------------------------------------------------------------
- * Measurement hooks (bench.py).  When enabled, every pack / unpack call brackets its main tile
- * kernel (pack: the tile encoder; unpack: the body decoder + fallback) with HIP events on the
- * call's stream.  cpk_timing_read synchronises those events, returns the summed milliseconds
- * and launch counts since the last read, and clears them. */
+ * Measurement hooks (bench.py).  When enabled, every pack / unpack call brackets its tile
+ * kernels with HIP events on the call's stream: timer 0 the pack tile encoder, timer 1 the
+ * unpack tile kernels together (index, resolve, expand, fallback), timers 2..5 each of those
+ * four alone.  cpk_timing_read synchronises the events, returns the summed milliseconds and
+ * launch counts of timers 0 and 1 since the last read, and clears every timer;
+ * cpk_timing_read_all does the same for all CPK_TIMERS timers. */
+#define CPK_TIMERS 6
 cpk_status cpk_timing_enable(cpk_ctx* ctx, int on);
 cpk_status cpk_timing_read(cpk_ctx* ctx, double* pack_ms, uint64_t* pack_launches,
                            double* unpack_ms, uint64_t* unpack_launches);
+cpk_status cpk_timing_read_all(cpk_ctx* ctx, double* ms /* CPK_TIMERS */,
+                               uint64_t* launches /* CPK_TIMERS */);
 
 #ifdef __cplusplus
 }  /* extern "C" */

@@ -203,3 +203,40 @@ def test_device_round_trip_generated(codec, profile):
     assert (st2.cpu() == 0).all()
     assert torch.equal(woff, off)
     assert torch.equal(back[:total], words[:total])
+
+
+@pytest.mark.parametrize("first,stride", [(0, 1), (3, 8)])
+def test_c5_mixed_sizes_round_trip(codec, oracle, first, stride):
+    """Config C5's shape (mixed profiles, 2^k-word messages, round-robin shard): device pack
+    equals the oracle's bytes, device unpack restores every message."""
+    import torch
+
+    n = 6000
+    off, total = codec.gen_offsets(n, nseg=1, seg_words=0, seed=11, first_msg=first,
+                                   msg_stride=stride)
+    words = codec.gen_messages("mixed", off, total, nseg=1, seed=11, first_msg=first,
+                               msg_stride=stride)
+    packed, moff, st = codec.pack_messages(words, off)
+    codec.sync()
+    P = int(moff[-1].item())
+    ref, roff, rst = oracle.pack_batch(words.cpu().numpy().view(np.uint64),
+                                       off.cpu().numpy().astype(np.uint64))
+    assert (st.cpu().numpy() == 0).all()
+    assert (moff.cpu().numpy() == roff.astype(np.int64)).all()
+    assert packed[:P].cpu().numpy().tobytes() == ref.tobytes()
+    back, woff, st2 = codec.unpack_messages(packed, moff, total, nbytes=P)
+    codec.sync()
+    s2 = st2.cpu().numpy()
+    assert (s2 == 0).all(), np.nonzero(s2)[0][:10]
+    assert torch.equal(woff, off)
+    assert torch.equal(back[:total], words[:total])
+
+
+def test_text_messages_many_tiles(codec, oracle):
+    """Long raw-run streams: tiles whose first bytes sit inside raw data (fallback decoder)."""
+    rng = np.random.default_rng(31)
+    msgs = []
+    for n in (512, 700, 1500, 2048, 4000, 9000):
+        m = cases.flat_message(rng, 1, [n], "text")
+        msgs.append(oracle.pack_flat(m)[0])
+    check_against_oracle(codec, oracle, msgs)
