@@ -214,6 +214,12 @@ struct UnpackScratch {
   uint32_t* t_flags;
   uint32_t* t_ent;
   int32_t* t_delta;
+  uint32_t* t_xe;
+  uint32_t* t_umask;
+  uint32_t* r1_x;
+  uint32_t* r1_w;
+  uint64_t* g_notok;
+  uint64_t* g_start;
   size_t total;
 };
 
@@ -243,6 +249,12 @@ UnpackScratch carve_unpack(void* base, uint64_t ntiles, uint64_t n) {
   s.t_flags = c.take<uint32_t>(ntiles);
   s.t_ent = c.take<uint32_t>(ntiles);
   s.t_delta = c.take<int32_t>(16 * ntiles);
+  s.t_xe = c.take<uint32_t>(16 * ntiles);
+  s.t_umask = c.take<uint32_t>(ntiles);
+  s.r1_x = c.take<uint32_t>(ntiles);
+  s.r1_w = c.take<uint32_t>(ntiles);
+  s.g_notok = c.take<uint64_t>((ntiles + 63) / 64);
+  s.g_start = c.take<uint64_t>((ntiles + 63) / 64);
   s.total = c.off;
   return s;
 }
@@ -306,7 +318,7 @@ cpk_status unpack_common(cpk_ctx* ctx, uint32_t mode, const uint8_t* d_packed, u
   a.fail_list = s.fail_list;
   a.fail_count = s.fail_count;
   a.err = ctx->err;
-  a.stamps = nullptr;
+  a.stamps = cpk::debug_stamps(1);  // diagnostic counters (CPK_STAMPS=1), else NULL
   a.debug_skip = cpk::debug_skip();
   a.tm = s.tm;
   a.t_wex = s.t_wex;
@@ -316,6 +328,12 @@ cpk_status unpack_common(cpk_ctx* ctx, uint32_t mode, const uint8_t* d_packed, u
   a.t_wpost = s.t_wpost;
   a.t_flags = s.t_flags;
   a.t_delta = s.t_delta;
+  a.t_xe = s.t_xe;
+  a.t_umask = s.t_umask;
+  a.r1_x = s.r1_x;
+  a.r1_w = s.r1_w;
+  a.g_notok = s.g_notok;
+  a.g_start = s.g_start;
   a.t_ent = s.t_ent;
   TimedLaunch tl(ctx, 1, stream);
   for (int stage = cpk::kUnpackIndex; stage <= cpk::kUnpackFallback; stage++) {

@@ -78,7 +78,13 @@ struct UnpackArgs {
   uint32_t* t_wpre;             // chain-0 words before t_fms
   uint32_t* t_wpost;            // words from the last message start on
   uint32_t* t_flags;
-  int32_t* t_delta;             // ntiles*16: entry e's words minus chain 0's (INT32_MIN: no merge)
+  int32_t* t_delta;             // ntiles*16: entry e's words minus chain 0's (no merge: its words)
+  uint32_t* t_xe;               // ntiles*16: exit of entry e's chain when it does not merge
+  uint32_t* t_umask;            // bit e: entry e's chain does not merge into chain 0
+  uint32_t* r1_x;               // resolve pass 1: exit under the optimistic entry
+  uint32_t* r1_w;               // resolve pass 1: words before the first message start
+  uint64_t* g_notok;            // per 64 tiles: optimistic entry did not merge
+  uint64_t* g_start;            // per 64 tiles: tile holds a message start
   uint32_t* t_ent;              // true entry (tile-relative)
 };
 

@@ -45,10 +45,9 @@ constexpr int kPad = 16;
 constexpr int kDead = 1 << 24;  // chain ran into the end of the batch
 constexpr uint64_t kSegBit = 1ull << 61;
 constexpr int kTab = 16;                    // entries 0..15 get a merge table
-constexpr int32_t kUnmerged = INT32_MIN;
 constexpr uint32_t kTileUnsettled = 1;      // lane fixed point hit its iteration cap
 constexpr uint32_t kTileHasStart = 2;       // a message starts inside the tile
-constexpr int kWalkCap = 1024;              // records a resolve thread walks before giving up
+constexpr int kWalkCap = 4096;              // records a resolve thread walks before giving up
 
 // status codes (include/cpk.h)
 constexpr int32_t kOK = 0, kEOF = 1, kOvershoot = 2, kTooMany = 3, kTooLarge = 4, kInvalid = 5;
@@ -406,10 +405,17 @@ __device__ __forceinline__ void run_jobs(const UnpackArgs& a, const RunJob& job)
   }
 }
 
+// Diagnostic counters (env CPK_STAMPS=1 only; a.stamps is NULL otherwise).
+enum : int { kDbgUnsettled = 0, kDbgTableMiss, kDbgWalkFail, kDbgWalks, kDbgFlagged };
+__device__ __forceinline__ void dbg_count(const UnpackArgs& a, int slot) {
+  if (a.stamps) atomicAdd(a.stamps + slot, 1ull);
+}
+
 __device__ __forceinline__ void flag_message(const UnpackArgs& a, uint64_t m) {
   if (atomicExch(a.fail_flag + m, 1u) == 0) {
     const uint32_t i = atomicAdd(a.fail_count, 1u);
     a.fail_list[i] = (uint32_t)m;
+    dbg_count(a, kDbgFlagged);
   }
 }
 
@@ -446,15 +452,43 @@ __device__ __forceinline__ void load_win(const UnpackArgs& a, int64_t mw, MsgWin
   }
 }
 
-// Stages packed bytes [A, A + kB + kPad) of the batch into d (zero past the end).
-__device__ __forceinline__ void stage_tile(const UnpackArgs& a, uint64_t A, uint8_t* d) {
-  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+// Starts only (index_kernel needs no more of the window).
+__device__ __forceinline__ void load_starts(const UnpackArgs& a, int64_t mw, MsgWin& w) {
+  const int64_t m = mw + lane_id();
+  w.mw = mw;
+  w.start = (m >= 0 && (uint64_t)m < a.nmsgs) ? a.in_off[m] : ~0ull;
+  w.end = ~0ull;
+  w.base = 0;
+  w.total = 0;
+  w.ok = 0;
+}
+
+// Packed bytes [A, A + kB + kPad) of the batch (zero past the end) in 16-byte pieces per lane:
+// loaded into registers first (stage_load) so that other independent loads can be issued before
+// the wave waits for them, then written to LDS (stage_store).
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+constexpr int kStageVecs = (kB + kPad + 1023) / 1024;
+struct Staged {
+  u32x4 v[kStageVecs];
+};
+
+__device__ __forceinline__ void stage_store(const Staged& sg, uint8_t* d) {
+  const int l = lane_id();
+#pragma unroll
+  for (int k = 0; k < kStageVecs; k++) {
+    const int o = 16 * (64 * k + l);
+    if (o < kB + kPad) *(u32x4*)(d + o) = sg.v[k];
+  }
+}
+
+__device__ __forceinline__ void stage_load(const UnpackArgs& a, uint64_t A, Staged& sg) {
   const int l = lane_id();
   const uint64_t P = a.nbytes;
   const bool aligned = ((uintptr_t)a.packed & 15) == 0;
 #pragma unroll
-  for (int k = 0; k < (kB + kPad) / 1024 + 1; k++) {
+  for (int k = 0; k < kStageVecs; k++) {
     const int o = 16 * (64 * k + l);
+    sg.v[k] = (u32x4){0, 0, 0, 0};
     if (o < kB + kPad) {
       u32x4 v = {0, 0, 0, 0};
       if (aligned && A + o + 16 <= P) {
@@ -471,24 +505,35 @@ __device__ __forceinline__ void stage_tile(const UnpackArgs& a, uint64_t A, uint
         }
         v = (u32x4){q0, q1, q2, q3};
       }
-      *(u32x4*)(d + o) = v;
+      sg.v[k] = v;
     }
   }
+}
+
+__device__ __forceinline__ void stage_tile(const UnpackArgs& a, uint64_t A, uint8_t* d) {
+  Staged sg;
+  stage_load(a, A, sg);
+  stage_store(sg, d);
 }
 
 // Message-start bitmap of tile [A, A + kB) into ms[64] (bit = tile-relative byte; the batch end
 // counts as a start when it falls inside the tile).  Returns one past the last message starting
 // in the tile; *nms_after = first message start at or after the tile end (tile-relative, capped
-// at the batch end).
+// at the batch end).  first != NULL: full windows, the first one (lane 0 = message mfirst-1)
+// returned; else message starts only.
 __device__ __forceinline__ uint64_t tile_msg_starts(const UnpackArgs& a, uint64_t A,
                                                     uint64_t mfirst, uint64_t* ms,
-                                                    int* nms_after) {
+                                                    int* nms_after, MsgWin* first) {
   const int l = lane_id();
   const uint64_t P = a.nbytes;
   ms[l] = 0;
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   MsgWin w2;
-  load_win(a, (int64_t)mfirst - 1, w2);
+  if (first) {
+    load_win(a, (int64_t)mfirst - 1, w2);
+    *first = w2;
+  } else {
+    load_starts(a, (int64_t)mfirst - 1, w2);
+  }
   uint64_t mlast;
   for (;;) {
     const bool in = l > 0 && w2.start >= A && w2.start < A + kB;
@@ -503,7 +548,9 @@ __device__ __forceinline__ uint64_t tile_msg_starts(const UnpackArgs& a, uint64_
       *nms_after = (int)((nx < P ? nx : P) - A);
       break;
     }
-    load_win(a, w2.mw + 63, w2);  // 63 starts in this window: continue with the next
+    // 63 starts in this window: continue with the next
+    if (first) load_win(a, w2.mw + 63, w2);
+    else load_starts(a, w2.mw + 63, w2);
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   if (P - A < (uint64_t)kB) {
@@ -553,19 +600,22 @@ __device__ __forceinline__ uint64_t make_dep(uint32_t tag) {
 // 3. Index: one wave per tile, chain 0 + merge table (see the file comment).
 __global__ __launch_bounds__(256) void index_kernel(UnpackArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds_data[4][kB + kPad];
-  __shared__ uint64_t lds_ms[4][64];
-  __shared__ uint64_t lds_tm[4][64];
+  __shared__ uint64_t lds_ms[4][64];  // message starts, then chain-0 masks (merge table)
   const int l = lane_id();
   const int wv = (int)uniform32(threadIdx.x >> 6);
   const uint64_t t = (uint64_t)blockIdx.x * 4 + wv;
   if (t >= a.ntiles) return;
   uint8_t* d = lds_data[wv];
+  uint64_t* lds_tm = lds_ms[wv];
   const uint64_t P = a.nbytes;
   const uint64_t A = t * kB;
 
-  stage_tile(a, A, d);
+  Staged stg;
+  stage_load(a, A, stg);
+  const uint64_t mfirst = uniform64(a.tile_first[t]);
+  stage_store(stg, d);
   int nms_tile_after;
-  (void)tile_msg_starts(a, A, a.tile_first[t], lds_ms[wv], &nms_tile_after);
+  (void)tile_msg_starts(a, A, mfirst, lds_ms[wv], &nms_tile_after, nullptr);
   const SubTile st = make_subtile(A, P, lds_ms[wv][l], nms_tile_after);
 
   // ---- chain 0: speculative walks, then the lane fixed point for entry 0 --------------------
@@ -612,23 +662,22 @@ __global__ __launch_bounds__(256) void index_kernel(UnpackArgs a) {
   const uint32_t wpost = readlane32(wave_incl_sum32(contrib), 63);
   a.tm[t * 64 + l] = tm;
   a.t_wex[t * 64 + l] = Wex;
-  lds_tm[wv][l] = tm;
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  lds_tm[l] = tm;
 
-  // ---- merge table: lane e (1..15) walks the chain entered at byte e until it meets chain 0 --
-  int m = 0;
+  // ---- merge table: lane e (1..15) walks the chain entered at byte e until it meets chain 0;
+  //      a chain that never does (parity-locked or raw-run data) is walked to the tile end
+  int m = 0, p = l;
   uint32_t ww = 0;
   bool merged = true;
   if (l >= 1 && l < kTab) {
-    int p = l;
-    for (int k = 0; k < kB; k++) {
+    for (int k = 0; k < 2 * kB; k++) {
       if (p >= fms) {
         if (fms < kB) m = fms;           // every chain restarts at the first message start
         else if (p == (int)x0) m = kB;   // left the tile at chain 0's exit
         else merged = false;
         break;
       }
-      if ((lds_tm[wv][p >> 6] >> (p & 63)) & 1) {
+      if ((lds_tm[p >> 6] >> (p & 63)) & 1) {
         m = p;
         break;
       }
@@ -646,7 +695,8 @@ __global__ __launch_bounds__(256) void index_kernel(UnpackArgs a) {
   int32_t delta = 0;
   if (l >= 1 && l < kTab) {
     if (!merged) {
-      delta = kUnmerged;
+      delta = (int32_t)ww;  // words of the chain's records in the tile
+      a.t_xe[t * kTab + l] = (uint32_t)p;
     } else {
       uint32_t w0;
       if (m >= kB) {
@@ -658,41 +708,48 @@ __global__ __launch_bounds__(256) void index_kernel(UnpackArgs a) {
         while (r2) {
           const int bb = lowest_bit(r2);
           r2 &= r2 - 1;
-          const int p = 64 * (m >> 6) + bb;
-          w0 += d[p + 1 + __popc(d[p])];
+          const int q = 64 * (m >> 6) + bb;
+          w0 += d[q + 1 + __popc(d[q])];
         }
       }
       delta = (int32_t)(ww - w0);
     }
   }
+  const uint32_t umask = (uint32_t)ballot(l >= 1 && l < kTab && !merged);
   if (l < kTab) a.t_delta[t * kTab + l] = delta;
   if (l == 0) {
     a.t_x0[t] = x0;
     a.t_fms[t] = (uint32_t)fms;
     a.t_wpre[t] = wpre0;
     a.t_wpost[t] = wpost;
+    a.t_umask[t] = umask;
     a.t_flags[t] = (settled ? 0u : kTileUnsettled) | (tile_has_start ? kTileHasStart : 0u);
   }
 }
 
 // Walks the chain entered at tile-relative byte E of tile t through global memory until it meets
-// a chain-0 record start (or the first message start).  True when it merges; *wpre = words of
-// the records from E up to the first message start.
+// a chain-0 record start or the first message start (merged: the tile's exit is chain 0's), or
+// leaves the tile (its own exit).  *wpre = words of its records before the first message start.
+// False when the walk cap is hit.
 __device__ bool walk_global(const UnpackArgs& a, uint64_t t, uint32_t E, uint32_t fms,
-                            uint32_t x0, uint32_t wpre0, uint32_t* wpre) {
+                            uint32_t x0, uint32_t wpre0, uint32_t* wpre, uint32_t* exit,
+                            bool* merged) {
   const uint8_t* b = a.packed;
   const uint64_t P = a.nbytes;
   const uint64_t A = t * kB;
   const uint64_t* tmt = a.tm + t * 64;
   auto byte_at = [&](uint64_t q) -> uint32_t { return q < P ? (uint32_t)b[q] : 0u; };
   uint32_t p = E, w = 0;
+  *merged = true;
+  *exit = x0;
   for (int k = 0; k < kWalkCap; k++) {
     if (p >= fms) {
-      if (fms < (uint32_t)kB || p == x0) {
-        *wpre = w;
-        return true;
+      *wpre = w;
+      if (fms >= (uint32_t)kB && p != x0) {
+        *merged = false;
+        *exit = p;
       }
-      return false;
+      return true;
     }
     const uint64_t tmw = tmt[p >> 6];
     if ((tmw >> (p & 63)) & 1) {
@@ -720,41 +777,164 @@ __device__ bool walk_global(const UnpackArgs& a, uint64_t t, uint32_t E, uint32_
   return false;
 }
 
-// 4. Resolve: one thread per tile (64 consecutive tiles per wave = one look-back group).
-__global__ __launch_bounds__(256) void resolve_kernel(UnpackArgs a) {
+// Tile t's entry given the exit of its predecessor (tile-relative to the predecessor).
+__device__ __forceinline__ uint32_t entry_from_exit(const UnpackArgs& a, uint64_t t, uint32_t xp) {
+  const uint32_t E = xp >= (uint32_t)kDead ? (uint32_t)kB : xp - (uint32_t)kB;
+  const uint32_t fms = a.t_fms[t];
+  return E < fms ? E : fms;
+}
+
+// Tile t entered at E: its exit, words before its first message start, and whether the entry's
+// chain merged into chain 0 (merge table for E < 16, a global walk beyond).  False: walk cap.
+__device__ bool classify(const UnpackArgs& a, uint64_t t, uint32_t E, uint32_t* exit,
+                         uint32_t* wpre, bool* merged) {
+  const uint32_t fms = a.t_fms[t], wpre0 = a.t_wpre[t], x0 = a.t_x0[t];
+  *merged = true;
+  *exit = x0;
+  if (E == 0) {
+    *wpre = wpre0;
+    return true;
+  }
+  if (E >= fms) {
+    *wpre = 0;
+    return true;
+  }
+  if (E < (uint32_t)kTab) {
+    const int32_t dl = a.t_delta[t * kTab + E];
+    if ((a.t_umask[t] >> E) & 1) {
+      *merged = false;
+      *exit = a.t_xe[t * kTab + E];
+      *wpre = (uint32_t)dl;
+      dbg_count(a, kDbgTableMiss);
+    } else {
+      *wpre = wpre0 + (uint32_t)dl;
+    }
+    return true;
+  }
+  dbg_count(a, kDbgWalks);
+  const bool ok = walk_global(a, t, E, fms, x0, wpre0, wpre, exit, merged);
+  if (!ok) dbg_count(a, kDbgWalkFail);
+  return ok;
+}
+
+__device__ __forceinline__ void flag_tile_messages(const UnpackArgs& a, uint64_t t) {
+  const uint64_t mf = a.tile_first[t];
+  const uint64_t A = t * kB;
+  if (mf > 0) flag_message(a, mf - 1);
+  for (uint64_t m = mf; m < a.nmsgs && a.in_off[m] < A + kB; m++) flag_message(a, m);
+}
+
+// 4a. Resolve, optimistic pass: one thread per tile.  Entry = the predecessor's chain-0 exit
+// (right whenever the predecessor's own entry merged, or it holds a message start).  Records
+// the tile's exit and words under that entry and, per 64 tiles, bitmaps of the tiles whose entry
+// chain did not merge and of the tiles holding a message start.
+__global__ __launch_bounds__(256) void resolve1_kernel(UnpackArgs a) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool valid = t < a.ntiles;
+  bool merged = true, has_start = false;
+  if (valid) {
+    const uint32_t flags = a.t_flags[t];
+    has_start = flags & kTileHasStart;
+    const uint32_t E = t == 0 ? 0u : entry_from_exit(a, t, a.t_x0[t - 1]);
+    uint32_t x = 0, w = 0;
+    if (!classify(a, t, E, &x, &w, &merged)) {
+      flag_tile_messages(a, t);
+      merged = true;
+    }
+    if (flags & kTileUnsettled) {
+      dbg_count(a, kDbgUnsettled);
+      flag_tile_messages(a, t);
+    }
+    a.r1_x[t] = x;
+    a.r1_w[t] = w;
+  }
+  const uint64_t nb = ballot(valid && !merged);
+  const uint64_t mb = ballot(valid && has_start);
+  if (lane_id() == 0 && valid) {
+    a.g_notok[t / kGroup] = nb;
+    a.g_start[t / kGroup] = mb;
+  }
+}
+
+// First not-merged tile in (lo, hi) (tile indices), or hi if none.
+__device__ __forceinline__ uint64_t next_notok(const UnpackArgs& a, uint64_t lo, uint64_t hi) {
+  uint64_t j = lo + 1;
+  while (j < hi) {
+    const uint64_t G = j / kGroup;
+    uint64_t nb = a.g_notok[G] & ~mask_lt((int)(j % kGroup));
+    if (nb) {
+      const uint64_t k = G * kGroup + lowest_bit(nb);
+      return k < hi ? k : hi;
+    }
+    j = (G + 1) * kGroup;
+  }
+  return hi;
+}
+
+// 4b. Resolve, exact pass: one thread per tile.  An optimistic entry is wrong only after a tile
+// whose own entry did not merge, with no message start in between.  Such a stretch is replayed
+// from its first tile (whose entry is right): entries follow the replayed exits until they agree
+// with the optimistic ones again.  Then segmented tile values + 64-tile group aggregates for the
+// word offsets (expand_kernel's look-back).
+__global__ __launch_bounds__(256) void resolve2_kernel(UnpackArgs a) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int l = lane_id();
   const bool valid = t < a.ntiles;
   uint64_t v = 0;
   if (valid) {
-    const uint32_t fms = a.t_fms[t];
     const uint32_t flags = a.t_flags[t];
-    const uint32_t wpre0 = a.t_wpre[t];
-    uint32_t E = 0;
+    uint32_t E = t == 0 ? 0u : entry_from_exit(a, t, a.t_x0[t - 1]);
+    uint32_t wpre = a.r1_w[t];
+    // the last tile s < t holding a message start, and the first non-merged tile in (s, t)
+    uint64_t k0 = t;
     if (t > 0) {
-      const uint32_t xp = a.t_x0[t - 1];
-      E = xp >= (uint32_t)kDead ? (uint32_t)kB : xp - (uint32_t)kB;
+      int64_t G = (int64_t)(t / kGroup);
+      uint64_t lim = mask_lt((int)(t % kGroup));
+      for (int guard = 0; G >= 0 && guard < (1 << 14); guard++, G--) {
+        const uint64_t mb = a.g_start[G] & lim;
+        uint64_t nb = a.g_notok[G] & lim;
+        if (mb) {
+          const int s = highest_bit(mb);
+          nb &= ~mask_le(s);
+          if (nb) k0 = (uint64_t)G * kGroup + lowest_bit(nb);
+          break;
+        }
+        if (nb) k0 = (uint64_t)G * kGroup + lowest_bit(nb);
+        lim = ~0ull;
+      }
     }
-    if (E > fms) E = fms;
     bool ok = true;
-    uint32_t wpre = 0;
-    if (E == 0) {
-      wpre = wpre0;
-    } else if (E >= fms) {
-      wpre = 0;
-    } else if (E < (uint32_t)kTab) {
-      const int32_t dl = a.t_delta[t * kTab + E];
-      if (dl == kUnmerged) ok = false;
-      else wpre = wpre0 + (uint32_t)dl;
-    } else {
-      ok = walk_global(a, t, E, fms, a.t_x0[t], wpre0, &wpre);
-    }
-    const uint64_t mf = a.tile_first[t];  // first message starting at or after the tile start
-    if (!ok && mf > 0) flag_message(a, mf - 1);
-    if (flags & kTileUnsettled) {
-      const uint64_t A = t * kB;
-      if (mf > 0) flag_message(a, mf - 1);
-      for (uint64_t m = mf; m < a.nmsgs && a.in_off[m] < A + kB; m++) flag_message(a, m);
+    if (k0 < t) {
+      // replay from k0: its entry is right, its exit is the non-merged chain's
+      uint32_t X = a.r1_x[k0];
+      uint64_t j = k0 + 1;
+      int steps = 0;
+      while (j <= t && ok) {
+        const uint32_t Ej = entry_from_exit(a, j, X);
+        const uint32_t Eopt = entry_from_exit(a, j, a.t_x0[j - 1]);
+        if (Ej == Eopt) {
+          // back on the optimistic path: right until the next non-merged tile
+          const uint64_t k = next_notok(a, j - 1, t);
+          if (k >= t) {
+            break;  // E (optimistic) and wpre (pass 1) are this tile's
+          }
+          X = a.r1_x[k];
+          j = k + 1;
+          continue;
+        }
+        bool mg;
+        uint32_t w;
+        if (++steps > 4096 || !classify(a, j, Ej, &X, &w, &mg)) {
+          ok = false;
+          break;
+        }
+        if (j == t) {
+          E = Ej;
+          wpre = w;
+        }
+        j++;
+      }
+      if (!ok) flag_tile_messages(a, t);
     }
     a.t_ent[t] = E;
     v = (flags & kTileHasStart) ? (kSegBit | a.t_wpost[t]) : (uint64_t)wpre;
@@ -772,9 +952,9 @@ __global__ __launch_bounds__(256) void resolve_kernel(UnpackArgs a) {
 __global__ __launch_bounds__(256) void expand_kernel(UnpackArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds_data[4][kB + kPad];
   __shared__ uint64_t lds_ms[4][64];
-  __shared__ uint64_t lds_tm[4][64];
-  __shared__ uint64_t lds_fix[4][64];
-  __shared__ uint16_t lds_list[4][kB / 4];  // record positions of half a tile (<= 1024)
+  // per wave 1 KiB: chain-0 masks + walked starts while the entry is patched, then the record
+  // list of a quarter tile (<= 512 records of >= 2 bytes)
+  __shared__ uint64_t lds_aux[4][kB / 32];
   __shared__ uint64_t dep_tab[256];
   const int l = lane_id();
   const int wv = (int)uniform32(threadIdx.x >> 6);  // wave-uniform (keeps tile math scalar)
@@ -783,48 +963,48 @@ __global__ __launch_bounds__(256) void expand_kernel(UnpackArgs a) {
   const uint64_t t = (uint64_t)blockIdx.x * 4 + wv;
   if (t >= a.ntiles) return;
   uint8_t* d = lds_data[wv];
-  uint16_t* list = lds_list[wv];
+  uint64_t* aux = lds_aux[wv];
+  uint16_t* list = (uint16_t*)aux;
   const uint32_t lut = deposit_sel((uint32_t)l & 15);
   const uint64_t A = t * kB;
 
-  stage_tile(a, A, d);
-  const uint64_t mfirst = a.tile_first[t];
-  int nms_after;
-  const uint64_t mlast = tile_msg_starts(a, A, mfirst, lds_ms[wv], &nms_after);
-  const uint64_t msw = lds_ms[wv][l];
+  // every load that depends only on t first, then what depends on them
+  Staged stg;
+  stage_load(a, A, stg);
+  const uint64_t mfirst = uniform64(a.tile_first[t]);
   uint64_t tm = a.tm[t * 64 + l];
-  const uint32_t E = a.t_ent[t];
-  const uint32_t fms = a.t_fms[t];
+  const uint32_t E = uniform32(a.t_ent[t]);
+  const uint32_t fms = uniform32(a.t_fms[t]);
   // words of the message at the tile start before this tile (tile values are final: no wait)
   const uint64_t excl = lookback2(a.desc, a.gdesc, t, kSegBit, a.err);
+  stage_store(stg, d);
+  int nms_after;
   MsgWin win;
-  load_win(a, (int64_t)mfirst - 1, win);
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  const uint64_t mlast = tile_msg_starts(a, A, mfirst, lds_ms[wv], &nms_after, &win);
+  const uint64_t msw = lds_ms[wv][l];
 
   // ---- chain 0 -> the true chain: starts before the merge point come from a walk from E ----
   if (E > 0) {
     const bool pre_ok = readlane32(win.ok, 0) != 0;  // message holding the tile's first byte
     int m = (int)fms;
-    lds_fix[wv][l] = 0;
+    aux[64 + l] = 0;
     if (pre_ok && E < fms) {
-      lds_tm[wv][l] = tm;
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      aux[l] = tm;
       if (l == 0) {
         int p = (int)E;
-        uint64_t* fix = lds_fix[wv];
+        uint64_t* fix = aux + 64;
         while (p < (int)fms && p < kB) {
-          if ((lds_tm[wv][p >> 6] >> (p & 63)) & 1) break;
+          if ((aux[p >> 6] >> (p & 63)) & 1) break;
           fix[p >> 6] |= 1ull << (p & 63);
           p += record_len(d, p);
         }
         m = p < (int)fms ? p : (int)fms;
       }
       m = (int)readlane32((uint32_t)m, 0);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
     const int s = 64 * l;
     const uint64_t below = m <= s ? 0ull : (m >= s + 64 ? ~0ull : mask_lt(m - s));
-    tm = (tm & ~below) | lds_fix[wv][l];
+    tm = (tm & ~below) | aux[64 + l];
   }
 
   // Fast expansion when every message touching the tile is in the window, has a valid header,
@@ -841,8 +1021,14 @@ __global__ __launch_bounds__(256) void expand_kernel(UnpackArgs a) {
   const uint32_t cnt_all = __popcll(tm);
   const uint32_t Rall_incl = wave_incl_sum32(cnt_all);
   const uint32_t nrec = readlane32(Rall_incl, 63);
-  const uint32_t nfirst = readlane32(Rall_incl, 31);
-  if (nfirst > kB / 4 || nrec - nfirst > kB / 4) fast = false;  // list capacity (1-byte records)
+  {
+    // list capacity per quarter tile (records shorter than 2 bytes exist only where message
+    // starts clip them)
+    const uint32_t q1 = readlane32(Rall_incl, 15), q2 = readlane32(Rall_incl, 31),
+                   q3 = readlane32(Rall_incl, 47);
+    constexpr uint32_t kList = kB / 8;
+    if (q1 > kList || q2 - q1 > kList || q3 - q2 > kList || nrec - q3 > kList) fast = false;
+  }
   if (!fast) {
     // general path: one lane per record, record positions by binary search, message of each
     // record from the window (see handle_record for the reference checks)
@@ -948,12 +1134,15 @@ __global__ __launch_bounds__(256) void expand_kernel(UnpackArgs a) {
     }
     return;
   }
-  // fast path: record list per half tile (lanes 0-31, then 32-63), 64 records per batch
+  // fast path: record list per quarter tile (lanes 16h .. 16h+15), 64 records per batch
   uint64_t sum = 0;        // words of the tile's records so far
   uint32_t base_key = 0;   // key of the latest message start so far (key-max reset)
   uint32_t mcount = 0;     // message starts so far
-  for (int h = 0; h < 2; h++) {
-    const bool mine = (l >> 5) == h;
+  // the current message (window lane mcount): batches without a message start use it as is
+  uint64_t cbase = readlane64(win.base, 0), ctotal = readlane64(win.total, 0);
+  uint64_t cend = readlane64(win.end, 0);
+  for (int h = 0; h < 4; h++) {
+    const bool mine = (l >> 4) == h;
     uint64_t bits = mine ? tm : 0;
     const uint32_t c = __popcll(bits);
     const uint32_t Rin = wave_incl_sum32(c);
@@ -988,15 +1177,26 @@ __global__ __launch_bounds__(256) void expand_kernel(UnpackArgs a) {
       const uint32_t w = act ? 1 + cnt : 0;
       const uint32_t inc = wave_incl_sum32(w);
       const uint64_t Sx = sum + inc - w;
-      const uint32_t key = is_ms ? (uint32_t)(Sx + 1) : 0;
-      uint32_t km = wave_incl_max32(key);
-      if (km < base_key) km = base_key;
-      const uint64_t wb = km ? Sx - (km - 1) : excl + Sx;
       const uint64_t msb = ballot(is_ms);
-      const int wl = (int)(mcount + (uint32_t)__popcll(msb & mask_le(l)));  // window lane
-      const uint64_t mbase = shfl64(win.base, wl);
-      const uint64_t mtotal = shfl64(win.total, wl);
-      const uint64_t mend = shfl64(win.end, wl);
+      uint32_t km;
+      int wl;  // window lane of the record's message
+      uint64_t mbase, mtotal, mend;
+      if (msb == 0) {
+        km = base_key;
+        wl = (int)mcount;
+        mbase = cbase;
+        mtotal = ctotal;
+        mend = cend;
+      } else {
+        const uint32_t key = is_ms ? (uint32_t)(Sx + 1) : 0;
+        km = wave_incl_max32(key);
+        if (km < base_key) km = base_key;
+        wl = (int)(mcount + (uint32_t)__popcll(msb & mask_le(l)));
+        mbase = shfl64(win.base, wl);
+        mtotal = shfl64(win.total, wl);
+        mend = shfl64(win.end, wl);
+      }
+      const uint64_t wb = km ? Sx - (km - 1) : excl + Sx;
       const uint64_t sel = dep_tab[tag];
       const uint32_t wlo = __builtin_amdgcn_perm(dhi, dlo, (uint32_t)sel);
       const uint32_t whi = __builtin_amdgcn_perm(dhi, dlo, (uint32_t)(sel >> 32));
@@ -1032,7 +1232,12 @@ __global__ __launch_bounds__(256) void expand_kernel(UnpackArgs a) {
       run_jobs(a, job);
       base_key = readlane32(km, 63);
       sum += readlane32(inc, 63);
-      mcount += (uint32_t)__popcll(msb);
+      if (msb) {
+        mcount += (uint32_t)__popcll(msb);
+        cbase = readlane64(win.base, (int)mcount);
+        ctotal = readlane64(win.total, (int)mcount);
+        cend = readlane64(win.end, (int)mcount);
+      }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
@@ -1164,7 +1369,9 @@ hipError_t launch_unpack_stage(int stage, const UnpackArgs& a, hipStream_t strea
       hipLaunchKernelGGL(index_kernel, dim3(wave_blocks), dim3(256), 0, stream, a);
       break;
     case kUnpackResolve:
-      hipLaunchKernelGGL(resolve_kernel, dim3((unsigned)((a.ntiles + 255) / 256)), dim3(256), 0,
+      hipLaunchKernelGGL(resolve1_kernel, dim3((unsigned)((a.ntiles + 255) / 256)), dim3(256), 0,
+                         stream, a);
+      hipLaunchKernelGGL(resolve2_kernel, dim3((unsigned)((a.ntiles + 255) / 256)), dim3(256), 0,
                          stream, a);
       break;
     case kUnpackExpand:
