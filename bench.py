@@ -179,7 +179,7 @@ def main():
     kt = codec.timing_read_all()
     kms = {k: (v[0] / v[1] if v[1] else 0.0) for k, v in kt.items()}
 
-    red = reduce_step(dt, float(U), float(P), kms["pack_tiles"], kms["unpack"], ok,
+    red = reduce_step(dt, float(U), float(P), kms["pack"], kms["unpack"], ok,
                       dist=dist, device=codec.device)
     dt_max, U_all = red["dt_max"], red["unpacked_all"]
     ok_all = red["ok_all"]
@@ -189,22 +189,25 @@ def main():
         ms_per_step = dt_max / args.steps * 1e3
         value = U_all / (dt_max / args.steps) / 2**30
         # algorithmic HBM bytes of one launch of each tile kernel
-        algo = {"pack_tiles": U + P, "unpack_index": P, "unpack_expand": U + P}
+        algo = {"pack_count": U, "pack_emit": U + P, "unpack_index": P, "unpack_expand": U + P}
+        if kms["pack_count"] == 0:  # single-pass pack kernel (CPK_PACK_FUSED=1)
+            algo = {"pack": U + P, "unpack_index": P, "unpack_expand": U + P}
         kern = {k: {"ms": round(kms[k], 4),
                     "GBps": round(algo[k] / (kms[k] * 1e-3) / 1e9, 1) if kms[k] > 0 else None,
                     "algorithmic_bytes": int(algo[k])} for k in algo}
-        for k in ("unpack_resolve", "unpack_fallback"):
-            kern[k] = {"ms": round(kms[k], 4)}
+        for k in ("pack", "unpack_resolve", "unpack_fallback"):
+            kern.setdefault(k, {"ms": round(kms[k], 4)})
         dom = max(algo, key=lambda k: kms[k])
         dom_ms = kms[dom]
         achieved = algo[dom] / (dom_ms * 1e-3) / 1e9
-        rt_ms = kms["pack_tiles"] + kms["unpack"]
+        rt_ms = kms["pack"] + kms["unpack"]
         rt = 2.0 * (U + P) / (rt_ms * 1e-3) / 1e9
         traffic = None
         tf = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
         if os.path.exists(tf):
             try:
-                traffic = json.load(open(tf)).get(dom)
+                t = json.load(open(tf)).get(dom)
+                traffic = int(t["bytes"]) if isinstance(t, dict) else t
             except Exception:
                 traffic = None
         result = {
@@ -240,7 +243,7 @@ def main():
                 "traffic": traffic,
                 "algorithmic_bytes_per_launch": int(algo[dom]),
                 "kernels": kern,
-                "pack_ms": round(kms["pack_tiles"], 4),
+                "pack_ms": round(kms["pack"], 4),
                 "unpack_ms": round(kms["unpack"], 4),
                 "roundtrip_GBps": round(rt, 1),
                 "roundtrip_frac": round(rt / HBM_PEAK_GBS, 4),

@@ -240,8 +240,8 @@ class Codec:
                                              C.byref(ul)), "cpk_timing_read")
         return pm.value, pl.value, um.value, ul.value
 
-    TIMERS = ("pack_tiles", "unpack", "unpack_index", "unpack_resolve", "unpack_expand",
-              "unpack_fallback")
+    TIMERS = ("pack", "unpack", "unpack_index", "unpack_resolve", "unpack_expand",
+              "unpack_fallback", "pack_count", "pack_emit")
 
     def timing_read_all(self):
         """{timer name: (summed ms, launches)} since the last read (include/cpk.h timers)."""

@@ -21,8 +21,9 @@ struct cpk_ctx {
   // device staging for the *_host entry points
   void* stage[4] = {nullptr, nullptr, nullptr, nullptr};
   size_t stage_size[4] = {0, 0, 0, 0};
-  // measurement hooks: [0] pack tile kernel, [1] unpack (index .. fallback), [2 + stage] each
-  // unpack stage kernel (index, resolve, expand, fallback)
+  // measurement hooks: [0] pack tile kernels (count .. emit), [1] unpack (index .. fallback),
+  // [2 + stage] each unpack stage kernel (index, resolve, expand, fallback), [6] pack count,
+  // [7] pack emit
   bool timing = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[CPK_TIMERS];
   std::vector<hipEvent_t> pool;
@@ -114,17 +115,15 @@ struct PackScratch {
   uint32_t* gcnt;
   uint32_t* state;
   uint64_t* bits;
+  uint32_t* scan_counter;
+  uint64_t* scan_desc;
   size_t zero_bytes;
   uint64_t* tile_first;
+  uint32_t* tile_b;
+  uint64_t* tile_bytes;
+  uint64_t* tile_off;
   size_t total;
 };
-
-size_t pack_scratch_bytes(uint64_t N, uint64_t ntiles) {
-  const uint64_t nbitw = (N + 63) / 64;
-  const uint64_t ng = (ntiles + 63) / 64;
-  return 16 + align16(8 * ntiles) + align16(8 * ng) + align16(4 * ng) + align16(4 * ntiles) +
-         align16(8 * nbitw) + align16(8 * ntiles) + 64;
-}
 
 PackScratch carve_pack(void* base, uint64_t N, uint64_t ntiles) {
   Carve c(base);
@@ -135,10 +134,19 @@ PackScratch carve_pack(void* base, uint64_t N, uint64_t ntiles) {
   s.gcnt = c.take<uint32_t>((ntiles + 63) / 64);
   s.state = c.take<uint32_t>(ntiles);
   s.bits = c.take<uint64_t>((N + 63) / 64);
+  s.scan_counter = c.take<uint32_t>(4);
+  s.scan_desc = c.take<uint64_t>(cpk::scan_tiles(ntiles + 1));
   s.zero_bytes = c.off;
   s.tile_first = c.take<uint64_t>(ntiles);
+  s.tile_b = c.take<uint32_t>(ntiles);
+  s.tile_bytes = c.take<uint64_t>(ntiles);
+  s.tile_off = c.take<uint64_t>(ntiles + 1);
   s.total = c.off;
   return s;
+}
+
+size_t pack_scratch_bytes(uint64_t N, uint64_t ntiles) {
+  return carve_pack(nullptr, N, ntiles).total + 64;
 }
 
 cpk_status pack_common(cpk_ctx* ctx, const uint64_t* d_words, uint64_t N, const uint64_t* d_off,
@@ -184,11 +192,29 @@ cpk_status pack_common(cpk_ctx* ctx, const uint64_t* d_words, uint64_t N, const 
   a.gdesc = s.gdesc;
   a.gcnt = s.gcnt;
   a.state = s.state;
+  a.tile_b = s.tile_b;
+  a.tile_bytes = s.tile_bytes;
+  a.tile_off = s.tile_off;
   a.err = ctx->err;
   a.stamps = cpk::debug_stamps(0);
   a.debug_skip = cpk::debug_skip();
   TimedLaunch tl(ctx, 0, stream);
-  e = cpk::launch_pack_tiles(a, stream);
+  if (cpk::pack_fused() || a.stamps) {
+    e = cpk::launch_pack_tiles(a, stream);
+  } else {
+    // count pass -> scan of tile byte counts -> emit pass
+    TimedLaunch tc(ctx, 6, stream);
+    e = cpk::launch_pack_stage(0, a, stream);
+    tc.done();
+    if (e == hipSuccess)
+      e = cpk::launch_exclusive_scan(s.tile_bytes, ntiles, s.tile_off, s.scan_counter,
+                                     s.scan_desc, ctx->err, stream);
+    if (e == hipSuccess) {
+      TimedLaunch te(ctx, 7, stream);
+      e = cpk::launch_pack_stage(1, a, stream);
+      te.done();
+    }
+  }
   tl.done();
   return hip_status(e);
 }

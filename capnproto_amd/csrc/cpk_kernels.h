@@ -30,13 +30,19 @@ struct PackTileArgs {
   uint64_t* gdesc;             // per 64-tile group look-back descriptors
   uint32_t* gcnt;              // per group arrival tickets
   uint32_t* state;             // ntiles exit budgets (0x80000000 | budget)
+  // two-pass form: count pass -> (entry budget, bytes) per tile; scan -> output offsets
+  uint32_t* tile_b;
+  uint64_t* tile_bytes;
+  const uint64_t* tile_off;
   uint32_t* err;
   unsigned long long* stamps;  // diagnostic build only (env CPK_STAMPS), else NULL
   uint32_t debug_skip;         // timing ablations only (env CPK_DEBUG_SKIP): 1 = no look-back
 };
 
 int pack_steps();  // words per pack tile = 64 * pack_steps()
+bool pack_fused();  // single-pass kernel (default) or count + emit (A/B knob CPK_PACK_TWO_PASS=1)
 hipError_t launch_pack_tiles(const PackTileArgs& a, hipStream_t stream);
+hipError_t launch_pack_stage(int stage, const PackTileArgs& a, hipStream_t stream);
 hipError_t launch_message_bits(const uint64_t* words, const uint64_t* off, uint64_t n,
                                uint64_t* bits, int32_t* status, hipStream_t stream);
 hipError_t launch_chunk_bits(const uint64_t* off, uint64_t n, uint64_t N, uint64_t* bits,

@@ -169,15 +169,27 @@ __device__ __forceinline__ void load_tile(const PackTileArgs& a, uint64_t t, Til
 //   look-back  two-level decoupled look-back on the tile's byte count
 //   flush    staged bytes -> global: 16-byte aligned stores (realigned by v_alignbyte), byte
 //            stores for the partial blocks at both ends; the staging area is re-zeroed.
-template <int S, bool PF, bool STAMPS>
+//
+// MODE kFused: the single-pass kernel above.  The two-pass form splits it at the look-back:
+// MODE kCount (persistent) does pass A and the count pass -- entry budgets still hand over
+// between waves, a one-hop wait only where a tile's first word continues a stretch -- and writes
+// each tile's entry budget and byte count; a scan turns the counts into output offsets; MODE kEmit
+// (one wave per tile, no waits) redoes pass A with the known entry budget, then pass B and the
+// flush at the known offset.
+constexpr int kFused = 0, kCount = 1, kEmit = 2;
+
+template <int S, bool PF, bool STAMPS, int MODE = kFused>
 __global__ __launch_bounds__(256) void pack_tiles_kernel(PackTileArgs a) {
   static_assert(S >= 2 && S <= 16 && (S % 2) == 0, "S steps per tile");
   constexpr int T = 64 * S;
   // Per-wave staging ring: a tile's records occupy [base, base + 32 + bytes) (16 B pads at both
   // ends), at most 32 + 640 * S bytes; the ring holds the tile being encoded and the previous
-  // one, whose look-back and flush are deferred until after this tile's emission pass.
+  // one, whose look-back and flush are deferred until after this tile's emission pass.  The emit
+  // pass flushes each tile at once (one region); the count pass stages nothing.
   constexpr int kMaxRegion = 32 + 640 * S;
-  constexpr int kStg = ((kMaxRegion * 6 / 5) + 15) & ~15;
+  constexpr int kStg = MODE == kCount ? 16
+                       : (MODE == kEmit ? ((kMaxRegion + 15) & ~15)
+                                        : (((kMaxRegion * 6 / 5) + 15) & ~15));
   __shared__ __attribute__((aligned(16))) uint8_t stg_all[4][kStg];
   __shared__ uint64_t sel_tab[256];
 
@@ -212,7 +224,9 @@ __global__ __launch_bounds__(256) void pack_tiles_kernel(PackTileArgs a) {
   // look-back, inclusive publish, flush of the staged bytes, positions
   auto finish = [&](const Pending& p) {
     uint64_t excl = 0;
-    if (a.debug_skip & 1) {
+    if constexpr (MODE == kEmit) {
+      excl = uniform64(a.tile_off[p.t]);
+    } else if (a.debug_skip & 1) {
       excl = p.t * 4096;  // timing ablation: no look-back (output meaningless)
     } else {
       excl = lookback2(a.desc, a.gdesc, p.t, 0, a.err);
@@ -255,9 +269,11 @@ __global__ __launch_bounds__(256) void pack_tiles_kernel(PackTileArgs a) {
     for (uint32_t i = l; i < nz16; i += 64) ((u32x4*)(sb + 16))[i] = (u32x4){0, 0, 0, 0};
     // positions: add the tile's global offset (own stores, read back past L1)
     if (a.pos) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      for (uint64_t i = p.pidx0 + l; i < p.pidx; i += 64)
-        a.pos_out[i] = load_agent(a.pos_out + i) + excl;
+      if constexpr (MODE != kEmit) {  // emit mode wrote absolute positions in pass B
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        for (uint64_t i = p.pidx0 + l; i < p.pidx; i += 64)
+          a.pos_out[i] = load_agent(a.pos_out + i) + excl;
+      }
       if (p.tend == N) {
         const uint64_t tot = excl + agg;
         for (uint64_t i = p.pidx + l; i <= a.npos; i += 64) a.pos_out[i] = tot;
@@ -334,10 +350,14 @@ __global__ __launch_bounds__(256) void pack_tiles_kernel(PackTileArgs a) {
       }
     });
     stm.mark(0);
+    // count pass: pass A was the last use of the words, the next tile's can be on their way
+    if constexpr (MODE == kCount) {
+      if (t + nwaves < a.ntiles) load_tile<S>(a, t + nwaves, cur);
+    }
 
     // ---- look-ahead: distance from tend to the first sync at / after it (<= 256) ------------
     int la = 0;
-    if ((lastZ || lastR) && tend < N) {
+    if (MODE != kCount && (lastZ || lastR) && tend < N) {
       uint64_t czc = lastZ, crc = lastR;
       la = 256;
       uint64_t xk[4] = {cur.nx, 0, 0, 0}, ck[4] = {readlane64(cur.cb, S), 0, 0, 0};
@@ -399,7 +419,7 @@ __global__ __launch_bounds__(256) void pack_tiles_kernel(PackTileArgs a) {
         }
         eb = (qq >= 0 && last - qq <= 255) ? 255 - (last - qq) : 0;
       }
-      if (l == 0) store_agent32(state + t, 0x80000000u | (uint32_t)eb);
+      if (MODE != kEmit && l == 0) store_agent32(state + t, 0x80000000u | (uint32_t)eb);
     }
 
     // prefetch the next tile (lands during pass B and the look-back)
@@ -407,7 +427,12 @@ __global__ __launch_bounds__(256) void pack_tiles_kernel(PackTileArgs a) {
     stm.mark(1);
 
     int b = 0;
-    if (first_sync > 0 && t > 0) b = (int)(wait_nonzero32(state + t - 1, a.err) & 0xffu);
+    if constexpr (MODE == kEmit) {
+      b = (int)uniform32(a.tile_b[t]);
+    } else {
+      if (first_sync > 0 && t > 0) b = (int)(wait_nonzero32(state + t - 1, a.err) & 0xffu);
+    }
+    const int b_entry = b;
     stm.mark(2);
 
     // ---- count pass (scalar): heads / coverage of every step, byte offsets -----------------
@@ -434,9 +459,18 @@ __global__ __launch_bounds__(256) void pack_tiles_kernel(PackTileArgs a) {
         agg32 += readlane32(vBase, s) + 2 * (uint32_t)__popcll(r.runheads);
       }
     });
-    if (first_sync == T && l == 0) store_agent32(state + t, 0x80000000u | (uint32_t)b);
+    if (MODE != kEmit && first_sync == T && l == 0) store_agent32(state + t, 0x80000000u | (uint32_t)b);
     const uint64_t agg = agg32;
-    if (!(a.debug_skip & 1)) publish_agg(a.desc, a.gdesc, a.gcnt, t, a.ntiles, agg, 0, a.err);
+    if constexpr (MODE == kCount) {
+      if (l == 0) {
+        a.tile_b[t] = (uint32_t)b_entry;
+        a.tile_bytes[t] = agg;
+      }
+      return;
+    }
+    if (MODE == kFused && !(a.debug_skip & 1))
+      publish_agg(a.desc, a.gdesc, a.gcnt, t, a.ntiles, agg, 0, a.err);
+    (void)b_entry;
     stm.mark(3);
 
     // ---- staging region: after the pending tile's, else at 0 (finishing it first if needed) ---
@@ -454,6 +488,8 @@ __global__ __launch_bounds__(256) void pack_tiles_kernel(PackTileArgs a) {
 
     // ---- pass B ----------------------------------------------------------------------------
     const uint64_t pidx0 = a.pos ? uniform64(a.tile_first[t]) : 0;
+    // emit mode knows the tile's output offset: positions are written absolute
+    const uint64_t pos_base = MODE == kEmit ? uniform64(a.tile_off[t]) : 0;
     uint64_t pidx = pidx0;
     uint32_t prel = ~0u;  // next requested position, tile-relative (~0: none in this tile)
     if (a.pos && pidx <= a.npos) {
@@ -491,14 +527,18 @@ __global__ __launch_bounds__(256) void pack_tiles_kernel(PackTileArgs a) {
         const uint32_t w2 = msel(FH, (hi >> 24) | c8, 0u);
         w0 = msel(COV, lo, w0);
         w1 = msel(COV, hi, w1);
-        // OR into the staging area at byte 16 + soff + o: four dwords from (at - 1) & ~3
+        // OR into the staging area at byte 16 + soff + o: four dwords from (at - 1) & ~3, each
+        // only where the record has bytes (a lane of a covered zero word has none; empty lanes
+        // would all hit the same dword and serialise on it)
         const uint32_t at = base + 16u + soff + o;
         const uint32_t rr = (0u - at) & 3u;
+        const uint32_t kk = 4u - rr;     // record start inside the 16-byte window (1..4)
+        const uint32_t ee = kk + len;    // record end inside the window
         uint32_t* dp = (uint32_t*)(stg + ((at - 1u) & ~3u));
-        atomicOr(dp + 0, __builtin_amdgcn_alignbyte(w0, 0u, rr));
-        atomicOr(dp + 1, __builtin_amdgcn_alignbyte(w1, w0, rr));
-        atomicOr(dp + 2, __builtin_amdgcn_alignbyte(w2, w1, rr));
-        atomicOr(dp + 3, __builtin_amdgcn_alignbyte(0u, w2, rr));
+        if (kk < 4u && len) atomicOr(dp + 0, __builtin_amdgcn_alignbyte(w0, 0u, rr));
+        if (ee > 4u) atomicOr(dp + 1, __builtin_amdgcn_alignbyte(w1, w0, rr));
+        if (ee > 8u) atomicOr(dp + 2, __builtin_amdgcn_alignbyte(w2, w1, rr));
+        if (ee > 12u) atomicOr(dp + 3, __builtin_amdgcn_alignbyte(0u, w2, rr));
         // requested positions inside this step: tile-relative offsets (excl added later)
         if (prel < 64u * s + 64u) {
           const uint64_t g0 = tbase + 64 * s;
@@ -507,7 +547,7 @@ __global__ __launch_bounds__(256) void pack_tiles_kernel(PackTileArgs a) {
             const uint64_t p = i <= a.npos ? a.pos[i] : ~0ull;
             const bool in = p < g0 + 64;
             const uint32_t oo = shfl32(o, in ? (int)(p - g0) : 0);
-            if (in) a.pos_out[i] = soff + oo;
+            if (in) a.pos_out[i] = pos_base + soff + oo;
             const uint64_t inm = ballot(in);
             pidx += __popcll(inm);
             const uint64_t pn = pidx <= a.npos ? uniform64(a.pos[pidx]) : ~0ull;
@@ -525,6 +565,18 @@ __global__ __launch_bounds__(256) void pack_tiles_kernel(PackTileArgs a) {
 
     // ---- finish the previous tile (its look-back had this tile's passes to resolve) --------
     if (pend.on) finish(pend);
+    if constexpr (MODE == kEmit) {  // no look-back to wait for: flush at once
+      Pending now;
+      now.t = t;
+      now.agg = agg;
+      now.tend = tend;
+      now.pidx0 = pidx0;
+      now.pidx = pidx;
+      now.base = base;
+      now.on = true;
+      finish(now);
+      return;
+    }
     pend.t = t;
     pend.agg = agg;
     pend.tend = tend;
@@ -638,6 +690,36 @@ static bool pack_prefetch() {
   static const bool on = [] {
     const char* e = getenv("CPK_PACK_PF");
     return e && atoi(e) != 0;
+  }();
+  return on;
+}
+
+// Two-pass form (default).  stage 0: count pass, persistent grid (its waves hand entry budgets
+// over); stage 1: emit pass, one wave per tile.  The caller scans tile_bytes into tile_off in
+// between.
+hipError_t launch_pack_stage(int stage, const PackTileArgs& a, hipStream_t stream) {
+  if (a.ntiles == 0) return hipSuccess;
+  constexpr int S = kPackSteps;
+  if (stage == 0) {
+    static const unsigned cap =
+        resident_blocks((const void*)pack_tiles_kernel<S, false, false, kCount>, 256, 0);
+    const uint64_t want = (a.ntiles + 3) / 4;
+    const unsigned blocks = (unsigned)(want < cap ? want : cap);
+    hipLaunchKernelGGL((pack_tiles_kernel<S, false, false, kCount>), dim3(blocks), dim3(256), 0,
+                       stream, a);
+  } else {
+    hipLaunchKernelGGL((pack_tiles_kernel<S, false, false, kEmit>),
+                       dim3((unsigned)((a.ntiles + 3) / 4)), dim3(256), 0, stream, a);
+  }
+  return hipGetLastError();
+}
+
+bool pack_fused() {
+  static const bool on = [] {
+    // A/B knob: CPK_PACK_TWO_PASS=1 selects count + scan + emit (measured slower on C2/C4/C5
+    // than the single-pass kernel once the emission's LDS atomics were predicated)
+    const char* e = getenv("CPK_PACK_TWO_PASS");
+    return !(e && atoi(e) != 0);
   }();
   return on;
 }

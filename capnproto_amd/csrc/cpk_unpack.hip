@@ -1158,9 +1158,12 @@ __global__ __launch_bounds__(256) void expand_kernel(UnpackArgs a) {
     for (uint32_t b0 = 0; b0 < nh; b0 += 64) {
       const uint32_t rr = b0 + l;
       const bool act = rr < nh;
-      const uint32_t e = act ? list[rr] : 0;
+      // branch-free body: an inactive lane reads a real entry (LDS stays in bounds) and is
+      // masked by selects, so the batch runs without exec-mask splits
+      const uint32_t e0 = list[rr < nh ? rr : nh - 1];
+      const uint32_t e = act ? e0 : 0u;
       const int p = (int)(e & 0xfff);
-      const bool is_ms = act && ((e >> 12) & 1);
+      const bool is_ms = (e >> 12) & 1;
       // bytes p .. p + 12: tag, up to 8 data bytes, count byte
       const uint32_t* dw = (const uint32_t*)(d + (p & ~3));
       const uint32_t sh = (uint32_t)p & 3;
@@ -1173,7 +1176,10 @@ __global__ __launch_bounds__(256) void expand_kernel(UnpackArgs a) {
       const uint32_t dhi = __builtin_amdgcn_alignbyte(b2w, b1w, 1);  // data bytes 4..7
       const uint32_t nz = __popc(tag);
       const bool z = tag == 0, f = tag == 0xff;
-      const uint32_t cnt = act ? (z ? ((b0w >> 8) & 0xff) : (f ? ((b2w >> 8) & 0xff) : 0u)) : 0u;
+      const uint32_t c1 = (b0w >> 8) & 0xff, c9 = (b2w >> 8) & 0xff;
+      uint32_t cnt = z ? c1 : 0u;
+      cnt = f ? c9 : cnt;
+      cnt = act ? cnt : 0u;
       const uint32_t w = act ? 1 + cnt : 0;
       const uint32_t inc = wave_incl_sum32(w);
       const uint64_t Sx = sum + inc - w;
@@ -1201,7 +1207,7 @@ __global__ __launch_bounds__(256) void expand_kernel(UnpackArgs a) {
       const uint32_t wlo = __builtin_amdgcn_perm(dhi, dlo, (uint32_t)sel);
       const uint32_t whi = __builtin_amdgcn_perm(dhi, dlo, (uint32_t)(sel >> 32));
       const uint64_t word = ((uint64_t)whi << 32) | wlo;
-      const uint32_t len = 1 + nz + ((z || f) ? 1 + (f ? 8 * cnt : 0) : 0);
+      const uint32_t len = 1 + nz + (uint32_t)(z | f) + (f ? 8 * cnt : 0u);
       const uint64_t pabs = A + p;
       // records that end a message (or break it) go through the reference checks
       const bool special = act && (wb + w >= mtotal || pabs + len >= mend);
