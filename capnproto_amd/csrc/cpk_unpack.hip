@@ -151,26 +151,32 @@ struct SubTile {
   int pend;          // batch end, tile-relative
 };
 
-// Next chain position after a record at p: the record end, clipped at the next message start.
-__device__ __forceinline__ int next_pos(const uint8_t* d, const SubTile& st, int p) {
-  int np = p + record_len(d, p);
-  const int k = p - st.s + 1;
+// First message start after position q of the sub-tile (q >= st.s): the next chain clip.
+__device__ __forceinline__ int next_start_after(const SubTile& st, int q) {
+  const int k = q - st.s + 1;
   const uint64_t after = k < 64 ? (st.msw >> k) : 0;
-  const int nm = after ? p + 1 + lowest_bit(after) : st.nms_after;
-  return np < nm ? np : nm;
+  return after ? q + 1 + lowest_bit(after) : st.nms_after;
 }
 
 // Walks from p (inside the sub-tile) marking record starts until the chain leaves the sub-tile
-// or reaches a position of `stop`.  Returns the position reached.
+// or reaches a position of `stop`.  Record ends are clipped at the next message start nm, which
+// only moves when the chain reaches it (rare), so the step itself carries no message logic.
+// Returns the position reached.
 __device__ __forceinline__ int walk(const uint8_t* d, const SubTile& st, int p, uint64_t stop,
                                     uint64_t* marks, uint64_t* runs = nullptr) {
   uint64_t m = 0, rm = 0;
+  int nm = next_start_after(st, p);
   while (p < st.vend) {
     const uint64_t bit = 1ull << (p - st.s);
     m |= bit;
     const uint32_t tag = d[p];
     if (tag == 0 || tag == 0xff) rm |= bit;
-    p = next_pos(d, st, p);
+    int np = p + record_len(d, p);
+    if (np >= nm) {
+      np = nm;
+      nm = np < st.end ? next_start_after(st, np) : st.nms_after;
+    }
+    p = np;
     if (p < st.vend && ((stop >> (p - st.s)) & 1)) break;
   }
   *marks = m;
@@ -187,9 +193,10 @@ __device__ __forceinline__ int walk(const uint8_t* d, const SubTile& st, int p, 
 // to lane.  Returns false when the iteration cap is hit (the caller flags the tile).
 __device__ __forceinline__ bool settle(const uint8_t* d, const SubTile& st, uint64_t chain,
                                        int sx, int E, int& e, uint64_t& tm, int& out,
-                                       uint64_t& runm) {
+                                       uint64_t& runm, int* iters = nullptr) {
   const int l = lane_id();
   for (int iter = 0; iter < 96; iter++) {
+    if (iters) *iters = iter + 1;
     const bool pass = e >= st.end || e >= st.pend;
     if (pass) {
       out = e >= st.pend ? kDead : e;
@@ -406,9 +413,13 @@ __device__ __forceinline__ void run_jobs(const UnpackArgs& a, const RunJob& job)
 }
 
 // Diagnostic counters (env CPK_STAMPS=1 only; a.stamps is NULL otherwise).
-enum : int { kDbgUnsettled = 0, kDbgTableMiss, kDbgWalkFail, kDbgWalks, kDbgFlagged };
+enum : int { kDbgUnsettled = 0, kDbgTableMiss, kDbgWalkFail, kDbgWalks, kDbgFlagged,
+             kDbgUmaskTiles, kDbgMergeSteps, kDbgSettleIters, kDbgWalkSteps, kDbgWalkStepsMax };
 __device__ __forceinline__ void dbg_count(const UnpackArgs& a, int slot) {
   if (a.stamps) atomicAdd(a.stamps + slot, 1ull);
+}
+__device__ __forceinline__ void dbg_add(const UnpackArgs& a, int slot, uint64_t v) {
+  if (a.stamps && lane_id() == 0) atomicAdd(a.stamps + slot, (unsigned long long)v);
 }
 
 __device__ __forceinline__ void flag_message(const UnpackArgs& a, uint64_t m) {
@@ -621,11 +632,19 @@ __global__ __launch_bounds__(256) void index_kernel(UnpackArgs a) {
   // ---- chain 0: speculative walks, then the lane fixed point for entry 0 --------------------
   uint64_t chain = 0, runm = 0;
   int sx = kDead;
-  if (st.s < st.pend) sx = walk(d, st, st.s, 0, &chain, &runm);
+  if (!(a.debug_skip & 4) && st.s < st.pend) sx = walk(d, st, st.s, 0, &chain, &runm);
   int e = st.s;
   uint64_t tm = 0;
   int out = 0;
-  const bool settled = settle(d, st, chain, sx, 0, e, tm, out, runm);
+  int siters = 0;
+  const bool settled =
+      (a.debug_skip & 4) ? true : settle(d, st, chain, sx, 0, e, tm, out, runm, &siters);
+  if (a.stamps) {
+    const uint32_t nrec = __popcll(chain);
+    dbg_add(a, kDbgSettleIters, (uint64_t)siters);
+    dbg_add(a, kDbgWalkSteps, readlane32(wave_incl_sum32(nrec), 63));
+    dbg_add(a, kDbgWalkStepsMax, readlane32(wave_incl_max32(nrec), 63));
+  }
   const uint32_t x0 = readlane32((uint32_t)out, 63);
 
   // first message start (the batch end counts), tile-relative; kB if none
@@ -669,20 +688,25 @@ __global__ __launch_bounds__(256) void index_kernel(UnpackArgs a) {
   int m = 0, p = l;
   uint32_t ww = 0;
   bool merged = true;
-  if (l >= 1 && l < kTab) {
+  int msteps = 0;
+  if (!(a.debug_skip & 8) && l >= 1 && l < kTab) {
     for (int k = 0; k < 2 * kB; k++) {
+      msteps = k;
       if (p >= fms) {
         if (fms < kB) m = fms;           // every chain restarts at the first message start
         else if (p == (int)x0) m = kB;   // left the tile at chain 0's exit
         else merged = false;
         break;
       }
-      if ((lds_tm[p >> 6] >> (p & 63)) & 1) {
+      // the four reads of a step are independent: one LDS round trip per record
+      const uint64_t mk = lds_tm[p >> 6];
+      const uint32_t tag = d[p], c1 = d[p + 1], c9 = d[p + 9];
+      asm volatile("" ::"v"(tag), "v"(c1), "v"(c9));  // keep the reads ahead of the branch
+      if ((mk >> (p & 63)) & 1) {
         m = p;
         break;
       }
-      const uint32_t tag = d[p];
-      const uint32_t cnt = tag == 0 ? d[p + 1] : (tag == 0xff ? d[p + 9] : 0u);
+      const uint32_t cnt = tag == 0 ? c1 : (tag == 0xff ? c9 : 0u);
       ww += 1 + cnt;
       p += rec_len(tag, cnt);
     }
@@ -716,6 +740,10 @@ __global__ __launch_bounds__(256) void index_kernel(UnpackArgs a) {
     }
   }
   const uint32_t umask = (uint32_t)ballot(l >= 1 && l < kTab && !merged);
+  if (a.stamps) {
+    dbg_add(a, kDbgMergeSteps, readlane32(wave_incl_max32((uint32_t)msteps), 63));
+    if (umask) dbg_add(a, kDbgUmaskTiles, 1);
+  }
   if (l < kTab) a.t_delta[t * kTab + l] = delta;
   if (l == 0) {
     a.t_x0[t] = x0;
@@ -981,7 +1009,6 @@ __global__ __launch_bounds__(256) void expand_kernel(UnpackArgs a) {
   int nms_after;
   MsgWin win;
   const uint64_t mlast = tile_msg_starts(a, A, mfirst, lds_ms[wv], &nms_after, &win);
-  const uint64_t msw = lds_ms[wv][l];
 
   // ---- chain 0 -> the true chain: starts before the merge point come from a walk from E ----
   if (E > 0) {
@@ -1141,18 +1168,23 @@ __global__ __launch_bounds__(256) void expand_kernel(UnpackArgs a) {
   // the current message (window lane mcount): batches without a message start use it as is
   uint64_t cbase = readlane64(win.base, 0), ctotal = readlane64(win.total, 0);
   uint64_t cend = readlane64(win.end, 0);
+  const uint16_t* ms16 = (const uint16_t*)lds_ms[wv];
   for (int h = 0; h < 4; h++) {
-    const bool mine = (l >> 4) == h;
-    uint64_t bits = mine ? tm : 0;
-    const uint32_t c = __popcll(bits);
+    // lane l takes bits [16(l%4), +16) of sub-tile 16h + l/4: four lanes per sub-tile keep the
+    // serial bit loop about four times shorter than one lane per sub-tile would
+    const int src = 16 * h + (l >> 2);
+    const uint32_t sh = 16u * ((uint32_t)l & 3);
+    uint32_t bits = (uint32_t)(shfl64(tm, src) >> sh) & 0xffffu;
+    const uint32_t msp = ms16[4 * src + (l & 3)];
+    const uint32_t c = __popc(bits);
     const uint32_t Rin = wave_incl_sum32(c);
     const uint32_t nh = readlane32(Rin, 63);
     uint32_t r = Rin - c;
+    const uint32_t pbase = 64u * (uint32_t)src + sh;
     while (bits) {
-      const int b = lowest_bit(bits);
+      const uint32_t b = (uint32_t)__builtin_ctz(bits);
       bits &= bits - 1;
-      const uint32_t ms = (uint32_t)((msw >> b) & 1);
-      list[r++] = (uint16_t)((64 * l + b) | (ms << 12));
+      list[r++] = (uint16_t)((pbase + b) | (((msp >> b) & 1u) << 12));
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     for (uint32_t b0 = 0; b0 < nh; b0 += 64) {
@@ -1182,18 +1214,45 @@ __global__ __launch_bounds__(256) void expand_kernel(UnpackArgs a) {
       cnt = act ? cnt : 0u;
       const uint32_t w = act ? 1 + cnt : 0;
       const uint32_t inc = wave_incl_sum32(w);
-      const uint64_t Sx = sum + inc - w;
+      const uint32_t o = inc - w;  // words of the batch before the record
       const uint64_t msb = ballot(is_ms);
+      const uint64_t sel = dep_tab[tag];
+      const uint32_t wlo = __builtin_amdgcn_perm(dhi, dlo, (uint32_t)sel);
+      const uint32_t whi = __builtin_amdgcn_perm(dhi, dlo, (uint32_t)(sel >> 32));
+      const uint64_t word = ((uint64_t)whi << 32) | wlo;
+      const uint32_t len = 1 + nz + (uint32_t)(z | f) + (f ? 8 * cnt : 0u);
+      RunJob job;
+      job.n = 0;
       uint32_t km;
       int wl;  // window lane of the record's message
-      uint64_t mbase, mtotal, mend;
+      uint64_t mbase, mtotal, mend, wb;
+      bool special;  // records that end a message (or break it) go through the reference checks
       if (msb == 0) {
+        // the batch continues the current message: wave-uniform base, 32-bit lane arithmetic
         km = base_key;
         wl = (int)mcount;
         mbase = cbase;
         mtotal = ctotal;
         mend = cend;
+        const uint64_t sb = km ? sum - (km - 1) : excl + sum;  // message words before the batch
+        const uint64_t r1 = ctotal > sb ? ctotal - sb : 0;
+        const uint64_t r2 = cend > A ? cend - A : 0;
+        const uint32_t lim1 = r1 > 0xffffffffull ? 0xffffffffu : (uint32_t)r1;
+        const uint32_t lim2 = r2 > 0xffffffffull ? 0xffffffffu : (uint32_t)r2;
+        special = act && (inc >= lim1 || (uint32_t)p + len >= lim2);
+        wb = sb + o;
+        if (act && !special) {
+          uint64_t* const wp = a.words + (cbase + sb);
+          wp[o] = word;
+          if (cnt) {
+            job.n = cnt;
+            job.dst = cbase + sb + o + 1;
+            job.raw = f;
+            job.src = A + (uint32_t)p + 10;
+          }
+        }
       } else {
+        const uint64_t Sx = sum + o;
         const uint32_t key = is_ms ? (uint32_t)(Sx + 1) : 0;
         km = wave_incl_max32(key);
         if (km < base_key) km = base_key;
@@ -1201,27 +1260,20 @@ __global__ __launch_bounds__(256) void expand_kernel(UnpackArgs a) {
         mbase = shfl64(win.base, wl);
         mtotal = shfl64(win.total, wl);
         mend = shfl64(win.end, wl);
-      }
-      const uint64_t wb = km ? Sx - (km - 1) : excl + Sx;
-      const uint64_t sel = dep_tab[tag];
-      const uint32_t wlo = __builtin_amdgcn_perm(dhi, dlo, (uint32_t)sel);
-      const uint32_t whi = __builtin_amdgcn_perm(dhi, dlo, (uint32_t)(sel >> 32));
-      const uint64_t word = ((uint64_t)whi << 32) | wlo;
-      const uint32_t len = 1 + nz + (uint32_t)(z | f) + (f ? 8 * cnt : 0u);
-      const uint64_t pabs = A + p;
-      // records that end a message (or break it) go through the reference checks
-      const bool special = act && (wb + w >= mtotal || pabs + len >= mend);
-      RunJob job;
-      job.n = 0;
-      if (act && !special) {
-        a.words[mbase + wb] = word;
-        if (cnt) {
-          job.n = cnt;
-          job.dst = mbase + wb + 1;
-          job.raw = f;
-          job.src = pabs + 10;
+        wb = km ? Sx - (km - 1) : excl + Sx;
+        special = act && (wb + w >= mtotal || A + p + len >= mend);
+        if (act && !special) {
+          a.words[mbase + wb] = word;
+          if (cnt) {
+            job.n = cnt;
+            job.dst = mbase + wb + 1;
+            job.raw = f;
+            job.src = A + p + 10;
+          }
         }
-      } else if (special) {
+      }
+      const uint64_t pabs = A + p;
+      if (special) {
         MsgInfo mi;
         mi.base = mbase;
         mi.total = mtotal;

@@ -26,13 +26,17 @@ P = int(moff[-1].item())
 codec.unpack_messages(packed, moff, total, nbytes=P)
 codec.sync()
 names = {0: ["passA", "lookahead+exit", "entry wait", "count+publish", "passB", "finish(prev)"],
-         1: ["unsettled tiles", "table misses", "walk fails", "walks", "flagged msgs"]}
+         1: ["unsettled tiles", "table misses", "walk fails", "walks", "flagged msgs",
+             "umask tiles", "merge steps (max/tile)", "settle iters", "walk records (sum)",
+             "walk records (max/tile)"]}
 for which in (0, 1):
     out = (C.c_uint64 * 16)()
     if L.cpk_debug_stamps(which, out) != 0:
         continue
     if which == 1:  # event counters of the unpack pipeline
         print("unpack counters:", {nm: out[i] for i, nm in enumerate(names[1])})
+        nt = (P + 4095) // 4096
+        print("per tile:", {nm: round(out[i] / nt, 2) for i, nm in enumerate(names[1]) if i >= 5})
         continue
     tiles = out[15] or 1
     tot = sum(out[i] for i in range(15))

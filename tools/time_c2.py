@@ -25,7 +25,9 @@ for _ in range(10):
 for _ in range(10):
     c.unpack_messages(out, moff, total, nbytes=P, words=back)
 torch.cuda.synchronize()
-pm, pl, um, ul = c.timing_read()
+allt = c.timing_read_all()
+(pm, pl), (um, ul) = allt["pack"], allt["unpack"]
 U = total * 8
 print(f"{sys.argv[1]} {cfg}: pack {pm / pl:.4f} ms ({U / (pm / pl) / 1e6:.0f} GB/s of U)  "
       f"unpack {um / ul:.4f} ms  P/U {P / U:.3f}  roundtrip_ok {ok}")
+print("   kernels (ms): " + "  ".join(f"{k} {v[0] / v[1]:.4f}" for k, v in allt.items() if v[1]))
