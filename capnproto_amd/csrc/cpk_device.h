@@ -130,6 +130,11 @@ __device__ __forceinline__ uint64_t compact_nonzero(uint64_t x) {
   return out;
 }
 
+// Cross-lane hand-off through LDS inside one wave: the wave's LDS instructions execute in
+// order, so only the compiler has to be kept from moving memory accesses across this point
+// (it reasons per lane and may otherwise reorder a lane's access past another lane's).
+__device__ __forceinline__ void lane_handoff() { asm volatile("" ::: "memory"); }
+
 // Bit masks.
 __device__ __forceinline__ uint64_t mask_le(int l) { return (2ull << l) - 1; }   // bits 0..l
 __device__ __forceinline__ uint64_t mask_lt(int l) { return (1ull << l) - 1; }   // bits 0..l-1

@@ -435,30 +435,57 @@ __global__ __launch_bounds__(256) void pack_tiles_kernel(PackTileArgs a) {
     const int b_entry = b;
     stm.mark(2);
 
-    // ---- count pass (scalar): heads / coverage of every step, byte offsets -----------------
+    // ---- count pass: heads / coverage of every step, byte offsets --------------------------
     //   bytes(step) = sum over O words of (1 + nz) + 8 |R| + 2 |Z heads + F heads|
-    uint32_t vCOVlo = 0, vCOVhi = 0, vZHlo = 0, vZHhi = 0, vFHlo = 0, vFHhi = 0, vSoff = 0;
-    uint32_t agg32 = 0;
-    static_for<0, S>([&](auto sc) {
-      constexpr int s = decltype(sc)::value;
-      if (64 * s < nvalid) {
-        const uint64_t Z = readlane64(((uint64_t)vZhi << 32) | vZlo, s);
-        const uint64_t F = readlane64(((uint64_t)vFhi << 32) | vFlo, s);
-        const uint64_t R = readlane64(((uint64_t)vRhi << 32) | vRlo, s);
-        const uint64_t SY = readlane64(((uint64_t)vSYhi << 32) | vSYlo, s);
-        const StepRes r = resolve_step(Z, F, R, SY, b, 64 * s + 63 < nvalid);
-        b = r.b_out;
-        const uint64_t COV = r.covered | ~valid_mask(nvalid, s);
-        vCOVlo = setlane<s>(vCOVlo, (uint32_t)COV);
-        vCOVhi = setlane<s>(vCOVhi, (uint32_t)(COV >> 32));
-        vZHlo = setlane<s>(vZHlo, (uint32_t)r.Zheads);
-        vZHhi = setlane<s>(vZHhi, (uint32_t)(r.Zheads >> 32));
-        vFHlo = setlane<s>(vFHlo, (uint32_t)r.Fheads);
-        vFHhi = setlane<s>(vFHhi, (uint32_t)(r.Fheads >> 32));
-        vSoff = setlane<s>(vSoff, agg32);
-        agg32 += readlane32(vBase, s) + 2 * (uint32_t)__popcll(r.runheads);
-      }
-    });
+    // Lane s resolves step s from the masks parked in its lanes (vector unit, all steps at once);
+    // only the entry budgets run step to step on the scalar unit, and a step's exit budget
+    // depends on its entry budget only when the step has no sync at all.
+    uint32_t vCOVlo, vCOVhi, vZHlo, vZHhi, vFHlo, vFHhi, vSoff;
+    uint32_t agg32;
+    {
+      const uint64_t vZ = ((uint64_t)vZhi << 32) | vZlo;
+      const uint64_t vF = ((uint64_t)vFhi << 32) | vFlo;
+      const uint64_t vR = ((uint64_t)vRhi << 32) | vRlo;
+      const uint64_t vSY = ((uint64_t)vSYhi << 32) | vSYlo;
+      const bool lane_step = l < S && 64 * l < nvalid;
+      const bool lv = 64 * l + 63 < nvalid;  // the step's last word is valid
+      // exit budget of a step with a sync: the same for every entry budget (entry 0 here)
+      const StepRes r0 = resolve_step(vZ, vF, vR, vSY, 0, lv);
+      const uint32_t info = (vSY != 0 ? 0x80000000u : 0u) | (vZ != 0 ? 0x40000000u : 0u) |
+                            (uint32_t)r0.b_out;
+      uint32_t vB = 0;
+      static_for<0, S>([&](auto sc) {
+        constexpr int s = decltype(sc)::value;
+        if (64 * s < nvalid) {
+          vB = setlane<s>(vB, (uint32_t)b);
+          const uint32_t inf = readlane32(info, s);
+          if (inf & 0x80000000u) {
+            b = (int)(inf & 0x3ffu);
+          } else if (b > 63) {
+            b -= 64;  // the entering run covers the whole step
+          } else if (inf & 0x40000000u) {
+            b += 192;  // zero stretch: a head at word b
+          } else {  // word stretch: the first F word at / after b opens a run
+            const uint64_t Fm = readlane64(vF, s) & ~mask_lt(b);
+            b = Fm ? 192 + lowest_bit(Fm) : 0;
+          }
+        }
+      });
+      const StepRes r = resolve_step(vZ, vF, vR, vSY, (int)vB, lv);
+      const int kv = nvalid - 64 * l;
+      const uint64_t V = kv >= 64 ? ~0ull : (kv <= 0 ? 0ull : mask_lt(kv));
+      const uint64_t COV = r.covered | ~V;
+      vCOVlo = (uint32_t)COV;
+      vCOVhi = (uint32_t)(COV >> 32);
+      vZHlo = (uint32_t)r.Zheads;
+      vZHhi = (uint32_t)(r.Zheads >> 32);
+      vFHlo = (uint32_t)r.Fheads;
+      vFHhi = (uint32_t)(r.Fheads >> 32);
+      const uint32_t bytes = lane_step ? vBase + 2u * (uint32_t)__popcll(r.runheads) : 0u;
+      const uint32_t incl = wave_incl_sum32(bytes);
+      vSoff = incl - bytes;
+      agg32 = readlane32(incl, S - 1);
+    }
     if (MODE != kEmit && first_sync == T && l == 0) store_agent32(state + t, 0x80000000u | (uint32_t)b);
     const uint64_t agg = agg32;
     if constexpr (MODE == kCount) {

@@ -490,6 +490,7 @@ __device__ __forceinline__ void stage_store(const Staged& sg, uint8_t* d) {
     const int o = 16 * (64 * k + l);
     if (o < kB + kPad) *(u32x4*)(d + o) = sg.v[k];
   }
+  lane_handoff();  // other lanes read these bytes next
 }
 
 __device__ __forceinline__ void stage_load(const UnpackArgs& a, uint64_t A, Staged& sg) {
@@ -555,8 +556,12 @@ __device__ __forceinline__ uint64_t tile_msg_starts(const UnpackArgs& a, uint64_
     const uint64_t inm = ballot(in);
     if (inm != (~0ull << 1)) {
       mlast = (uint64_t)(w2.mw + 1 + __popcll(inm));
-      const uint64_t nx = mlast < a.nmsgs ? uniform64(a.in_off[mlast]) : P;
-      *nms_after = (int)((nx < P ? nx : P) - A);
+      if (nms_after) {
+        // message mlast is the window lane after the last one in the tile (a missing entry
+        // reads ~0): no extra round trip to in_off
+        const uint64_t nx = readlane64(w2.start, (int)(mlast - (uint64_t)w2.mw));
+        *nms_after = (int)((nx < P ? nx : P) - A);
+      }
       break;
     }
     // 63 starts in this window: continue with the next
@@ -682,6 +687,7 @@ __global__ __launch_bounds__(256) void index_kernel(UnpackArgs a) {
   a.tm[t * 64 + l] = tm;
   a.t_wex[t * 64 + l] = Wex;
   lds_tm[l] = tm;
+  lane_handoff();
 
   // ---- merge table: lane e (1..15) walks the chain entered at byte e until it meets chain 0;
   //      a chain that never does (parity-locked or raw-run data) is walked to the tile end
@@ -976,39 +982,71 @@ __global__ __launch_bounds__(256) void resolve2_kernel(UnpackArgs a) {
   if (l == 0 && valid) a.gdesc[t / kGroup] = kDescAgg | (segm ? kSegBit : 0) | sum;
 }
 
-// 5. Expand: one wave per tile.
-__global__ __launch_bounds__(256) void expand_kernel(UnpackArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds_data[4][kB + kPad];
-  __shared__ uint64_t lds_ms[4][64];
-  // per wave 1 KiB: chain-0 masks + walked starts while the entry is patched, then the record
-  // list of a quarter tile (<= 512 records of >= 2 bytes)
-  __shared__ uint64_t lds_aux[4][kB / 32];
-  __shared__ uint64_t dep_tab[256];
-  const int l = lane_id();
-  const int wv = (int)uniform32(threadIdx.x >> 6);  // wave-uniform (keeps tile math scalar)
-  dep_tab[threadIdx.x] = make_dep(threadIdx.x);
-  __syncthreads();
-  const uint64_t t = (uint64_t)blockIdx.x * 4 + wv;
-  if (t >= a.ntiles) return;
-  uint8_t* d = lds_data[wv];
-  uint64_t* aux = lds_aux[wv];
-  uint16_t* list = (uint16_t*)aux;
-  const uint32_t lut = deposit_sel((uint32_t)l & 15);
-  const uint64_t A = t * kB;
-
-  // every load that depends only on t first, then what depends on them
+// Tile inputs that depend only on the tile index: prefetched one tile ahead by expand_kernel.
+struct ExpandFetch {
   Staged stg;
-  stage_load(a, A, stg);
-  const uint64_t mfirst = uniform64(a.tile_first[t]);
-  uint64_t tm = a.tm[t * 64 + l];
-  const uint32_t E = uniform32(a.t_ent[t]);
-  const uint32_t fms = uniform32(a.t_fms[t]);
-  // words of the message at the tile start before this tile (tile values are final: no wait)
-  const uint64_t excl = lookback2(a.desc, a.gdesc, t, kSegBit, a.err);
-  stage_store(stg, d);
-  int nms_after;
+  uint64_t tm;        // chain-0 record-start mask of the lane's sub-tile
+  uint64_t d1, d2;    // look-back values: in-group predecessors, groups before
+  uint64_t mfirst;
+  uint32_t E, fms;
+};
+
+__device__ __forceinline__ void expand_fetch(const UnpackArgs& a, uint64_t t, ExpandFetch& f) {
+  const int l = lane_id();
+  stage_load(a, t * kB, f.stg);
+  f.mfirst = uniform64(a.tile_first[t]);
+  f.tm = a.tm[t * 64 + l];
+  f.E = uniform32(a.t_ent[t]);
+  f.fms = uniform32(a.t_fms[t]);
+  const uint64_t g = t / kGroup;
+  const int j = (int)(t - g * kGroup);
+  f.d1 = l < j ? (a.desc[t - 1 - (uint64_t)l] & kDescValue) : 0;
+  const int64_t G = (int64_t)g - 1;
+  f.d2 = G - l >= 0 ? (a.gdesc[G - l] & kDescValue) : 0;
+}
+
+// Exclusive (segmented) word prefix of tile t from the final tile / group values of
+// resolve2_kernel (prefetched by expand_fetch: the in-group predecessors and up to 64 groups
+// before); farther groups are loaded only when none of those holds a message start.
+__device__ __forceinline__ uint64_t lookback_final(const UnpackArgs& a, uint64_t t,
+                                                   uint64_t d1, uint64_t d2) {
+  const int l = lane_id();
+  const uint64_t g = t / kGroup;
+  const int j = (int)(t - g * kGroup);
+  int64_t G = (int64_t)g - 1;
+  uint64_t excl = 0;
+  if (j > 0) {
+    excl = reduce_nearest(d1, j - 1, kSegBit);
+    if (excl & kSegBit) return excl & ~kSegBit;
+  }
+  while (G >= 0) {
+    const uint64_t sb = ballot(G - l >= 0 && (d2 & kSegBit));
+    const int k = sb ? lowest_bit(sb) : 63;
+    excl = seg_combine(reduce_nearest(d2, k, kSegBit), excl, kSegBit);
+    if (sb) break;
+    G -= 64;
+    d2 = G - l >= 0 ? (a.gdesc[G - l] & kDescValue) : 0;
+  }
+  return excl & ~kSegBit;
+}
+
+// One tile of expand_kernel.
+__device__ __forceinline__ void expand_tile(const UnpackArgs& a, uint64_t t, const ExpandFetch& f,
+                                            uint8_t* d, uint64_t* aux, uint64_t* msl,
+                                            const uint64_t* dep_tab, uint32_t lut) {
+  const int l = lane_id();
+  uint16_t* list = (uint16_t*)aux;
+  const uint64_t A = t * kB;
+  lane_handoff();  // the previous tile's reads of the wave's LDS stay before this tile's writes
+  const uint64_t mfirst = f.mfirst;
+  uint64_t tm = f.tm;
+  const uint32_t E = f.E;
+  const uint32_t fms = f.fms;
+  // words of the message at the tile start before this tile (tile values are final)
+  const uint64_t excl = lookback_final(a, t, f.d1, f.d2);
+  stage_store(f.stg, d);
   MsgWin win;
-  const uint64_t mlast = tile_msg_starts(a, A, mfirst, lds_ms[wv], &nms_after, &win);
+  const uint64_t mlast = tile_msg_starts(a, A, mfirst, msl, nullptr, &win);
 
   // ---- chain 0 -> the true chain: starts before the merge point come from a walk from E ----
   if (E > 0) {
@@ -1017,17 +1055,32 @@ __global__ __launch_bounds__(256) void expand_kernel(UnpackArgs a) {
     aux[64 + l] = 0;
     if (pre_ok && E < fms) {
       aux[l] = tm;
+      lane_handoff();
       if (l == 0) {
+        // the reads of a step are independent (one LDS round trip per record); the walked
+        // starts of a sub-tile collect in a register until the walk leaves it
         int p = (int)E;
         uint64_t* fix = aux + 64;
+        int cur = p >> 6;
+        uint64_t fm = 0;
         while (p < (int)fms && p < kB) {
-          if ((aux[p >> 6] >> (p & 63)) & 1) break;
-          fix[p >> 6] |= 1ull << (p & 63);
-          p += record_len(d, p);
+          const uint64_t mk = aux[p >> 6];
+          const uint32_t tg = d[p], c9 = d[p + 9];
+          asm volatile("" ::"v"(tg), "v"(c9));
+          if ((mk >> (p & 63)) & 1) break;
+          if ((p >> 6) != cur) {
+            fix[cur] = fm;
+            fm = 0;
+            cur = p >> 6;
+          }
+          fm |= 1ull << (p & 63);
+          p += rec_len(tg, c9);
         }
+        fix[cur] = fm;
         m = p < (int)fms ? p : (int)fms;
       }
       m = (int)readlane32((uint32_t)m, 0);
+      lane_handoff();
     }
     const int s = 64 * l;
     const uint64_t below = m <= s ? 0ull : (m >= s + 64 ? ~0ull : mask_lt(m - s));
@@ -1060,7 +1113,7 @@ __global__ __launch_bounds__(256) void expand_kernel(UnpackArgs a) {
     // general path: one lane per record, record positions by binary search, message of each
     // record from the window (see handle_record for the reference checks)
     const uint32_t R = Rall_incl - cnt_all;
-    const uint64_t* msw_all = lds_ms[wv];
+    const uint64_t* msw_all = msl;
     int64_t mcur = (int64_t)mfirst - 1;
     uint64_t nxt_start = readlane64(win.start, 1);
     uint64_t sum = 0;
@@ -1168,8 +1221,8 @@ __global__ __launch_bounds__(256) void expand_kernel(UnpackArgs a) {
   // the current message (window lane mcount): batches without a message start use it as is
   uint64_t cbase = readlane64(win.base, 0), ctotal = readlane64(win.total, 0);
   uint64_t cend = readlane64(win.end, 0);
-  const uint16_t* ms16 = (const uint16_t*)lds_ms[wv];
-  for (int h = 0; h < 4; h++) {
+  const uint16_t* ms16 = (const uint16_t*)msl;
+  for (int h = 0; h < ((a.debug_skip & 32) ? 0 : 4); h++) {
     // lane l takes bits [16(l%4), +16) of sub-tile 16h + l/4: four lanes per sub-tile keep the
     // serial bit loop about four times shorter than one lane per sub-tile would
     const int src = 16 * h + (l >> 2);
@@ -1187,7 +1240,7 @@ __global__ __launch_bounds__(256) void expand_kernel(UnpackArgs a) {
       list[r++] = (uint16_t)((pbase + b) | (((msp >> b) & 1u) << 12));
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    for (uint32_t b0 = 0; b0 < nh; b0 += 64) {
+    for (uint32_t b0 = 0; b0 < ((a.debug_skip & 16) ? 0u : nh); b0 += 64) {
       const uint32_t rr = b0 + l;
       const bool act = rr < nh;
       // branch-free body: an inactive lane reads a real entry (LDS stays in bounds) and is
@@ -1299,6 +1352,28 @@ __global__ __launch_bounds__(256) void expand_kernel(UnpackArgs a) {
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
+}
+
+
+// 5. Expand: one wave per tile (a persistent form with the next tile's inputs prefetched ran
+// slower: the prefetch registers cost occupancy and spills).
+__global__ __launch_bounds__(256) void expand_kernel(UnpackArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds_data[4][kB + kPad];
+  __shared__ uint64_t lds_ms[4][64];
+  // per wave 1 KiB: chain-0 masks + walked starts while the entry is patched, then the record
+  // list of a quarter tile (<= 512 records of >= 2 bytes)
+  __shared__ uint64_t lds_aux[4][kB / 32];
+  __shared__ uint64_t dep_tab[256];
+  const int l = lane_id();
+  const int wv = (int)uniform32(threadIdx.x >> 6);  // wave-uniform (keeps tile math scalar)
+  dep_tab[threadIdx.x] = make_dep(threadIdx.x);
+  __syncthreads();
+  const uint64_t t = (uint64_t)blockIdx.x * 4 + wv;
+  if (t >= a.ntiles) return;
+  ExpandFetch f;
+  expand_fetch(a, t, f);
+  expand_tile(a, t, f, lds_data[wv], lds_aux[wv], lds_ms[wv], dep_tab,
+              deposit_sel((uint32_t)l & 15));
 }
 
 // 6. Serial re-decode of flagged messages: one wave per message; lane 0 walks the records of a
