@@ -35,12 +35,16 @@ namespace {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-// v_writelane: lane `s` (compile-time) of `dst` takes the wave-uniform value `v`.
+// v_writelane: lane `s` (compile-time) of `dst` takes the wave-uniform value `v`.  Inline asm
+// (this compiler has no writelane builtin) hides the SGPR read from the hazard recognizer, so
+// the value goes through an SALU move first: a writelane reading an SGPR that a VALU (ballot)
+// has just written returned stale data.
 template <int L>
 __device__ __forceinline__ uint32_t setlane(uint32_t dst, uint32_t v) {
-  asm("v_writelane_b32 %0, %1, %2"
-      : "+v"(dst)
-      : "s"((uint32_t)__builtin_amdgcn_readfirstlane((int)v)), "i"(L));
+  uint32_t tmp;
+  asm volatile("s_mov_b32 %1, %2\n\ts_nop 0\n\tv_writelane_b32 %0, %1, %3"
+               : "+v"(dst), "=&s"(tmp)
+               : "s"((uint32_t)__builtin_amdgcn_readfirstlane((int)v)), "i"(L));
   return dst;
 }
 
@@ -292,20 +296,19 @@ __global__ __launch_bounds__(256) void pack_tiles_kernel(PackTileArgs a) {
     const uint64_t tend = tbase + T < N ? tbase + T : N;
     const int nvalid = FULL ? T : (int)(tend - tbase);
     const int last = nvalid - 1;
-    uint64_t zc = 0, rc = 0;
+    uint64_t zc0 = 0, rc0 = 0;  // class of the word before the tile
     if (tbase > 0) {
       const uint64_t pw = uniform64(cur.pw);
-      zc = pw == 0;
-      rc = __popc(tag_of((uint32_t)pw, (uint32_t)(pw >> 32))) >= 7;
+      zc0 = pw == 0;
+      rc0 = __popc(tag_of((uint32_t)pw, (uint32_t)(pw >> 32))) >= 7;
     }
 
     // ---- pass A --------------------------------------------------------------------------
-    // per-step masks parked in VGPR lanes (lane s = step s) to keep SGPR pressure low
+    // per step: tags and the Z / R / F ballots, parked in VGPR lanes (lane s = step s); the sync
+    // masks and state-independent byte counts of all steps are then formed at once in lanes
     uint32_t vSYlo = 0, vSYhi = 0, vFlo = 0, vFhi = 0, vZlo = 0, vZhi = 0, vRlo = 0, vRhi = 0;
-    uint32_t vNsa = 0, vBase = 0;
+    uint32_t vNsa = 0, vBase = 0, vOb = 0;
     uint32_t tagpk[S / 2];
-    bool lastZ = false, lastR = false;
-    int first_sync = T, sg = -1;
     static_for<0, S>([&](auto sc) {
       constexpr int s = decltype(sc)::value;
       const uint64_t x = cur.x[s];
@@ -316,39 +319,61 @@ __global__ __launch_bounds__(256) void pack_tiles_kernel(PackTileArgs a) {
       } else {
         tagpk[s >> 1] = tag;
       }
-      const uint64_t V = valid_mask(nvalid, s);
-      const uint64_t C = readlane64(cur.cb, s);
-      const uint64_t Z = ballot(x == 0) & V;
-      const uint64_t R = ballot(__popc(tag) >= 7) & V;
-      const uint64_t Fs = ballot(tag == 0xff) & V;
-      const uint64_t O = V & ~Z & ~R;
-      const uint64_t SY = C | O | (Z & ~((Z << 1) | zc)) | (R & ~((R << 1) | rc)) | ~V;
-      vSYlo = setlane<s>(vSYlo, (int)(uint32_t)SY);
-      vSYhi = setlane<s>(vSYhi, (int)(uint32_t)(SY >> 32));
-      vFlo = setlane<s>(vFlo, (int)(uint32_t)Fs);
-      vFhi = setlane<s>(vFhi, (int)(uint32_t)(Fs >> 32));
-      vZlo = setlane<s>(vZlo, (int)(uint32_t)Z);
-      vZhi = setlane<s>(vZhi, (int)(uint32_t)(Z >> 32));
-      vRlo = setlane<s>(vRlo, (int)(uint32_t)R);
-      vRhi = setlane<s>(vRhi, (int)(uint32_t)(R >> 32));
-      // state-independent bytes of the step: 1 + nz per O word, 8 per R word
+      const uint64_t Z = ballot(x == 0);  // words past the batch end load as 0: masked below
+      const uint64_t R = ballot(__popc(tag) >= 7);
+      const uint64_t Fs = ballot(tag == 0xff);
+      vFlo = setlane<s>(vFlo, (uint32_t)Fs);
+      vFhi = setlane<s>(vFhi, (uint32_t)(Fs >> 32));
+      vZlo = setlane<s>(vZlo, (uint32_t)Z);
+      vZhi = setlane<s>(vZhi, (uint32_t)(Z >> 32));
+      vRlo = setlane<s>(vRlo, (uint32_t)R);
+      vRhi = setlane<s>(vRhi, (uint32_t)(R >> 32));
+      // sum of nz over the O words of the step (their bytes are 1 + nz)
       const uint32_t nz = __popc(tag);
-      const uint32_t ob = (x != 0 && nz < 7) ? nz : 0;  // O words: 1 + nz = |O| + sum nz
-      const uint32_t base = (uint32_t)(__popcll(O) + 8 * __popcll(R) + __popcll(ballot(ob & 1)) +
-                                       2 * __popcll(ballot(ob & 2)) + 4 * __popcll(ballot(ob & 4)));
-      vBase = setlane<s>(vBase, base);
-      const uint64_t m = SY & V;
-      if (m) {
-        if (first_sync == T) first_sync = 64 * s + lowest_bit(m);
-        sg = 64 * s + highest_bit(m);
-      }
-      zc = Z >> 63;
-      rc = R >> 63;
-      if (s == (last >> 6)) {
-        lastZ = (Z >> (last & 63)) & 1;
-        lastR = (R >> (last & 63)) & 1;
-      }
+      const uint32_t ob = (x != 0 && nz < 7) ? nz : 0;
+      vOb = setlane<s>(vOb, (uint32_t)(__popcll(ballot(ob & 1)) + 2 * __popcll(ballot(ob & 2)) +
+                                       4 * __popcll(ballot(ob & 4))));
     });
+    bool lastZ, lastR;
+    int first_sync = T, sg = -1;
+    {
+      const int kv = nvalid - 64 * l;
+      const uint64_t V = FULL ? ~0ull : (kv >= 64 ? ~0ull : (kv <= 0 ? 0ull : mask_lt(kv)));
+      const uint64_t Z = (((uint64_t)vZhi << 32) | vZlo) & V;
+      const uint64_t R = (((uint64_t)vRhi << 32) | vRlo) & V;
+      const uint64_t F = (((uint64_t)vFhi << 32) | vFlo) & V;
+      // class of the word before the step: the previous lane's last word (tile: word tbase-1)
+      uint32_t zc = dpp_src<0x111, 0xf>((uint32_t)(Z >> 32)) >> 31;
+      uint32_t rc = dpp_src<0x111, 0xf>((uint32_t)(R >> 32)) >> 31;
+      if (l == 0) {
+        zc = (uint32_t)zc0;
+        rc = (uint32_t)rc0;
+      }
+      const uint64_t C = cur.cb;  // lane s: chunk-start bits of step s
+      const uint64_t O = V & ~Z & ~R;
+      const uint64_t SY =
+          C | O | (Z & ~((Z << 1) | zc)) | (R & ~((R << 1) | rc)) | ~V;
+      vSYlo = (uint32_t)SY;
+      vSYhi = (uint32_t)(SY >> 32);
+      vZlo = (uint32_t)Z;
+      vZhi = (uint32_t)(Z >> 32);
+      vRlo = (uint32_t)R;
+      vRhi = (uint32_t)(R >> 32);
+      vFlo = (uint32_t)F;
+      vFhi = (uint32_t)(F >> 32);
+      // state-independent bytes of the step: 1 + nz per O word, 8 per R word
+      vBase = (uint32_t)(__popcll(O) + 8 * __popcll(R)) + vOb;
+      const uint64_t m = l < S ? (SY & V) : 0ull;
+      const uint64_t bm = ballot(m != 0);
+      if (bm) {
+        const int fl = lowest_bit(bm), hl = highest_bit(bm);
+        first_sync = 64 * fl + lowest_bit(readlane64(m, fl));
+        sg = 64 * hl + highest_bit(readlane64(m, hl));
+      }
+      const int ls = last >> 6;
+      lastZ = (readlane64(Z, ls) >> (last & 63)) & 1;
+      lastR = (readlane64(R, ls) >> (last & 63)) & 1;
+    }
     stm.mark(0);
     // count pass: pass A was the last use of the words, the next tile's can be on their way
     if constexpr (MODE == kCount) {
