@@ -183,7 +183,8 @@ __device__ __forceinline__ void load_tile(const PackTileArgs& a, uint64_t t, Til
 constexpr int kFused = 0, kCount = 1, kEmit = 2;
 
 template <int S, bool PF, bool STAMPS, int MODE = kFused>
-__global__ __launch_bounds__(256) void pack_tiles_kernel(PackTileArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S <= 8 ? 6 : 2, 8))) void pack_tiles_kernel(
+    PackTileArgs a) {
   static_assert(S >= 2 && S <= 16 && (S % 2) == 0, "S steps per tile");
   constexpr int T = 64 * S;
   // Per-wave staging ring: a tile's records occupy [base, base + 32 + bytes) (16 B pads at both
