@@ -44,7 +44,9 @@ constexpr int kB = (int)kUnpackTileBytes;  // 4096
 constexpr int kPad = 16;
 constexpr int kDead = 1 << 24;  // chain ran into the end of the batch
 constexpr uint64_t kSegBit = 1ull << 61;
-constexpr int kTab = 16;                    // entries 0..15 get a merge table
+constexpr int kTab = 16;                    // merge-table slots per tile
+constexpr int kTabWalk = 10;                // entries 1..9 are walked (a record that is not a
+                                            // raw run ends at most 9 bytes into the next tile)
 constexpr uint32_t kTileUnsettled = 1;      // lane fixed point hit its iteration cap
 constexpr uint32_t kTileHasStart = 2;       // a message starts inside the tile
 constexpr int kWalkCap = 4096;              // records a resolve thread walks before giving up
@@ -695,7 +697,7 @@ __global__ __launch_bounds__(256) void index_kernel(UnpackArgs a) {
   uint32_t ww = 0;
   bool merged = true;
   int msteps = 0;
-  if (!(a.debug_skip & 8) && l >= 1 && l < kTab) {
+  if (!(a.debug_skip & 8) && l >= 1 && l < kTabWalk) {
     for (int k = 0; k < 2 * kB; k++) {
       msteps = k;
       if (p >= fms) {
@@ -833,7 +835,7 @@ __device__ bool classify(const UnpackArgs& a, uint64_t t, uint32_t E, uint32_t* 
     *wpre = 0;
     return true;
   }
-  if (E < (uint32_t)kTab) {
+  if (E < (uint32_t)kTabWalk) {
     const int32_t dl = a.t_delta[t * kTab + E];
     if ((a.t_umask[t] >> E) & 1) {
       *merged = false;
