@@ -13,24 +13,25 @@
 //                       segment table with the reference's checks; yields the flat size.
 //   2. scan             message word offsets (cpk_scan.hip).
 //   3. index_kernel     one wave per tile.  Resolves "chain 0", the chain entered at the tile's
-//                       first byte: each lane walks its 64-byte sub-tile speculatively, then a
-//                       fixed point settles every lane's true entry.  Stores chain 0's record-start
-//                       masks (512 B per tile), its exit, word counts, and for entries 1..15 whether
-//                       (and with what word difference) their chain merges into chain 0.
-//   4. resolve_kernel   one thread per tile.  The true entry is the predecessor's chain-0 exit
-//                       (exact when the predecessor's own entry merged -- which the predecessor's
-//                       thread checks -- or the predecessor holds a message start).  Checks that
-//                       this tile's entry merges (table, or a walk through global memory for an
-//                       entry past a raw run), words before the first message start, and writes
-//                       segmented tile values + 64-tile group aggregates for the word offsets.
-//                       An entry that does not merge flags its message for fallback_kernel.
+//                       first byte: each lane walks its 64-byte sub-tile speculatively (message
+//                       clips kept out of the step), then a fixed point settles every lane's true
+//                       entry.  Stores chain 0's record-start masks (512 B per tile), its exit, word
+//                       counts, and a merge table: for entries 1..9 the word difference to chain 0
+//                       where their chain meets it, or their own exit and words when it never does.
+//   4. resolve1_kernel  one thread per tile: optimistic entry = the predecessor's chain-0 exit;
+//                       table lookup (or a walk through global memory for an entry past a raw
+//                       run); marks the tiles whose entry does not merge, per 64-tile group.
+//      resolve2_kernel  an optimistic entry is wrong only after such a tile with no message start
+//                       in between: those stretches are replayed from their first tile; writes
+//                       segmented tile word values and 64-tile group aggregates.
 //   5. expand_kernel    one wave per tile.  Word offset by a look-back over the (final) tile
-//                       values, chain 0 patched for the true entry, then records are expanded
-//                       one lane per record, 64 consecutive records at a time (coalesced stores);
-//                       zero and raw runs are written cooperatively by the wave.
-//   6. fallback_kernel  flagged messages, decoded serially (one wave per message).  Canonical
-//                       dense streams never need it; long raw-run (text) streams whose tiles
-//                       chain 0 cannot synchronise with do.
+//                       values (both hops' loads in one round trip), chain 0 patched for the true
+//                       entry, then records are expanded one lane per record, 64 consecutive
+//                       records at a time (record list per quarter tile, built four lanes per
+//                       sub-tile; coalesced stores); zero and raw runs are written by the wave.
+//   6. fallback_kernel  messages flagged by an unsettled fixed point or a capped walk, decoded
+//                       serially (one wave per message).  None of the benchmark configurations
+//                       needs it; the error tests do.
 #include <limits.h>
 
 #include "cpk_device.h"
