@@ -639,8 +639,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S <= 8 ? 6 
     pend.on = true;
     stm.mark(5);
     };
-    if (t * T + T <= N) tile(std::true_type{});
-    else tile(std::false_type{});
+    // one instantiation of the tile body (the partial last tile's masks cost a few VALU per
+    // step): a second, full-tile copy doubles the kernel's code for no measurable gain
+    tile(std::false_type{});
     if (PF) cur = nxt;
   }  // tile loop
   if (pend.on) finish(pend);
