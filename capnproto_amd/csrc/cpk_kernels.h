@@ -7,7 +7,7 @@
 
 namespace cpk {
 
-constexpr int kPackSteps = 8;                   // words per pack tile = 64 * kPackSteps
+constexpr int kPackSteps = 16;                  // words per pack tile = 64 * kPackSteps
 constexpr uint64_t kPackTileWords = 64 * kPackSteps;
 constexpr uint64_t kUnpackTileBytes = 4096;     // packed bytes per unpack tile (>= 2050)
 

@@ -183,7 +183,7 @@ __device__ __forceinline__ void load_tile(const PackTileArgs& a, uint64_t t, Til
 constexpr int kFused = 0, kCount = 1, kEmit = 2;
 
 template <int S, bool PF, bool STAMPS, int MODE = kFused>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S <= 8 ? 6 : 2, 8))) void pack_tiles_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S <= 8 ? 6 : 3, 8))) void pack_tiles_kernel(
     PackTileArgs a) {
   static_assert(S >= 2 && S <= 16 && (S % 2) == 0, "S steps per tile");
   constexpr int T = 64 * S;
@@ -715,7 +715,7 @@ __global__ void tile_first_kernel(const uint64_t* __restrict__ pos, uint64_t npo
 // ---------------------------------------------------------------------------------------------
 int pack_steps() {
   static int steps = [] {
-    const char* e = getenv("CPK_PACK_STEPS");  // tuning knob: 8 or 16 (default)
+    const char* e = getenv("CPK_PACK_STEPS");  // tuning knob: 4, 8 or 16 (default)
     const int v = e ? atoi(e) : kPackSteps;
     return (v == 8 || v == 16 || v == 4) ? v : kPackSteps;
   }();
@@ -739,11 +739,13 @@ hipError_t launch_pack_s(const PackTileArgs& a, hipStream_t stream) {
   return hipGetLastError();
 }
 
-// Tuning knob (env CPK_PACK_PF=1): prefetch the next tile into registers during the current one.
+// Prefetch of the next tile's words into registers during the current tile: on by default at
+// 16 steps per tile, where LDS (the staging ring) and not registers bounds occupancy at 3 waves
+// per SIMD; off at 8 steps, where the registers would cost occupancy.  Env CPK_PACK_PF=0/1.
 static bool pack_prefetch() {
   static const bool on = [] {
     const char* e = getenv("CPK_PACK_PF");
-    return e && atoi(e) != 0;
+    return e ? atoi(e) != 0 : pack_steps() == 16;
   }();
   return on;
 }
@@ -751,9 +753,8 @@ static bool pack_prefetch() {
 // Two-pass form (default).  stage 0: count pass, persistent grid (its waves hand entry budgets
 // over); stage 1: emit pass, one wave per tile.  The caller scans tile_bytes into tile_off in
 // between.
-hipError_t launch_pack_stage(int stage, const PackTileArgs& a, hipStream_t stream) {
-  if (a.ntiles == 0) return hipSuccess;
-  constexpr int S = kPackSteps;
+template <int S>
+hipError_t launch_pack_stage_s(int stage, const PackTileArgs& a, hipStream_t stream) {
   if (stage == 0) {
     static const unsigned cap =
         resident_blocks((const void*)pack_tiles_kernel<S, false, false, kCount>, 256, 0);
@@ -766,6 +767,15 @@ hipError_t launch_pack_stage(int stage, const PackTileArgs& a, hipStream_t strea
                        dim3((unsigned)((a.ntiles + 3) / 4)), dim3(256), 0, stream, a);
   }
   return hipGetLastError();
+}
+
+hipError_t launch_pack_stage(int stage, const PackTileArgs& a, hipStream_t stream) {
+  if (a.ntiles == 0) return hipSuccess;
+  switch (pack_steps()) {
+    case 4: return launch_pack_stage_s<4>(stage, a, stream);
+    case 8: return launch_pack_stage_s<8>(stage, a, stream);
+    default: return launch_pack_stage_s<16>(stage, a, stream);
+  }
 }
 
 bool pack_fused() {
@@ -783,8 +793,8 @@ hipError_t launch_pack_tiles(const PackTileArgs& a, hipStream_t stream) {
   const bool pf = pack_prefetch();
   switch (pack_steps()) {
     case 4: return pf ? launch_pack_s<4, true>(a, stream) : launch_pack_s<4, false>(a, stream);
-    case 16: return pf ? launch_pack_s<16, true>(a, stream) : launch_pack_s<16, false>(a, stream);
-    default: return pf ? launch_pack_s<8, true>(a, stream) : launch_pack_s<8, false>(a, stream);
+    case 8: return pf ? launch_pack_s<8, true>(a, stream) : launch_pack_s<8, false>(a, stream);
+    default: return pf ? launch_pack_s<16, true>(a, stream) : launch_pack_s<16, false>(a, stream);
   }
 }
 
