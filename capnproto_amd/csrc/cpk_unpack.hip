@@ -1035,7 +1035,7 @@ __device__ __forceinline__ uint64_t lookback_final(const UnpackArgs& a, uint64_t
 
 // One tile of expand_kernel.
 __device__ __forceinline__ void expand_tile(const UnpackArgs& a, uint64_t t, const ExpandFetch& f,
-                                            uint8_t* d, uint64_t* aux, uint64_t* msl,
+                                            uint8_t* d, uint64_t* aux,
                                             const uint64_t* dep_tab, uint32_t lut) {
   const int l = lane_id();
   uint16_t* list = (uint16_t*)aux;
@@ -1049,7 +1049,11 @@ __device__ __forceinline__ void expand_tile(const UnpackArgs& a, uint64_t t, con
   const uint64_t excl = lookback_final(a, t, f.d1, f.d2);
   stage_store(f.stg, d);
   MsgWin win;
-  const uint64_t mlast = tile_msg_starts(a, A, mfirst, msl, nullptr, &win);
+  // message starts: built in aux, then kept in registers (lane = sub-tile), so that aux is free
+  // for the entry patch and the record lists
+  const uint64_t mlast = tile_msg_starts(a, A, mfirst, aux, nullptr, &win);
+  const uint64_t msw = aux[l];
+  lane_handoff();
 
   // ---- chain 0 -> the true chain: starts before the merge point come from a walk from E ----
   if (E > 0) {
@@ -1116,7 +1120,6 @@ __device__ __forceinline__ void expand_tile(const UnpackArgs& a, uint64_t t, con
     // general path: one lane per record, record positions by binary search, message of each
     // record from the window (see handle_record for the reference checks)
     const uint32_t R = Rall_incl - cnt_all;
-    const uint64_t* msw_all = msl;
     int64_t mcur = (int64_t)mfirst - 1;
     uint64_t nxt_start = readlane64(win.start, 1);
     uint64_t sum = 0;
@@ -1152,7 +1155,9 @@ __device__ __forceinline__ void expand_tile(const UnpackArgs& a, uint64_t t, con
       const uint64_t pabs = A + p;
       const Rec rc = read_rec(d, p);
       const uint32_t w = act ? 1 + rc.cnt : 0;
-      const bool is_ms = act && ((msw_all[p >> 6] >> (p & 63)) & 1);
+      // every lane takes part in the shuffle (an inactive source lane would read as 0)
+      const uint64_t msrc = shfl64(msw, p >> 6);
+      const bool is_ms = act && ((msrc >> (p & 63)) & 1);
       const uint32_t inc = wave_incl_sum32(w);
       const uint64_t Sx = sum + inc - w;
       const uint32_t key = is_ms ? (uint32_t)(Sx + 1) : 0;
@@ -1224,14 +1229,13 @@ __device__ __forceinline__ void expand_tile(const UnpackArgs& a, uint64_t t, con
   // the current message (window lane mcount): batches without a message start use it as is
   uint64_t cbase = readlane64(win.base, 0), ctotal = readlane64(win.total, 0);
   uint64_t cend = readlane64(win.end, 0);
-  const uint16_t* ms16 = (const uint16_t*)msl;
   for (int h = 0; h < ((a.debug_skip & 32) ? 0 : 4); h++) {
     // lane l takes bits [16(l%4), +16) of sub-tile 16h + l/4: four lanes per sub-tile keep the
     // serial bit loop about four times shorter than one lane per sub-tile would
     const int src = 16 * h + (l >> 2);
     const uint32_t sh = 16u * ((uint32_t)l & 3);
     uint32_t bits = (uint32_t)(shfl64(tm, src) >> sh) & 0xffffu;
-    const uint32_t msp = ms16[4 * src + (l & 3)];
+    const uint32_t msp = (uint32_t)(shfl64(msw, src) >> sh) & 0xffffu;
     const uint32_t c = __popc(bits);
     const uint32_t Rin = wave_incl_sum32(c);
     const uint32_t nh = readlane32(Rin, 63);
@@ -1360,11 +1364,11 @@ __device__ __forceinline__ void expand_tile(const UnpackArgs& a, uint64_t t, con
 
 // 5. Expand: one wave per tile (a persistent form with the next tile's inputs prefetched ran
 // slower: the prefetch registers cost occupancy and spills).
-__global__ __launch_bounds__(256) void expand_kernel(UnpackArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) void expand_kernel(
+    UnpackArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds_data[4][kB + kPad];
-  __shared__ uint64_t lds_ms[4][64];
-  // per wave 1 KiB: chain-0 masks + walked starts while the entry is patched, then the record
-  // list of a quarter tile (<= 512 records of >= 2 bytes)
+  // per wave 1 KiB: message starts while they are found, chain-0 masks + walked starts while
+  // the entry is patched, then the record list of a quarter tile (<= 512 records of >= 2 bytes)
   __shared__ uint64_t lds_aux[4][kB / 32];
   __shared__ uint64_t dep_tab[256];
   const int l = lane_id();
@@ -1375,7 +1379,7 @@ __global__ __launch_bounds__(256) void expand_kernel(UnpackArgs a) {
   if (t >= a.ntiles) return;
   ExpandFetch f;
   expand_fetch(a, t, f);
-  expand_tile(a, t, f, lds_data[wv], lds_aux[wv], lds_ms[wv], dep_tab,
+  expand_tile(a, t, f, lds_data[wv], lds_aux[wv], dep_tab,
               deposit_sel((uint32_t)l & 15));
 }
 
