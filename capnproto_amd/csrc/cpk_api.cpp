@@ -682,6 +682,47 @@ cpk_status cpk_pack_chunks_host(cpk_ctx* ctx, const uint64_t* h_words, uint64_t 
   return CPK_OK;
 }
 
+cpk_status cpk_unpack_words_host(cpk_ctx* ctx, const uint8_t* h_packed, uint64_t avail_bytes,
+                                 uint64_t* h_words, uint64_t nwords, uint64_t* consumed_out) {
+  if (!ctx || (!h_packed && avail_bytes) || (!h_words && nwords) || !consumed_out)
+    return CPK_ERR_INVALID_ARGUMENT;
+  if (hipSetDevice(ctx->device) != hipSuccess) return CPK_ERR_HIP;
+  *consumed_out = 0;
+  if (nwords == 0) return CPK_OK;
+  if (avail_bytes == 0) return CPK_ERR_PREMATURE_EOF;
+  cpk_status st;
+  if ((st = ensure(&ctx->stage[0], &ctx->stage_size[0], nwords * 8 + 16)) != CPK_OK) return st;
+  if ((st = ensure(&ctx->stage[1], &ctx->stage_size[1], avail_bytes + 16)) != CPK_OK) return st;
+  if ((st = ensure(&ctx->stage[2], &ctx->stage_size[2], 64)) != CPK_OK) return st;
+  uint64_t* d_words = (uint64_t*)ctx->stage[0];
+  uint8_t* d_packed = (uint8_t*)ctx->stage[1];
+  uint64_t* d_in_off = (uint64_t*)ctx->stage[2];  // [2]
+  uint64_t* d_word_off = d_in_off + 2;            // [2]
+  uint64_t* d_in_end = d_word_off + 2;            // [1]
+  int32_t* d_status = (int32_t*)(d_in_end + 1);
+  const uint64_t offs[4] = {0, avail_bytes, 0, nwords};
+  hipStream_t s = nullptr;
+  if (hipMemcpyAsync(d_packed, h_packed, avail_bytes, hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipMemcpyAsync(d_in_off, offs, 32, hipMemcpyHostToDevice, s) != hipSuccess)
+    return CPK_ERR_HIP;
+  // one exact-size chunk (the flat-packed mode) with the end of its last record reported
+  st = unpack_common(ctx, 1, d_packed, avail_bytes, d_in_off, 1, d_word_off, d_words, nwords,
+                     nullptr, d_status, nullptr, 0, s, d_in_end);
+  if (st != CPK_OK) return st;
+  if ((st = cpk_sync(ctx, s)) != CPK_OK) return st;
+  uint64_t end = 0;
+  int32_t ms = 0;
+  if (hipMemcpy(&end, d_in_end, 8, hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemcpy(&ms, d_status, 4, hipMemcpyDeviceToHost) != hipSuccess)
+    return CPK_ERR_HIP;
+  if (ms == CPK_ERR_TRAILING_BYTES) ms = CPK_OK;  // the rest of the buffer is not ours
+  if (ms != CPK_OK) return (cpk_status)ms;
+  *consumed_out = end;
+  if (hipMemcpy(h_words, d_words, nwords * 8, hipMemcpyDeviceToHost) != hipSuccess)
+    return CPK_ERR_HIP;
+  return CPK_OK;
+}
+
 cpk_status cpk_unpacked_size_host(cpk_ctx* ctx, const uint8_t* h_packed, uint64_t nbytes,
                                   uint64_t* words_out) {
   if (!ctx || (!h_packed && nbytes) || !words_out) return CPK_ERR_INVALID_ARGUMENT;

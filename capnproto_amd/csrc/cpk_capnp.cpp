@@ -225,6 +225,61 @@ void writePackedMessageToFd(int fd, ArrayPtr<const ArrayPtr<const word>> segment
 }
 
 // ---- unpack ----------------------------------------------------------------------------------
+size_t _::PackedInputStream::tryRead(void* buffer, size_t minBytes, size_t maxBytes) {
+  // serialize-packed.c++:34-51
+  if (maxBytes == 0) return 0;
+  if (minBytes % 8 != 0 || maxBytes % 8 != 0)
+    fail(CPK_ERR_INVALID_ARGUMENT, "PackedInputStream reads must be word-aligned.");
+  if (minBytes > maxBytes) minBytes = maxBytes;
+  cpk_ctx* ctx = threadContext();
+  uint64_t* dst = static_cast<uint64_t*>(buffer);
+  std::vector<byte> acc;  // bytes already taken from the stream (the read spans buffers)
+  for (;;) {
+    ArrayPtr<const byte> buf = inner_.tryGetReadBuffer();
+    if (acc.empty() && buf.size() == 0) return 0;  // :48-51: nothing at all to read
+    const byte* data = buf.begin();
+    size_t avail = buf.size();
+    if (!acc.empty()) {
+      acc.insert(acc.end(), buf.begin(), buf.end());
+      data = acc.data();
+      avail = acc.size();
+    }
+    const size_t before = acc.empty() ? 0 : acc.size() - buf.size();
+    uint64_t used = 0;
+    cpk_status st = cpk_unpack_words_host(ctx, data, avail, dst, maxBytes / 8, &used);
+    if (st == CPK_ERR_PREMATURE_EOF && buf.size() > 0) {
+      // the records continue past what is buffered: take these bytes and refill
+      if (acc.empty()) acc.assign(buf.begin(), buf.end());
+      inner_.skip(buf.size());
+      continue;
+    }
+    if (st == CPK_ERR_PREMATURE_EOF) {
+      // the input has ended: what it holds is enough if it ends at a record boundary with at
+      // least minBytes of output (:65-80, the early return once out >= outMin)
+      uint64_t have = 0;
+      if (cpk_unpacked_size_host(ctx, data, avail, &have) == CPK_OK && have * 8 >= minBytes &&
+          have * 8 < maxBytes) {
+        check(cpk_unpack_words_host(ctx, data, avail, dst, have, &used), "PackedInputStream");
+        inner_.skip(used - before);
+        return have * 8;
+      }
+      fail(CPK_ERR_PREMATURE_EOF, "PackedInputStream");
+    }
+    check(st, "PackedInputStream");
+    inner_.skip(used - before);
+    return maxBytes;
+  }
+}
+
+void _::PackedInputStream::skip(size_t bytes) {
+  // serialize-packed.c++:185-299: the same parse without a destination -- decoded into scratch
+  // in one piece, since a run may not cross `bytes` but may cross any smaller piece
+  if (bytes == 0) return;
+  if (bytes % 8 != 0) fail(CPK_ERR_INVALID_ARGUMENT, "PackedInputStream reads must be word-aligned.");
+  std::vector<uint64_t> scratch(bytes / 8);
+  if (tryRead(scratch.data(), bytes, bytes) < bytes) fail(CPK_ERR_PREMATURE_EOF, "PackedInputStream");
+}
+
 PackedMessageReader::PackedMessageReader(BufferedInputStream& in, ReaderOptions options,
                                          ArrayPtr<word> scratch)
     : options_(options) {

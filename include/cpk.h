@@ -192,6 +192,13 @@ cpk_status cpk_read_packed_message_host(cpk_ctx* ctx, const uint8_t* h_packed,
 cpk_status cpk_pack_chunks_host(cpk_ctx* ctx, const uint64_t* h_words, uint64_t total_words,
                                 const uint64_t* h_chunk_word_off, uint64_t nchunks, uint8_t* h_out,
                                 uint64_t out_capacity, uint64_t* h_chunk_out_off);
+/* PackedInputStream::tryRead at a record boundary (serialize-packed.c++:34-183): decodes exactly
+ * nwords words from the front of a host buffer into h_words and returns the packed bytes they
+ * used in *consumed_out.  CPK_ERR_PREMATURE_EOF when the buffer ends first (a stream caller
+ * reads more and retries); CPK_ERR_RUN_OVERSHOOT when a run crosses the nwords boundary ("Packed
+ * input did not end cleanly on a segment boundary."). */
+cpk_status cpk_unpack_words_host(cpk_ctx* ctx, const uint8_t* h_packed, uint64_t avail_bytes,
+                                 uint64_t* h_words, uint64_t nwords, uint64_t* consumed_out);
 /* computeUnpackedSizeInWords (serialize-packed.c++:482-508) of one host buffer. */
 cpk_status cpk_unpacked_size_host(cpk_ctx* ctx, const uint8_t* h_packed, uint64_t nbytes,
                                   uint64_t* words_out);

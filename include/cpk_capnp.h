@@ -187,6 +187,25 @@ class PackedOutputStream : public OutputStream {
   BufferedOutputStream& inner_;
 };
 
+// serialize-packed.h:37-47 (serialize-packed.c++:34-299).  Decodes packed input from `inner`
+// on the device, a whole number of records per call: tryRead fills up to maxBytes (whole words),
+// returning early only when the input ends at a record boundary with at least minBytes out;
+// "Premature end of packed input." when it ends before minBytes or inside a record; "Packed
+// input did not end cleanly on a segment boundary." when a run crosses maxBytes.  skip(bytes)
+// consumes exactly `bytes` unpacked bytes with the same checks.
+class PackedInputStream : public InputStream {
+ public:
+  explicit PackedInputStream(BufferedInputStream& inner) : inner_(inner) {}
+  size_t tryRead(void* buffer, size_t minBytes, size_t maxBytes) override;
+  size_t tryRead(ArrayPtr<byte> dst, size_t minBytes) {  // the newer kj signature
+    return tryRead(dst.begin(), minBytes, dst.size());
+  }
+  void skip(size_t bytes) override;
+
+ private:
+  BufferedInputStream& inner_;
+};
+
 }  // namespace _
 
 // serialize-packed.h:65-71 / serialize.h InputStreamMessageReader: reads one packed message

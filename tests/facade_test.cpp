@@ -77,6 +77,19 @@ static void kat_chunks(const std::string& dir) {
     _::PackedOutputStream pk(out);
     pk.write(unpacked.data(), unpacked.size());
     CHECK(same(out.getArray(), packed), "KAT %d pack", n);
+    if (!unpacked.empty()) {
+      // serialize-packed-test.c++:85-101: and back through PackedInputStream
+      ArrayInputStream ain(ArrayPtr<const byte>(packed.data(), packed.size()));
+      _::PackedInputStream pin(ain);
+      std::vector<byte> back(unpacked.size());
+      pin.InputStream::read(back.data(), back.size());
+      CHECK(back == unpacked, "KAT %d PackedInputStream::read", n);
+      CHECK(ain.tryGetReadBuffer().size() == 0, "KAT %d read consumed the input", n);
+      ArrayInputStream ain2(ArrayPtr<const byte>(packed.data(), packed.size()));
+      _::PackedInputStream pin2(ain2);
+      pin2.skip(unpacked.size());
+      CHECK(ain2.tryGetReadBuffer().size() == 0, "KAT %d PackedInputStream::skip", n);
+    }
     n++;
   }
   CHECK(n >= 10, "KATs read: %d", n);
@@ -231,6 +244,53 @@ static void errors(const std::string& dir) {
   }
 }
 
+// _::PackedInputStream on its own (serialize-packed.c++:34-299): reads split at record
+// boundaries, refills across small buffers, and its exceptions.
+static void input_stream(const std::string& dir) {
+  std::vector<byte> msg = read_file(dir + "/binary"), packed = read_file(dir + "/packed");
+  {  // two reads split at a word boundary the records respect: the segment table, then the rest
+    ArrayInputStream ain(ArrayPtr<const byte>(packed.data(), packed.size()));
+    _::PackedInputStream pin(ain);
+    std::vector<byte> back(msg.size());
+    pin.InputStream::read(back.data(), 8);
+    pin.InputStream::read(back.data() + 8, back.size() - 8);
+    CHECK(back == msg, "PackedInputStream: table, then segments");
+    CHECK(ain.tryGetReadBuffer().size() == 0, "PackedInputStream: input consumed");
+  }
+  int fds[2];
+  if (pipe(fds) == 0) {  // 7-byte stream buffers: every read spans refills
+    if (write(fds[1], packed.data(), packed.size()) != (ssize_t)packed.size()) g_fail++;
+    close(fds[1]);
+    FdBufferedInputStream fin(fds[0], 7);
+    _::PackedInputStream pin(fin);
+    std::vector<byte> back(msg.size());
+    pin.InputStream::read(back.data(), back.size());
+    CHECK(back == msg, "PackedInputStream over 7-byte buffers");
+    close(fds[0]);
+  }
+  auto expect = [](const char* hexin, size_t minB, size_t maxB, cpk_status want, size_t got_bytes,
+                   const char* what) {
+    std::vector<byte> in = hex(hexin);
+    ArrayInputStream ain(ArrayPtr<const byte>(in.data(), in.size()));
+    _::PackedInputStream pin(ain);
+    std::vector<word> out(maxB / 8 + 1);
+    cpk_status st = CPK_OK;
+    size_t n = 0;
+    try {
+      n = pin.tryRead(out.data(), minB, maxB);
+    } catch (const Exception& e) {
+      st = e.status();
+    }
+    CHECK(st == want && (st != CPK_OK || n == got_bytes), "%s: status %d bytes %zu", what,
+          (int)st, n);
+  };
+  expect("", 8, 8, CPK_OK, 0, "empty input reads nothing");
+  expect("0001", 8, 8, CPK_ERR_RUN_OVERSHOOT, 0, "zero run crossing the read");
+  expect("ff0102", 8, 8, CPK_ERR_PREMATURE_EOF, 0, "truncated record");
+  expect("0000", 8, 16, CPK_OK, 8, "input ends at a record boundary past minBytes");
+  expect("0000", 16, 16, CPK_ERR_PREMATURE_EOF, 0, "input ends before minBytes");
+}
+
 int main(int argc, char** argv) {
   const std::string dir = argc > 1 ? argv[1] : "tests/golden";
   try {
@@ -239,6 +299,7 @@ int main(int argc, char** argv) {
     fixtures(dir, "segmented", "segmented-packed");
     two_messages(dir);
     errors(dir);
+    input_stream(dir);
   } catch (const Exception& e) {
     fprintf(stderr, "unexpected exception: %s\n", e.what());
     return 2;
