@@ -9,20 +9,36 @@ buffers.  value = unpacked bytes of all ranks / wall time of one step (max over 
     python bench.py [--config c2|c3|c4|c5] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N        (independent shards, weak scaling)
 
-Extra JSON objects: "roofline" (dominant kernel, timed live with HIP events on its stream) and
-"cpu_baseline" (the reference CPU codec -- oracle/_ref, compiled from the reference's sources --
-timed on a bounded sample of the same workload on this host, 1 thread, rank 0 at N=1 only).
+The headline line is the --config workload (C2 by default).  At N=1 the default run also
+measures C3 and C4 (``sub_results``, each with its own roofline), so one driver run covers the
+4 KiB - 64 MiB range.  Every measured batch is checked after timing: exact device round trip,
+and -- where tests/golden/manifest.json pins the workload -- SHA-256 of the packed bytes equal to
+the reference codec's.  A mismatch (or a diagnostic build knob in the environment) prints no
+``value`` and exits non-zero.
+
+Extra JSON objects:
+  roofline      headline: the round trip, 2(U+P) algorithmic bytes per step / wall time of a
+                step, against the 8 TB/s HBM peak; plus the read-only fraction
+                (U+P)/t, a D2D copy measured in the same run, and the dominant kernel alone
+                (HIP events on the stream the kernels run on).
+  cpu_baseline  the reference CPU codec (oracle/_ref, compiled from the reference's sources) on
+                this host, 1 thread and all the host cores this job has, on a bounded sample of
+                the same workload (rank 0 at N=1 only).
 """
 from __future__ import annotations
 
 import argparse
+import glob
+import hashlib
 import json
 import os
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+METRIC = "packed encode+decode GiB/s (device-resident), 4 KiB-64 MiB msg batch"
 
 # SURVEY.md 8(d) configurations.  seg_words=0: per-message size 2^k words, k uniform in [3, 11].
 CONFIGS = {
@@ -35,6 +51,7 @@ CONFIGS = {
     "c5": dict(nmsgs=(32 << 20) // 8, nseg=1, seg_words=0, profile="mixed", shard="round_robin",
                workload="C5: 32 Mi mixed-size messages (64 B-16 KiB), round-robin, 4 Mi per GPU"),
 }
+DEBUG_ENV = ("CPK_DEBUG_SKIP", "CPK_STAMPS")
 
 
 def parse():
@@ -43,18 +60,61 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--sub", default=None,
+                    help="comma-separated extra configs measured after the headline "
+                         "(default at N=1: c3,c4; 'none' to skip)")
+    ap.add_argument("--sub-steps", type=int, default=5)
+    ap.add_argument("--shard", default=None, choices=["block", "round_robin", "bytes"],
+                    help="message assignment to ranks (default: the config's)")
     ap.add_argument("--seed", type=int, default=20261015)
-    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+    ap.add_argument("--cpu-seconds", type=float, default=8.0,
                     help="CPU-baseline budget (bounded sample of the same workload)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-verify", action="store_true",
+                    help="skip the manifest hash check (the device round trip is still checked)")
     ap.add_argument("--host-inclusive", action="store_true",
                     help="also time the H2D/D2H-inclusive path (reported on stderr)")
     return ap.parse_args()
 
 
-def cpu_baseline(words_np, off_np, seconds):
+def kernel_source_hash() -> str:
+    """Content hash of the device code (pins a committed PMC traffic file to these kernels)."""
+    h = hashlib.sha256()
+    for p in sorted(glob.glob(os.path.join(ROOT, "capnproto_amd", "csrc", "*.hip")) +
+                    glob.glob(os.path.join(ROOT, "capnproto_amd", "csrc", "*.h"))):
+        h.update(os.path.basename(p).encode())
+        h.update(open(p, "rb").read())
+    return h.hexdigest()
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def host_threads() -> int:
+    """Host cores this job may use: the box's CPU share (OMP_NUM_THREADS is set to it there),
+    capped by what the machine reports."""
+    n = os.cpu_count() or 1
+    e = os.environ.get("OMP_NUM_THREADS")
+    if e and e.isdigit() and int(e) > 0:
+        n = min(n, int(e))
+    return n
+
+
+def cpu_baseline(sample_words, sample_off, seconds, threads):
     """The reference codec (oracle/_ref: capnproto serialize-packed.c++ compiled from its own
-    sources) or, if that build is absent, the C restatement -- on a bounded sample."""
+    sources) or, if that build is absent, the C restatement -- pack (ArrayOutputStream shape)
+    then unpack (ArrayInputStream + PackedMessageReader shape) of a bounded sample, first on one
+    thread, then on `threads` threads each owning a disjoint slice.  ctypes drops the GIL for
+    the duration of each foreign call, so the threads run the codec in parallel."""
+    import ctypes as C
+
     import numpy as np
 
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -62,70 +122,167 @@ def cpu_baseline(words_np, off_np, seconds):
 
     try:
         impl, kind = P.Reference(), "reference"
-        pack = lambda: impl.pack_batch(words_np, off_np)  # noqa: E731
     except OSError:
         impl, kind = P.Oracle(), "port"
-        pack = lambda: impl.pack_batch(words_np, off_np)[:2]  # noqa: E731
-    packed, poff = pack()
-    packed = np.ascontiguousarray(packed)
-    cap = len(words_np)
+    u8p, u64p, i32p = C.POINTER(C.c_uint8), C.POINTER(C.c_uint64), C.POINTER(C.c_int32)
 
-    def unpack():
-        return impl.unpack_batch(packed, poff, cap)
+    class Job:
+        def __init__(self, words, off):
+            self.words = np.ascontiguousarray(words, dtype="<u8")
+            self.off = np.ascontiguousarray(off - off[0], dtype="<u8")
+            self.n = len(off) - 1
+            self.cap = P.packed_bound(len(self.words), 2 * self.n + 2)
+            self.out = np.zeros(self.cap, np.uint8)
+            self.poff = np.zeros(self.n + 1, "<u8")
+            self.back = np.zeros(max(1, len(self.words)), "<u8")
+            self.woff = np.zeros(self.n + 1, "<u8")
+            self.st = np.zeros(max(1, self.n), np.int32)
+            self.tp = self.tu = 0.0
+            self.reps = 0
 
-    U = words_np.nbytes
-    tp = tu = 0.0
-    reps = 0
-    t_end = time.perf_counter() + seconds
-    while time.perf_counter() < t_end or reps == 0:
-        t0 = time.perf_counter()
-        pack()
-        t1 = time.perf_counter()
-        unpack()
-        t2 = time.perf_counter()
-        tp += t1 - t0
-        tu += t2 - t1
-        reps += 1
+        def pack(self):
+            if kind == "reference":
+                impl.lib.ref_pack_batch(self.words.ctypes.data_as(u64p),
+                                        self.off.ctypes.data_as(u64p), self.n,
+                                        self.out.ctypes.data_as(u8p), self.cap,
+                                        self.poff.ctypes.data_as(u64p))
+            else:
+                impl.lib.cpko_pack_batch(self.words.ctypes.data_as(u64p),
+                                         self.off.ctypes.data_as(u64p), self.n,
+                                         self.out.ctypes.data_as(u8p),
+                                         self.poff.ctypes.data_as(u64p),
+                                         self.st.ctypes.data_as(i32p))
+
+        def unpack(self):
+            if kind == "reference":
+                impl.lib.ref_unpack_batch(self.out.ctypes.data_as(u8p),
+                                          self.poff.ctypes.data_as(u64p), self.n,
+                                          self.back.ctypes.data_as(u64p), len(self.back),
+                                          self.woff.ctypes.data_as(u64p))
+            else:
+                impl.lib.cpko_unpack_batch(self.out.ctypes.data_as(u8p),
+                                           self.poff.ctypes.data_as(u64p), self.n,
+                                           self.back.ctypes.data_as(u64p), len(self.back),
+                                           self.woff.ctypes.data_as(u64p),
+                                           self.st.ctypes.data_as(i32p), 8 << 20)
+
+        def run(self, t_end):
+            while time.perf_counter() < t_end or self.reps == 0:
+                t0 = time.perf_counter()
+                self.pack()
+                t1 = time.perf_counter()
+                self.unpack()
+                t2 = time.perf_counter()
+                self.tp += t1 - t0
+                self.tu += t2 - t1
+                self.reps += 1
+
+    # one thread on the first slice; then `threads` threads on slices of the whole sample
+    nm = len(sample_off) - 1
+    per = max(1, nm // threads)
+    slices = [(i * per, min(nm, (i + 1) * per)) for i in range(threads) if i * per < nm]
+    jobs = [Job(sample_words[int(sample_off[a]):int(sample_off[b])], sample_off[a:b + 1])
+            for a, b in slices]
+    jobs[0].pack()
+    ref_packed = jobs[0].out[: int(jobs[0].poff[-1])].copy()
+    one = jobs[0]
+    one.run(time.perf_counter() + seconds / 2)
+    U1 = one.words.nbytes
+    single = {"value": U1 * one.reps / (one.tp + one.tu) / 2**30,
+              "pack_GiBps": U1 * one.reps / one.tp / 2**30,
+              "unpack_GiBps": U1 * one.reps / one.tu / 2**30, "cores": 1,
+              "sample": f"{one.n} messages ({U1 / 2**20:.1f} MiB) x {one.reps} passes"}
+    for j in jobs:
+        j.tp = j.tu = 0.0
+        j.reps = 0
+    t_end = time.perf_counter() + seconds / 2
+    w0 = time.perf_counter()
+    th = [threading.Thread(target=j.run, args=(t_end,)) for j in jobs]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    wall = time.perf_counter() - w0
+    Ub = sum(j.words.nbytes * j.reps for j in jobs)
+    multi = Ub / wall / 2**30
     return {
-        "value": U * reps / (tp + tu) / 2**30,
+        "value": round(multi, 3),
         "unit": "GiB/s",
-        "cores": 1,
+        "cores": len(jobs),
         "kind": kind,
-        "sample": f"{len(off_np) - 1} messages ({U / 2**20:.1f} MiB unpacked, "
-                  f"{len(packed) / 2**20:.2f} MiB packed) x {reps} pack+unpack passes, 1 thread",
-        "pack_GiBps": U * reps / tp / 2**30,
-        "unpack_GiBps": U * reps / tu / 2**30,
-    }, packed, poff
+        "sample": f"{nm} messages of the workload ({sample_words.nbytes / 2**20:.1f} MiB), "
+                  f"{len(jobs)} threads each packing then unpacking its own slice for "
+                  f"{seconds / 2:.0f} s; single-thread pass on {one.n} messages",
+        "single_thread": {k: (round(v, 3) if isinstance(v, float) else v)
+                          for k, v in single.items()},
+        "nproc": os.cpu_count(),
+        "cpu_model": cpu_model(),
+    }, ref_packed, jobs[0].poff.copy(), one.n
 
 
-def main():
-    args = parse()
-    import numpy as np
+def measure_copy(torch, device, nbytes=1 << 30, reps=10):
+    """Device-to-device copy bandwidth in the same run (read + write bytes / time)."""
+    a = torch.empty(nbytes, dtype=torch.uint8, device=device)
+    b = torch.empty_like(a)
+    a.fill_(1)
+    b.copy_(a)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    del a, b
+    torch.cuda.empty_cache()
+    return 2 * nbytes / (ms * 1e-3) / 1e9
+
+
+def sha_dev(t, chunk=1 << 28):
     import torch
 
-    import capnproto_amd
-    from capnproto_amd.shard import reduce_step, shard_messages
+    b = t.view(torch.uint8) if t.dtype != torch.uint8 else t
+    h = hashlib.sha256()
+    for i in range(0, b.numel(), chunk):
+        h.update(memoryview(b[i : i + chunk].cpu().numpy()))
+    return h.hexdigest()
 
-    rank = int(os.environ.get("RANK", 0))
-    world = int(os.environ.get("WORLD_SIZE", 1))
-    local = int(os.environ.get("LOCAL_RANK", 0))
-    if world != args.gpus and rank == 0:
-        print(f"note: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
-    torch.cuda.set_device(local)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+def manifest_entry(name, cfg, seed, first, stride, n):
+    p = os.path.join(ROOT, "tests", "golden", "manifest.json")
+    if not os.path.exists(p):
+        return None
+    man = json.load(open(p)).get("configs", {})
+    for c in man.values():
+        if (c["seed"], c["first_msg"], c["msg_stride"], c["nmsgs"], c["profile"], c["nseg"],
+                c["seg_words"]) == (seed, first, stride, n, cfg["profile"], cfg["nseg"],
+                                    cfg["seg_words"]):
+            return c
+    return None
+
+
+def run_config(name, args, steps, warmup, rank, world, dist, codec):
+    import torch
+
+    from capnproto_amd.shard import balanced_ranges, reduce_step, shard_messages
+
+    cfg = CONFIGS[name]
 
     def barrier():
         if dist is not None:
             dist.barrier()
 
-    cfg = CONFIGS[args.config]
-    codec = capnproto_amd.Codec(local)
-    # Independent message shards (weak scaling: nmsgs per GPU): capnproto_amd/shard.py.
-    first, stride, n = shard_messages(rank, world, cfg["nmsgs"] * world, cfg.get("shard", "block"))
+    mode = args.shard or cfg.get("shard", "block")
+    n_global = cfg["nmsgs"] * world
+    if mode == "bytes":
+        goff, _ = codec.gen_offsets(n_global, nseg=cfg["nseg"], seg_words=cfg["seg_words"],
+                                    seed=args.seed)
+        first, n = balanced_ranges(goff, world)[rank]
+        stride = 1
+        del goff
+    else:
+        first, stride, n = shard_messages(rank, world, n_global, mode)
     off, total = codec.gen_offsets(n, nseg=cfg["nseg"], seg_words=cfg["seg_words"],
                                    seed=args.seed, first_msg=first, msg_stride=stride)
     words = codec.gen_messages(cfg["profile"], off, total, nseg=cfg["nseg"], seed=args.seed,
@@ -150,13 +307,13 @@ def main():
         codec.unpack_messages(packed, moff, total, nbytes=P, words=back, msg_word_off=woff,
                               status=ust)
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
     codec.sync()
     torch.cuda.synchronize()
     barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         step()
     torch.cuda.synchronize()
     barrier()
@@ -164,15 +321,21 @@ def main():
     codec.sync()
     dt = t1 - t0
 
-    # correctness of what was timed: exact round trip + statuses
+    # correctness of what was timed: exact round trip + statuses, then the reference's hashes
     ok = bool((pst == 0).all().item() and (ust == 0).all().item() and torch.equal(woff, off)
-              and torch.equal(back, words[:total]))
+              and torch.equal(back[:total], words[:total]))
+    man = None if args.no_verify else manifest_entry(name, cfg, args.seed, first, stride, n)
+    ref_ok = None
+    if man is not None:
+        ref_ok = (man["packed_bytes"] == P and sha_dev(packed[:P]) == man["sha256_packed"]
+                  and sha_dev(moff) == man["sha256_out_off"])
+        ok = ok and ref_ok
 
     # per-kernel durations: a second pass of the same steps with HIP events around every tile
     # kernel, on the stream the kernels run on (kept out of the wall-clock pass above)
     codec.timing_read_all()  # discard
     codec.timing(True)
-    for _ in range(args.steps):
+    for _ in range(steps):
         step()
     codec.timing(False)
     codec.sync()
@@ -181,94 +344,174 @@ def main():
 
     red = reduce_step(dt, float(U), float(P), kms["pack"], kms["unpack"], ok,
                       dist=dist, device=codec.device)
-    dt_max, U_all = red["dt_max"], red["unpacked_all"]
-    ok_all = red["ok_all"]
+    res = {"name": name, "cfg": cfg, "n": n, "U": U, "P": P, "first": first, "stride": stride,
+           "mode": mode, "dt_max": red["dt_max"], "U_all": red["unpacked_all"],
+           "ok_all": red["ok_all"], "ref_checked": man is not None, "ref_ok": ref_ok,
+           "kms": kms, "steps": steps, "warmup": warmup}
+    res["tensors"] = (words, off, packed, moff, total, cap)
+    return res
 
-    result = None
-    if rank == 0:
-        ms_per_step = dt_max / args.steps * 1e3
-        value = U_all / (dt_max / args.steps) / 2**30
-        # algorithmic HBM bytes of one launch of each tile kernel
+
+def summarize(res, world, copy_gbps):
+    """Per-config JSON: value, roofline (headline = round trip), dominant kernel."""
+    U, P, steps = res["U"], res["P"], res["steps"]
+    kms = res["kms"]
+    t_step = res["dt_max"] / steps  # seconds, max over ranks
+    value = res["U_all"] / t_step / 2**30
+    # per-GPU algorithmic bytes of one round trip: pack (read U, write P) + unpack (read P,
+    # write U); SURVEY.md 8(d)
+    rt = 2.0 * (U + P) / t_step / 1e9
+    rd = (U + P) / t_step / 1e9
+    algo = {"pack": U + P, "unpack_index": P, "unpack_expand": U + P}
+    if kms.get("pack_count", 0) > 0:  # two-pass pack (A/B knob)
         algo = {"pack_count": U, "pack_emit": U + P, "unpack_index": P, "unpack_expand": U + P}
-        if kms["pack_count"] == 0:  # single-pass pack kernel (CPK_PACK_FUSED=1)
-            algo = {"pack": U + P, "unpack_index": P, "unpack_expand": U + P}
-        kern = {k: {"ms": round(kms[k], 4),
-                    "GBps": round(algo[k] / (kms[k] * 1e-3) / 1e9, 1) if kms[k] > 0 else None,
-                    "algorithmic_bytes": int(algo[k])} for k in algo}
-        for k in ("pack", "unpack_resolve", "unpack_fallback"):
-            kern.setdefault(k, {"ms": round(kms[k], 4)})
-        dom = max(algo, key=lambda k: kms[k])
-        dom_ms = kms[dom]
-        achieved = algo[dom] / (dom_ms * 1e-3) / 1e9
-        rt_ms = kms["pack"] + kms["unpack"]
-        rt = 2.0 * (U + P) / (rt_ms * 1e-3) / 1e9
-        traffic = None
-        tf = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
-        if os.path.exists(tf):
-            try:
-                t = json.load(open(tf)).get(dom)
-                traffic = int(t["bytes"]) if isinstance(t, dict) else t
-            except Exception:
-                traffic = None
+    kern = {k: {"ms": round(kms[k], 4),
+                "GBps": round(algo[k] / (kms[k] * 1e-3) / 1e9, 1) if kms[k] > 0 else None,
+                "algorithmic_bytes": int(algo[k])} for k in algo}
+    for k in ("unpack_resolve", "unpack_fallback"):
+        kern.setdefault(k, {"ms": round(kms[k], 4)})
+    dom = max(algo, key=lambda k: kms[k])
+    dom_ach = algo[dom] / (kms[dom] * 1e-3) / 1e9 if kms[dom] > 0 else 0.0
+    traffic = None
+    tf = os.path.join(ROOT, "profiles", f"traffic_{res['name']}.json")
+    if os.path.exists(tf):
+        try:
+            t = json.load(open(tf))
+            if t.get("kernel_src_sha256") == kernel_source_hash():
+                traffic = {k: v for k, v in t.items() if k != "kernel_src_sha256"}
+        except Exception:
+            traffic = None
+    cfg = res["cfg"]
+    return {
+        "value": round(value, 3),
+        "ms_per_step": round(t_step * 1e3, 4),
+        "config": {
+            "workload": cfg["workload"],
+            "messages_per_gpu": res["n"],
+            "unpacked_bytes_per_gpu": U,
+            "packed_bytes_per_gpu": P,
+            "packed_ratio": round(P / U, 4),
+            "profile": cfg["profile"],
+            "shard": res["mode"],
+            "parallelism": f"dp{world} (independent message shards, no data-path collective)",
+        },
+        "parity": ("bit-exact round trip; packed bytes SHA-256 == reference "
+                   "(tests/golden/manifest.json)" if res["ref_checked"] else
+                   "bit-exact round trip (no reference manifest for this shard)"),
+        "roofline": {
+            "bound": "hbm",
+            "what": "round trip: 2(U+P) algorithmic bytes per GPU per step / wall time of a step",
+            "achieved": round(rt, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(rt / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "read_only_frac": round(rd / HBM_PEAK_GBS, 4),
+            "measured_copy_GBps": round(copy_gbps, 1) if copy_gbps else None,
+            "frac_of_measured_copy": round(rt / copy_gbps, 4) if copy_gbps else None,
+            "dominant_kernel": {
+                "kernel": dom,
+                "achieved": round(dom_ach, 1),
+                "frac": round(dom_ach / HBM_PEAK_GBS, 4),
+                "algorithmic_bytes_per_launch": int(algo[dom]),
+            },
+            "kernels": kern,
+            "pack_ms": round(kms["pack"], 4),
+            "unpack_ms": round(kms["unpack"], 4),
+        },
+    }
+
+
+def main():
+    args = parse()
+    bad = [e for e in DEBUG_ENV if os.environ.get(e, "0") not in ("", "0")]
+    if bad:
+        print(json.dumps({"error": f"diagnostic knob(s) set: {bad}; refusing to report a value"}))
+        sys.exit(2)
+    import numpy as np
+    import torch
+
+    import capnproto_amd
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    if world != args.gpus and rank == 0:
+        print(f"note: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    codec = capnproto_amd.Codec(local)
+    copy_gbps = measure_copy(torch, codec.device)
+    head = run_config(args.config, args, args.steps, args.warmup, rank, world, dist, codec)
+    ok = head["ok_all"]
+
+    cb = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        words, off, packed, moff, total, cap = head["tensors"]
+        nt = host_threads()
+        per = max(1, (4 << 20) // max(1, head["U"] // head["n"]))  # ~4 MiB per thread
+        k = min(head["n"], per * nt)
+        o = off[: k + 1].cpu().numpy().astype(np.uint64)
+        ws = words[: int(o[-1])].cpu().numpy().view(np.uint64)
+        cb, ref_packed, ref_off, k1 = cpu_baseline(ws, o, args.cpu_seconds, nt)
+        # the CPU codec's packed bytes of its first slice must equal the device's bit for bit
+        gp = packed[: int(moff[k1].item())].cpu().numpy()
+        if gp.tobytes() != np.asarray(ref_packed).tobytes():
+            ok = False
+    hi = None
+    if args.host_inclusive and world == 1:
+        words, off, packed, moff, total, cap = head["tensors"]
+        hi = host_inclusive(codec, words, off, total, head["n"], cap, args.steps)
+    head.pop("tensors")
+    torch.cuda.empty_cache()
+
+    subs = []
+    sub = args.sub if args.sub is not None else ("c3,c4" if world == 1 else "none")
+    for nm in [s for s in sub.split(",") if s and s != "none" and s != args.config]:
+        r = run_config(nm, args, args.sub_steps, 2, rank, world, dist, codec)
+        r.pop("tensors")
+        torch.cuda.empty_cache()
+        ok = ok and r["ok_all"]
+        subs.append(r)
+
+    if rank == 0:
+        if not ok:
+            print(json.dumps({"metric": METRIC, "error": "parity MISMATCH: no value reported",
+                              "config": args.config}))
+            sys.exit(1)
+        s = summarize(head, world, copy_gbps)
         result = {
-            "metric": "packed encode+decode GiB/s (device-resident), 4 KiB-64 MiB msg batch",
-            "value": round(value, 3),
+            "metric": METRIC,
+            "value": s["value"],
             "unit": "GiB/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 4),
+            "ms_per_step": s["ms_per_step"],
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (deterministic on-device generator, SURVEY.md 8(d))",
-            "config": {
-                "workload": cfg["workload"],
-                "messages_per_gpu": n,
-                "unpacked_bytes_per_gpu": U,
-                "packed_bytes_per_gpu": P,
-                "packed_ratio": round(P / U, 4),
-                "profile": cfg["profile"],
-                "parallelism": f"dp{world} (independent message shards, no data-path collective)",
-            },
-            "parity": "bit-exact round trip" if ok_all else "MISMATCH",
-            "roofline": {
-                "bound": "hbm",
-                "kernel": dom,
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "algorithmic_bytes_per_launch": int(algo[dom]),
-                "kernels": kern,
-                "pack_ms": round(kms["pack"], 4),
-                "unpack_ms": round(kms["unpack"], 4),
-                "roundtrip_GBps": round(rt, 1),
-                "roundtrip_frac": round(rt / HBM_PEAK_GBS, 4),
-            },
-            "cpu_baseline": None,
+            "config": s["config"],
+            "parity": s["parity"] + ("; CPU codec packed bytes == device on its sample"
+                                     if cb else ""),
+            "roofline": s["roofline"],
+            "cpu_baseline": cb,
         }
-
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        k = min(n, max(1, (4 << 20) // max(1, U // n)))  # ~4 MiB sample of the same workload
-        o = off[: k + 1].cpu().numpy().astype(np.uint64)
-        wsample = words[: int(o[-1])].cpu().numpy().view(np.uint64)
-        cb, ref_packed, ref_off = cpu_baseline(wsample, o, args.cpu_seconds)
-        result["cpu_baseline"] = cb
-        # packed bytes of the sample must equal the reference's bit for bit
-        gp = packed[: int(moff[k].item())].cpu().numpy()
-        if gp.tobytes() != np.asarray(ref_packed).tobytes():
-            result["parity"] = "MISMATCH vs reference packed bytes"
-        else:
-            result["parity"] += f"; packed bytes == {cb['kind']} CPU codec on the sample"
-
-    if args.host_inclusive and world == 1:
-        hi = host_inclusive(codec, words, off, total, n, cap, args.steps)
-        print(json.dumps({"host_inclusive": hi}), file=sys.stderr)
-
-    if rank == 0:
+        if subs:
+            result["sub_results"] = []
+            for r in subs:
+                sr = summarize(r, world, copy_gbps)
+                sr["steps"] = r["steps"]
+                result["sub_results"].append(sr)
+        if hi is not None:
+            result["host_inclusive"] = hi
         print(json.dumps(result))
     codec.close()
     if dist is not None:
@@ -276,7 +519,9 @@ def main():
 
 
 def host_inclusive(codec, words, off, total, n, cap, steps):
-    """U / (H2D(U) + pack + D2H(P) + H2D(P) + unpack + D2H(U)) with pinned host buffers."""
+    """U / (H2D(U) + pack + D2H(P) + H2D(P) + unpack + D2H(U)) with pinned host buffers: the
+    path starting and ending in host memory.  Serial: one stream, every copy waits for the
+    previous stage."""
     import torch
 
     hw = torch.empty(total, dtype=torch.int64, pin_memory=True)
@@ -302,8 +547,10 @@ def host_inclusive(codec, words, off, total, n, cap, steps):
         hb.copy_(back, non_blocking=True)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / steps
-    return {"GiBps": total * 8 / dt / 2**30, "ms_per_step": dt * 1e3,
-            "path": "pinned H2D(U) + pack + D2H(P) + H2D(P) + unpack + D2H(U)"}
+    ok = torch.equal(hb, hw)
+    return {"GiBps": round(total * 8 / dt / 2**30, 3), "ms_per_step": round(dt * 1e3, 3),
+            "round_trip_exact": bool(ok),
+            "path": "pinned H2D(U) + pack + D2H(P) + H2D(P) + unpack + D2H(U), one stream"}
 
 
 if __name__ == "__main__":

@@ -29,6 +29,43 @@ def shard_messages(rank: int, world: int, n_global: int, mode: str = "block"):
     raise ValueError(f"unknown shard mode {mode!r}")
 
 
+def balanced_ranges(msg_word_off, world: int):
+    """Byte-balanced contiguous partition: cut the message sequence where the
+    running unpacked size crosses r/world of the total, so every rank gets a contiguous range
+    of messages whose byte count is within one message of total/world (round-robin on mixed
+    sizes is only balanced on average).  msg_word_off: n+1 word offsets (numpy array or torch
+    tensor).  Returns [(first_msg, count)] per rank."""
+    import numpy as np
+
+    off = np.asarray(msg_word_off.cpu() if hasattr(msg_word_off, "cpu") else msg_word_off,
+                     dtype=np.int64)
+    n = len(off) - 1
+    total = int(off[-1])
+    cuts = [0]
+    for r in range(1, world):
+        target = (total * r) // world
+        # first message whose start is at or past the target share
+        cuts.append(max(cuts[-1], min(n, int(np.searchsorted(off[:n], target, side="left")))))
+    cuts.append(n)
+    return [(cuts[r], cuts[r + 1] - cuts[r]) for r in range(world)]
+
+
+def global_offsets(local_packed_total: int, dist=None, device=None):
+    """Global output placement of each rank's packed bytes in the batch case:
+    ONE all-gather of the per-rank packed totals (one u64 per rank); rank r's bytes go at the
+    sum of the totals of ranks < r.  Returns (base of this rank, global total)."""
+    import torch
+
+    t = torch.tensor([local_packed_total], dtype=torch.int64, device=device)
+    if dist is None:
+        return 0, int(local_packed_total)
+    parts = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, t)
+    vals = [int(p.item()) for p in parts]
+    r = dist.get_rank()
+    return sum(vals[:r]), sum(vals)
+
+
 def reduce_step(dt_s: float, unpacked: float, packed: float, pack_ms: float, unpack_ms: float,
                 ok: bool, dist=None, device=None):
     """Whole-job numbers of one measurement: time = max over ranks (the job ends when the

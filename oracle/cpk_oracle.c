@@ -286,3 +286,74 @@ uint64_t cpko_splitmix64(uint64_t x) {
   x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
   return x ^ (x >> 31);
 }
+
+/* Host restatement of the benchmark generator (capnproto_amd/csrc/cpk_gen.hip: gen_word,
+ * gen_kernel, gen_sizes_kernel) -- the synthetic workloads of SURVEY.md 8(d).  Test
+ * infrastructure: lets tests/ and tools/make_manifest.py rebuild any message of a bench config
+ * on the host, so the reference's packed bytes can be pinned for the full-size configs. */
+static uint64_t text_word(uint64_t h) {
+  uint64_t w = 0;
+  for (int b = 0; b < 8; b++) w |= (uint64_t)(0x20 + ((h >> (8 * b)) & 0xff) % 95) << (8 * b);
+  return w;
+}
+
+static uint64_t gen_word(int profile, uint64_t seed, uint64_t msg, uint64_t idx) {
+  const uint64_t mkey = cpko_splitmix64(seed ^ (msg * 0xD1B54A32D192ED03ull));
+  if (profile == 3) profile = (int)(mkey % 3);
+  const uint64_t h = cpko_splitmix64(mkey + idx * 0x9E3779B97F4A7C15ull);
+  if (profile == 2) return text_word(h);
+  if (profile == 1) {
+    const uint64_t blk = idx / 340, p = idx % 340;
+    const uint64_t nz = 4 + cpko_splitmix64(mkey ^ (blk * 0xA24BAED4963EE407ull)) % 73;
+    if (p >= nz) return 0;
+    if (h >> 63) return (h & 0xfc) | ((h >> 8) & 0xff) << 32 | ((h >> 16) & 0xffff) << 48;
+    return h & 0xffffff;
+  }
+  const uint32_t r = (uint32_t)((h >> 56) % 100);
+  if (r < 45) {
+    const int k = 1 + (int)((h >> 48) % 3);
+    return h & ((1ull << (8 * k)) - 1);
+  }
+  if (r < 65) return (h & 0xffff) | (((h >> 16) & 0xffff) << 32);
+  if (r < 80) return 0;
+  if (r < 90) return (h & 0xff) | ((h >> 8) & 0xff) << 32 | ((h >> 16) & 0xff) << 48;
+  return text_word(cpko_splitmix64(h));
+}
+
+void cpko_gen_offsets(uint64_t seed, uint64_t first_msg, uint64_t stride, uint64_t nmsgs,
+                      uint32_t nseg, uint64_t seg_words, uint64_t* off) {
+  const uint64_t tw = nseg / 2 + 1;
+  uint64_t o = 0;
+  if (stride == 0) stride = 1;
+  for (uint64_t m = 0; m < nmsgs; m++) {
+    off[m] = o;
+    if (seg_words) {
+      o += tw + (uint64_t)nseg * seg_words;
+    } else {
+      const uint64_t k =
+          3 + cpko_splitmix64(seed ^ ((first_msg + m * stride) * 0x94D049BB133111EBull)) % 9;
+      o += tw + (1ull << k);
+    }
+  }
+  off[nmsgs] = o;
+}
+
+void cpko_gen_messages(int profile, uint64_t seed, uint64_t first_msg, uint64_t stride,
+                       uint64_t nmsgs, uint32_t nseg, const uint64_t* off, uint64_t* words) {
+  const uint64_t tw = nseg / 2 + 1;
+  if (stride == 0) stride = 1;
+  for (uint64_t m = 0; m < nmsgs; m++) {
+    uint64_t* w = words + (off[m] - off[0]);
+    const uint64_t body = (off[m + 1] - off[m]) - tw;
+    const uint64_t seg = body / nseg;
+    uint32_t* t32 = (uint32_t*)w;
+    for (uint64_t i = 0; i < 2 * tw; i++) {
+      uint32_t v = 0;
+      if (i == 0) v = nseg - 1;
+      else if (i <= nseg) v = (uint32_t)(i < nseg ? seg : body - seg * (nseg - 1));
+      t32[i] = v;
+    }
+    const uint64_t g = first_msg + m * stride;
+    for (uint64_t i = 0; i < body; i++) w[tw + i] = gen_word(profile, seed, g, i);
+  }
+}

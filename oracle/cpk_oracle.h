@@ -66,6 +66,14 @@ int32_t cpko_unpack_batch(const uint8_t* packed, const uint64_t* msg_in_off, uin
  * SplitMix64 per (seed, message, word).  See SURVEY.md 8(d). */
 uint64_t cpko_splitmix64(uint64_t x);
 
+/* Host restatement of the benchmark generator (capnproto_amd/csrc/cpk_gen.hip), same arguments
+ * as cpk_gen_offsets / cpk_gen_messages (include/cpk.h).  off has nmsgs + 1 entries; words
+ * receives messages first_msg, first_msg + stride, ... with off[0] mapped to words[0]. */
+void cpko_gen_offsets(uint64_t seed, uint64_t first_msg, uint64_t stride, uint64_t nmsgs,
+                      uint32_t nseg, uint64_t seg_words, uint64_t* off);
+void cpko_gen_messages(int profile, uint64_t seed, uint64_t first_msg, uint64_t stride,
+                       uint64_t nmsgs, uint32_t nseg, const uint64_t* off, uint64_t* words);
+
 #ifdef __cplusplus
 }
 #endif

@@ -103,6 +103,30 @@ class Oracle:
                                         C.c_uint64]
         L.cpko_splitmix64.restype = C.c_uint64
         L.cpko_splitmix64.argtypes = [C.c_uint64]
+        L.cpko_gen_offsets.restype = None
+        L.cpko_gen_offsets.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64,
+                                       C.c_uint32, C.c_uint64, _u64p]
+        L.cpko_gen_messages.restype = None
+        L.cpko_gen_messages.argtypes = [C.c_int, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64,
+                                        C.c_uint32, _u64p, _u64p]
+
+    # -- host restatement of the bench generator (capnproto_amd/csrc/cpk_gen.hip)
+    PROFILES = {"flat": 0, "pointer": 1, "text": 2, "mixed": 3}
+
+    def gen_offsets(self, nmsgs, nseg=1, seg_words=0, seed=0, first_msg=0, msg_stride=1):
+        off = np.zeros(nmsgs + 1, "<u8")
+        self.lib.cpko_gen_offsets(seed, first_msg, msg_stride, nmsgs, nseg, seg_words,
+                                  _ptr(off, _u64p))
+        return off
+
+    def gen_messages(self, profile, off, nseg=1, seed=0, first_msg=0, msg_stride=1):
+        """Messages first_msg + i * msg_stride for i < len(off) - 1 (off may start anywhere)."""
+        off = np.ascontiguousarray(off, dtype="<u8")
+        words = np.zeros(max(1, int(off[-1] - off[0])), "<u8")
+        self.lib.cpko_gen_messages(self.PROFILES.get(profile, profile), seed, first_msg,
+                                   msg_stride, len(off) - 1, nseg, _ptr(off, _u64p),
+                                   _ptr(words, _u64p))
+        return words[: int(off[-1] - off[0])]
 
     # -- a1: PackedOutputStream::write(one piece)
     def pack_chunk(self, words) -> bytes:

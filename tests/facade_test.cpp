@@ -291,6 +291,35 @@ static void input_stream(const std::string& dir) {
   expect("0000", 16, 16, CPK_ERR_PREMATURE_EOF, 0, "input ends before minBytes");
 }
 
+// Config C1: samples/addressbook.c++ -- writeAddressBook packs with writePackedMessageToFd
+// (:75), printAddressBook reads with PackedFdMessageReader (:79).  tests/golden/addressbook.bin
+// is the sample's message, addressbook.packed the reference's bytes for it.
+static void addressbook(const std::string& dir) {
+  std::vector<byte> msg = read_file(dir + "/addressbook.bin");
+  std::vector<byte> ref = read_file(dir + "/addressbook.packed");
+  CHECK(msg.size() == 288 && ref.size() == 151, "addressbook fixtures present");
+  if (msg.size() != 288) return;
+  auto segs = segments_of(msg);
+  int fds[2];
+  if (pipe(fds) != 0) return;
+  writePackedMessageToFd(fds[1], ArrayPtr<const ArrayPtr<const word>>(segs.data(), segs.size()));
+  std::vector<byte> got(ref.size() + 16);
+  const ssize_t n = read(fds[0], got.data(), got.size());
+  got.resize(n > 0 ? (size_t)n : 0);
+  CHECK(got == ref, "addressbook: writePackedMessageToFd bytes == reference (%zd B)", n);
+  // the reader side of the sample: the same bytes back through a pipe
+  writePackedMessageToFd(fds[1], ArrayPtr<const ArrayPtr<const word>>(segs.data(), segs.size()));
+  close(fds[1]);
+  {
+    PackedFdMessageReader reader(fds[0]);
+    CHECK(reader.segmentCount() == 1, "addressbook: one segment");
+    auto s0 = reader.getSegment(0);
+    CHECK(s0.size() == segs[0].size() && memcmp(s0.begin(), segs[0].begin(), s0.size() * 8) == 0,
+          "addressbook: PackedFdMessageReader segment 0");
+  }
+  close(fds[0]);
+}
+
 int main(int argc, char** argv) {
   const std::string dir = argc > 1 ? argv[1] : "tests/golden";
   try {
@@ -300,6 +329,7 @@ int main(int argc, char** argv) {
     two_messages(dir);
     errors(dir);
     input_stream(dir);
+    addressbook(dir);
   } catch (const Exception& e) {
     fprintf(stderr, "unexpected exception: %s\n", e.what());
     return 2;

@@ -147,3 +147,39 @@ def test_batch_vs_reference(oracle):
     segs = [np.concatenate(P.split_flat(words[off[i]:off[i + 1]]) or [np.zeros(0, "<u8")])
             for i in range(len(off) - 1)]
     assert wr.tobytes() == np.concatenate(segs).tobytes()
+
+
+def test_c1_addressbook_fixture(oracle):
+    """Config C1: the addressbook sample's message (samples/addressbook.c++:47-76) and its
+    packed form, both hash-pinned to the compiled sample; the oracle packs the
+    one to the other and reads it back (addressbook.c++:79, PackedFdMessageReader)."""
+    import hashlib
+
+    msg, packed = _read("addressbook.bin"), _read("addressbook.packed")
+    assert hashlib.sha256(msg).hexdigest().startswith("6734639c")
+    assert hashlib.sha256(packed).hexdigest().startswith("6cb6a027")
+    w = P.words_of(msg)
+    got, st = oracle.pack_flat(w)
+    assert st == P.OK and got == packed
+    rs, rw, used = oracle.read_message(packed)
+    assert rs == P.OK and used == len(packed) and rw.tobytes() == msg
+
+
+@pytest.mark.parametrize("name", ["c2", "c3", "c4", "c5", "c5r0of8"])
+def test_manifest_prefixes(oracle, name):
+    """The oracle's host generator + packer reproduce the reference's hashes for the first
+    messages of every bench configuration (tests/golden/manifest.json, tools/make_manifest.py)."""
+    import hashlib
+
+    c = json.load(open(os.path.join(G, "manifest.json")))["configs"][name]
+    pre = c["prefix"]
+    off = oracle.gen_offsets(pre["nmsgs"], nseg=c["nseg"], seg_words=c["seg_words"],
+                             seed=c["seed"], first_msg=c["first_msg"], msg_stride=c["msg_stride"])
+    w = oracle.gen_messages(c["profile"], off, nseg=c["nseg"], seed=c["seed"],
+                            first_msg=c["first_msg"], msg_stride=c["msg_stride"])
+    assert int(off[-1]) == pre["words"]
+    assert hashlib.sha256(w).hexdigest() == pre["sha256_words"]
+    packed, poff, st = oracle.pack_batch(w, off)
+    assert (st == 0).all() and len(packed) == pre["packed_bytes"]
+    assert hashlib.sha256(packed).hexdigest() == pre["sha256_packed"]
+    assert hashlib.sha256(poff.astype("<u8")).hexdigest() == pre["sha256_out_off"]

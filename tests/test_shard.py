@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 import torch.multiprocessing as mp
 
-from capnproto_amd.shard import reduce_step, shard_messages
+from capnproto_amd.shard import balanced_ranges, global_offsets, reduce_step, shard_messages
 
 
 @pytest.mark.parametrize("mode", ["block", "round_robin"])
@@ -56,7 +56,9 @@ def _worker(rank, world, port, q):
         same = per_msg == alone
         red = reduce_step(0.5 + rank, float(off[-1] * 8), float(poff[-1]), 1.0 + rank, 2.0,
                           same, dist=dist)
-        q.put((rank, red, same, [first + stride * i for i in range(count)]))
+        base, gtotal = global_offsets(int(poff[-1]), dist=dist)
+        q.put((rank, red, same, [first + stride * i for i in range(count)],
+               (base, gtotal, bytes(packed))))
     finally:
         dist.destroy_process_group()
 
@@ -75,8 +77,24 @@ def test_gloo_world2_shards_and_reduction():
     out.sort()
     ids = sorted(out[0][3] + out[1][3])
     assert ids == list(range(12))
-    for rank, red, same, _ in out:
+    for rank, red, same, _, _ in out:
         assert same, "per-message packed bytes depend on the shard"
         assert red["dt_max"] == 1.5 and red["pack_ms"] == 2.0
         assert red["ok_all"]
     assert out[0][1]["unpacked_all"] == out[1][1]["unpacked_all"] > 0
+    # global placement from the all-gathered per-rank totals: rank 1 starts where rank 0 ends,
+    # and the concatenation is the whole batch's packed stream
+    (b0, t0, p0), (b1, t1, p1) = out[0][4], out[1][4]
+    assert b0 == 0 and b1 == len(p0) and t0 == t1 == len(p0) + len(p1)
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_balanced_ranges(world):
+    rng = np.random.default_rng(world)
+    sizes = 2 ** rng.integers(3, 12, 5000) + 1  # C5-like: 2^k words + table word
+    off = np.concatenate([[0], np.cumsum(sizes)])
+    parts = balanced_ranges(off, world)
+    assert sum(c for _, c in parts) == len(sizes)
+    assert [f for f, _ in parts] == list(np.cumsum([0] + [c for _, c in parts])[:-1])
+    loads = [int(off[f + c] - off[f]) for f, c in parts]
+    assert max(loads) - min(loads) <= 2 * int(sizes.max())
