@@ -27,6 +27,11 @@ struct cpk_ctx {
   bool timing = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[CPK_TIMERS];
   std::vector<hipEvent_t> pool;
+  // diagnostics: the last pack call's per-tile tables (cpk_debug_pack_tables)
+  uint64_t* dbg_tile_bytes = nullptr;
+  uint8_t* dbg_step_b = nullptr;
+  uint32_t* dbg_tile_b = nullptr;
+  uint64_t dbg_ntiles = 0;
 };
 
 namespace cpk {
@@ -122,6 +127,7 @@ struct PackScratch {
   uint32_t* tile_b;
   uint64_t* tile_bytes;
   uint64_t* tile_off;
+  uint8_t* step_b;
   size_t total;
 };
 
@@ -141,6 +147,7 @@ PackScratch carve_pack(void* base, uint64_t N, uint64_t ntiles) {
   s.tile_b = c.take<uint32_t>(ntiles);
   s.tile_bytes = c.take<uint64_t>(ntiles);
   s.tile_off = c.take<uint64_t>(ntiles + 1);
+  s.step_b = c.take<uint8_t>(16 * ntiles);
   s.total = c.off;
   return s;
 }
@@ -154,7 +161,7 @@ cpk_status pack_common(cpk_ctx* ctx, const uint64_t* d_words, uint64_t N, const 
                        uint64_t* d_out_off, int32_t* d_status, hipStream_t stream) {
   if (!ctx || (!d_off && n) || (!d_words && N) || (!d_out && cap)) return CPK_ERR_INVALID_ARGUMENT;
   if (hipSetDevice(ctx->device) != hipSuccess) return CPK_ERR_HIP;
-  const uint64_t T = 64ull * cpk::pack_steps();
+  const uint64_t T = 64ull * (cpk::pack_v2() ? cpk::pack2_steps() : cpk::pack_steps());
   const uint64_t ntiles = (N + T - 1) / T;
   cpk_status st = ensure(&ctx->scratch, &ctx->scratch_size, pack_scratch_bytes(N, ntiles));
   if (st != CPK_OK) return st;
@@ -195,11 +202,18 @@ cpk_status pack_common(cpk_ctx* ctx, const uint64_t* d_words, uint64_t N, const 
   a.tile_b = s.tile_b;
   a.tile_bytes = s.tile_bytes;
   a.tile_off = s.tile_off;
+  a.step_b = s.step_b;
   a.err = ctx->err;
+  ctx->dbg_tile_bytes = s.tile_bytes;
+  ctx->dbg_step_b = s.step_b;
+  ctx->dbg_tile_b = s.tile_b;
+  ctx->dbg_ntiles = ntiles;
   a.stamps = cpk::debug_stamps(0);
   a.debug_skip = cpk::debug_skip();
   TimedLaunch tl(ctx, 0, stream);
-  if (cpk::pack_fused() || a.stamps) {
+  if (cpk::pack_v2()) {
+    e = cpk::launch_pack_tiles2(a, stream);
+  } else if (cpk::pack_fused() || a.stamps) {
     e = cpk::launch_pack_tiles(a, stream);
   } else {
     // count pass -> scan of tile byte counts -> emit pass
@@ -749,6 +763,18 @@ cpk_status cpk_unpacked_size_host(cpk_ctx* ctx, const uint8_t* h_packed, uint64_
       hipMemcpy(&ms, d_status, 4, hipMemcpyDeviceToHost) != hipSuccess)
     return CPK_ERR_HIP;
   return (cpk_status)ms;
+}
+
+// Diagnostic (not in include/cpk.h): the last pack call's per-tile tables (two-pass kernels).
+extern "C" cpk_status cpk_debug_pack_tables(cpk_ctx* ctx, uint64_t* bytes, uint32_t* tile_b,
+                                            uint8_t* step_b, uint64_t n) {
+  if (!ctx || !ctx->dbg_tile_bytes || n > ctx->dbg_ntiles) return CPK_ERR_INVALID_ARGUMENT;
+  if (hipDeviceSynchronize() != hipSuccess) return CPK_ERR_HIP;
+  if (hipMemcpy(bytes, ctx->dbg_tile_bytes, 8 * n, hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemcpy(tile_b, ctx->dbg_tile_b, 4 * n, hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemcpy(step_b, ctx->dbg_step_b, 16 * n, hipMemcpyDeviceToHost) != hipSuccess)
+    return CPK_ERR_HIP;
+  return CPK_OK;
 }
 
 // Diagnostic (not in include/cpk.h): copies and clears the phase-stamp sums (CPK_STAMPS=1).

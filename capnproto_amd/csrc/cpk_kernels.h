@@ -33,7 +33,8 @@ struct PackTileArgs {
   // two-pass form: count pass -> (entry budget, bytes) per tile; scan -> output offsets
   uint32_t* tile_b;
   uint64_t* tile_bytes;
-  const uint64_t* tile_off;
+  uint64_t* tile_off;
+  uint8_t* step_b;             // two-pass kernels (cpk_pack2.hip): budget entering each step
   uint32_t* err;
   unsigned long long* stamps;  // diagnostic build only (env CPK_STAMPS), else NULL
   uint32_t debug_skip;         // timing ablations only (env CPK_DEBUG_SKIP): 1 = no look-back
@@ -42,6 +43,10 @@ struct PackTileArgs {
 int pack_steps();  // words per pack tile = 64 * pack_steps()
 bool pack_fused();  // single-pass kernel (default) or count + emit (A/B knob CPK_PACK_TWO_PASS=1)
 hipError_t launch_pack_tiles(const PackTileArgs& a, hipStream_t stream);
+// single-sweep pack kernel (cpk_pack2.hip, the default; CPK_PACK_V1=1 selects the kernels above)
+int pack2_steps();  // words per tile = 64 * pack2_steps()
+bool pack_v2();
+hipError_t launch_pack_tiles2(const PackTileArgs& a, hipStream_t stream);
 hipError_t launch_pack_stage(int stage, const PackTileArgs& a, hipStream_t stream);
 hipError_t launch_message_bits(const uint64_t* words, const uint64_t* off, uint64_t n,
                                uint64_t* bits, int32_t* status, hipStream_t stream);
