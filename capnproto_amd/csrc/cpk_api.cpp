@@ -40,7 +40,7 @@ uint32_t debug_skip() {
   return v;
 }
 unsigned long long* debug_stamps(int which) {
-  static unsigned long long* bufs[2] = {nullptr, nullptr};
+  static unsigned long long* bufs[4] = {nullptr, nullptr, nullptr, nullptr};
   static const bool on = getenv("CPK_STAMPS") && atoi(getenv("CPK_STAMPS")) != 0;
   if (!on) return nullptr;
   if (!bufs[which]) {
@@ -359,6 +359,7 @@ cpk_status unpack_common(cpk_ctx* ctx, uint32_t mode, const uint8_t* d_packed, u
   a.fail_count = s.fail_count;
   a.err = ctx->err;
   a.stamps = cpk::debug_stamps(1);  // diagnostic counters (CPK_STAMPS=1), else NULL
+  a.stamps2 = cpk::debug_stamps(2);  // diagnostic phase cycles of index_kernel
   a.debug_skip = cpk::debug_skip();
   a.tm = s.tm;
   a.t_wex = s.t_wex;

@@ -365,24 +365,42 @@ __device__ __forceinline__ void publish_incl(uint64_t* desc, uint64_t* gdesc, ui
 // debug buffer, never into outputs.
 constexpr int kStampSlots = 16;
 __device__ __forceinline__ uint64_t stamp_now() {
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  return __builtin_amdgcn_s_memtime();
+  // no s_waitcnt: a phase ends where the wave gets to, memory still in flight (forcing the wait
+  // at every mark serialised the loads the phases are meant to overlap)
+  asm volatile("" ::: "memory");
+  const uint64_t t = __builtin_amdgcn_s_memtime();
+  asm volatile("" ::: "memory");
+  return t;
 }
 template <bool ON>
 struct Stamps {
+  // deltas accumulate in registers; flush() adds them to the debug buffer once (a global atomic
+  // per mark would put its own round trip into every measured phase)
   unsigned long long* buf;
   uint64_t last;
+  uint64_t acc[kStampSlots];
   __device__ __forceinline__ void start(unsigned long long* b) {
     if constexpr (ON) {
       buf = b;
+      for (int i = 0; i < kStampSlots; i++) acc[i] = 0;
       last = stamp_now();
     }
+  }
+  __device__ __forceinline__ void restart() {
+    if constexpr (ON) last = stamp_now();
   }
   __device__ __forceinline__ void mark(int slot) {
     if constexpr (ON) {
       const uint64_t now = stamp_now();
-      if (lane_id() == 0 && buf) atomicAdd(buf + slot, (unsigned long long)(now - last));
+      acc[slot] += now - last;
       last = now;
+    }
+  }
+  __device__ __forceinline__ void flush() {
+    if constexpr (ON) {
+      if (lane_id() == 0 && buf)
+        for (int i = 0; i < kStampSlots - 1; i++)
+          if (acc[i]) atomicAdd(buf + i, (unsigned long long)acc[i]);
     }
   }
 };

@@ -80,6 +80,7 @@ struct UnpackArgs {
   uint32_t* fail_count;
   uint32_t* err;
   unsigned long long* stamps;   // diagnostic build only (env CPK_STAMPS), else NULL
+  unsigned long long* stamps2;  // diagnostic: per-phase cycles of index_kernel
   uint32_t debug_skip;
   // tile tables: index_kernel -> resolve_kernel -> expand_kernel (cpk_unpack.hip)
   uint64_t* tm;                 // ntiles*64 chain-0 record-start masks (bit = byte of a sub-tile)

@@ -213,6 +213,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S <= 8 ? 6 
   uint32_t* const state = a.state;
   const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
   Stamps<STAMPS> stm;
+  stm.start(a.stamps);
   uint64_t t = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wv;
   TileLoad<S> cur;
   if (t < a.ntiles) load_tile<S>(a, t, cur);
@@ -292,7 +293,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S <= 8 ? 6 
     TileLoad<S> nxt;
     auto tile = [&](auto full_c) {
     constexpr bool FULL = decltype(full_c)::value;
-    stm.start(a.stamps);
+    stm.restart();
     const uint64_t tbase = t * T;
     const uint64_t tend = tbase + T < N ? tbase + T : N;
     const int nvalid = FULL ? T : (int)(tend - tbase);
@@ -313,27 +314,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S <= 8 ? 6 
     static_for<0, S>([&](auto sc) {
       constexpr int s = decltype(sc)::value;
       const uint64_t x = cur.x[s];
-      const uint32_t tag = tag_of((uint32_t)x, (uint32_t)(x >> 32));
-      if (s & 1) {
-        tagpk[s >> 1] |= tag << 16;
-        asm volatile("" : "+v"(tagpk[s >> 1]));  // keep the packed form (VGPR pressure)
-      } else {
-        tagpk[s >> 1] = tag;
-      }
+      if (s % 2 == 0) tagpk[s >> 1] = 0;
       const uint64_t Z = ballot(x == 0);  // words past the batch end load as 0: masked below
-      const uint64_t R = ballot(__popc(tag) >= 7);
-      const uint64_t Fs = ballot(tag == 0xff);
-      vFlo = setlane<s>(vFlo, (uint32_t)Fs);
-      vFhi = setlane<s>(vFhi, (uint32_t)(Fs >> 32));
       vZlo = setlane<s>(vZlo, (uint32_t)Z);
       vZhi = setlane<s>(vZhi, (uint32_t)(Z >> 32));
-      vRlo = setlane<s>(vRlo, (uint32_t)R);
-      vRhi = setlane<s>(vRhi, (uint32_t)(R >> 32));
-      // sum of nz over the O words of the step (their bytes are 1 + nz)
-      const uint32_t nz = __popc(tag);
-      const uint32_t ob = (x != 0 && nz < 7) ? nz : 0;
-      vOb = setlane<s>(vOb, (uint32_t)(__popcll(ballot(ob & 1)) + 2 * __popcll(ballot(ob & 2)) +
-                                       4 * __popcll(ballot(ob & 4))));
+      if (Z != ~0ull) {  // an all-zero step has tag 0, no R / F word and no O bytes
+        const uint32_t tag = tag_of((uint32_t)x, (uint32_t)(x >> 32));
+        tagpk[s >> 1] |= tag << (16 * (s & 1));
+        asm volatile("" : "+v"(tagpk[s >> 1]));  // keep the packed form (VGPR pressure)
+        const uint64_t R = ballot(__popc(tag) >= 7);
+        const uint64_t Fs = ballot(tag == 0xff);
+        vFlo = setlane<s>(vFlo, (uint32_t)Fs);
+        vFhi = setlane<s>(vFhi, (uint32_t)(Fs >> 32));
+        vRlo = setlane<s>(vRlo, (uint32_t)R);
+        vRhi = setlane<s>(vRhi, (uint32_t)(R >> 32));
+        // sum of nz over the O words of the step (their bytes are 1 + nz)
+        const uint32_t nz = __popc(tag);
+        const uint32_t ob = (x != 0 && nz < 7) ? nz : 0;
+        vOb = setlane<s>(vOb, (uint32_t)(__popcll(ballot(ob & 1)) +
+                                         2 * __popcll(ballot(ob & 2)) +
+                                         4 * __popcll(ballot(ob & 4))));
+      }
     });
     bool lastZ, lastR;
     int first_sync = T, sg = -1;
@@ -561,6 +562,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S <= 8 ? 6 
         const uint64_t ZH = readlane64(((uint64_t)vZHhi << 32) | vZHlo, s);
         const uint64_t FH = readlane64(((uint64_t)vFHhi << 32) | vFHlo, s);
         const uint32_t soff = readlane32(vSoff, s);
+        const uint64_t Zs = ((uint64_t)readlane32(vZhi, s) << 32) | readlane32(vZlo, s);
+        if (Zs == ~0ull && !(prel < 64u * s + 64u)) {
+          // all-zero step: the records are its Z heads, two bytes each ([00, count]); the tag
+          // byte stays zero in the staging area, only a non-zero count is stored
+          uint64_t hm = ZH;
+          uint32_t k = 0;
+          while (hm) {
+            const int h = lowest_bit(hm);
+            hm &= hm - 1;
+            const uint64_t after = SY & ~mask_le(h);
+            const uint32_t ns = after ? (uint32_t)lowest_bit(after) : 64u + readlane32(vNsa, s);
+            const uint32_t cnt = min(ns - (uint32_t)h - 1u, 255u);
+            if (cnt && l == 0) stg[base + 16u + soff + 2 * k + 1] = (uint8_t)cnt;
+            k++;
+          }
+          continue;
+        }
         // record length: head 1 + nz (+1 count byte for run heads), covered R 8, covered Z 0
         const uint32_t n1 = nz + 1;
         const uint32_t len = msel(COV, n1 & 8u, n1 + msel(ZH | FH, 1u, 0u));
@@ -645,6 +663,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S <= 8 ? 6 
     if (PF) cur = nxt;
   }  // tile loop
   if (pend.on) finish(pend);
+  stm.flush();
 }
 
 // Chunk-start bitmap + per-message framing status for a batch of flat messages.
