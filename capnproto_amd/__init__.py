@@ -75,6 +75,8 @@ def load_library():
         "cpk_unpack_messages": (C.c_int, [vp, vp, u64, vp, u64, vp, u64, vp, vp, vp, vp]),
         "cpk_unpacked_size": (C.c_int, [vp, vp, u64, vp, u64, vp, vp, vp]),
         "cpk_unpack_chunks": (C.c_int, [vp, vp, u64, vp, vp, u64, vp, u64, vp, vp]),
+        "cpk_split_packed_stream": (C.c_int, [vp, vp, u64, vp, u64, u64, vp, vp, vp, vp, vp,
+                                              vp]),
         "cpk_pack_messages_host": (C.c_int, [vp, vp, u64, vp, u64, vp, u64, vp, vp]),
         "cpk_unpack_messages_host": (C.c_int, [vp, vp, u64, vp, u64, vp, u64, vp, vp, vp]),
         "cpk_gen_messages": (C.c_int, [vp, C.c_int, u64, u64, u64, u64, u32, vp, vp, vp]),
@@ -227,6 +229,30 @@ class Codec:
                                                _ptr(status), self._stream(stream)),
                     "cpk_unpack_chunks")
         return words, status[:n]
+
+    def split_packed_stream(self, packed, words_capacity, max_msgs, nbytes=None, words=None,
+                            traversal_limit_words=None, stream=None):
+        """Stream boundary discovery (include/cpk.h cpk_split_packed_stream): messages back to
+        back in one packed buffer, offsets unknown.  Returns (words, msg_word_off, msg_in_off,
+        status, nmsgs) -- device tensors with max_msgs + 1 entries, nmsgs a 1-element device
+        tensor."""
+        torch = self.torch
+        P = packed.numel() if nbytes is None else nbytes
+        if words is None:
+            words = torch.empty(max(words_capacity, 1), dtype=torch.int64, device=self.device)
+        woff = torch.empty(max_msgs + 1, dtype=torch.int64, device=self.device)
+        ioff = torch.empty(max_msgs + 1, dtype=torch.int64, device=self.device)
+        status = torch.empty(max_msgs + 1, dtype=torch.int32, device=self.device)
+        n = torch.empty(1, dtype=torch.int64, device=self.device)
+        lim = None
+        if traversal_limit_words is not None:
+            lim = C.byref(Limits(traversal_limit_words))
+        self._check(self.lib.cpk_split_packed_stream(self.ctx, _ptr(packed), P, _ptr(words),
+                                                     words_capacity, max_msgs, _ptr(woff),
+                                                     _ptr(ioff), _ptr(status), _ptr(n), lim,
+                                                     self._stream(stream)),
+                    "cpk_split_packed_stream")
+        return words, woff, ioff, status, n
 
     # ------------------------------------------------------------------ measurement hooks
     def timing(self, on: bool = True):

@@ -6,6 +6,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <new>
 #include <utility>
 #include <vector>
@@ -303,7 +304,8 @@ cpk_status unpack_common(cpk_ctx* ctx, uint32_t mode, const uint8_t* d_packed, u
                          const uint64_t* d_in_off, uint64_t n, const uint64_t* d_word_off_in,
                          uint64_t* d_words, uint64_t cap, uint64_t* d_word_off_out,
                          int32_t* d_status, uint64_t* d_size_out, uint64_t limit,
-                         hipStream_t stream, uint64_t* d_in_end = nullptr) {
+                         hipStream_t stream, uint64_t* d_in_end = nullptr,
+                         uint64_t* d_rec_pos = nullptr) {
   if (!ctx || (!d_in_off && n) || (!d_packed && P) || (!d_status && n))
     return CPK_ERR_INVALID_ARGUMENT;
   if (hipSetDevice(ctx->device) != hipSuccess) return CPK_ERR_HIP;
@@ -347,6 +349,7 @@ cpk_status unpack_common(cpk_ctx* ctx, uint32_t mode, const uint8_t* d_packed, u
   a.status = d_status;
   a.size_out = d_size_out;
   a.in_end = d_in_end;
+  a.rec_pos = d_rec_pos;
   a.mode = mode;
   a.ntiles = ntiles;
   a.tile_counter = nullptr;
@@ -556,6 +559,41 @@ cpk_status cpk_read_packed_messages(cpk_ctx* ctx, const uint8_t* d_packed, uint6
                        (hipStream_t)stream, d_msg_in_end);
 }
 
+cpk_status cpk_split_packed_stream(cpk_ctx* ctx, const uint8_t* d_packed, uint64_t nbytes,
+                                   uint64_t* d_words, uint64_t words_capacity, uint64_t max_msgs,
+                                   uint64_t* d_msg_word_off, uint64_t* d_msg_in_off,
+                                   int32_t* d_status, uint64_t* d_nmsgs, const cpk_limits* limits,
+                                   void* stream) {
+  if (!ctx || (!d_packed && nbytes) || !d_msg_word_off || !d_msg_in_off || !d_status || !d_nmsgs ||
+      (!d_words && words_capacity) || (words_capacity == 0 && nbytes))
+    return CPK_ERR_INVALID_ARGUMENT;
+  if (hipSetDevice(ctx->device) != hipSuccess) return CPK_ERR_HIP;
+  const uint64_t limit = limits ? limits->traversal_limit_words : 8ull * 1024 * 1024;
+  hipStream_t s = (hipStream_t)stream;
+  // the record-head map (one u64 per output word) and 8 words of call state: in_off[2],
+  // word_off[2], meta[4] (stop byte, stop word, decode status)
+  cpk_status st = ensure(&ctx->stage[3], &ctx->stage_size[3], words_capacity * 8 + 128);
+  if (st != CPK_OK) return st;
+  uint64_t* state = (uint64_t*)ctx->stage[3];
+  uint64_t* rec_pos = state + 8;
+  uint64_t* meta = state + 4;
+  hipError_t e = cpk::launch_set_u64x4(state, 0, nbytes, 0, words_capacity, s);
+  if (e == hipSuccess) e = cpk::launch_set_u64x4(meta, 0, 0, CPK_ERR_PREMATURE_EOF, 0, s);
+  if (e == hipSuccess && words_capacity)
+    e = hipMemsetAsync(rec_pos, 0xff, words_capacity * 8, s);
+  if (e != hipSuccess) return CPK_ERR_HIP;
+  if (nbytes) {
+    // the whole stream as one flat chunk of up to words_capacity words, stopping at the first
+    // record the input cuts (prefix mode: meta[0..1] = where it stopped)
+    st = unpack_common(ctx, 1, d_packed, nbytes, state, 1, state + 2, d_words, words_capacity,
+                       nullptr, (int32_t*)(meta + 2), meta + 1, 0, s, meta, rec_pos);
+    if (st != CPK_OK) return st;
+  }
+  return hip_status(cpk::launch_split_walk(d_packed, nbytes, d_words, rec_pos, meta, max_msgs,
+                                           limit, d_msg_word_off, d_msg_in_off, d_status,
+                                           d_nmsgs, s));
+}
+
 cpk_status cpk_unpacked_size(cpk_ctx* ctx, const uint8_t* d_packed, uint64_t total_bytes,
                              const uint64_t* d_in_off, uint64_t n, uint64_t* d_words_out,
                              int32_t* d_status, void* stream) {
@@ -736,6 +774,60 @@ cpk_status cpk_unpack_words_host(cpk_ctx* ctx, const uint8_t* h_packed, uint64_t
   if (hipMemcpy(h_words, d_words, nwords * 8, hipMemcpyDeviceToHost) != hipSuccess)
     return CPK_ERR_HIP;
   return CPK_OK;
+}
+
+cpk_status cpk_unpack_prefix_host(cpk_ctx* ctx, const uint8_t* h_packed, uint64_t avail_bytes,
+                                  uint64_t* h_words, uint64_t max_words, uint64_t* words_out,
+                                  uint64_t* consumed_out) {
+  if (!ctx || (!h_packed && avail_bytes) || !words_out || !consumed_out)
+    return CPK_ERR_INVALID_ARGUMENT;
+  if (hipSetDevice(ctx->device) != hipSuccess) return CPK_ERR_HIP;
+  *words_out = 0;
+  *consumed_out = 0;
+  if (max_words == 0) return CPK_OK;
+  if (avail_bytes == 0) return CPK_ERR_PREMATURE_EOF;
+  // a record of b bytes yields at most 128 b words (a 2-byte zero run: 256 words), so the
+  // device never writes past min(max_words, 128 * avail + 256) words
+  const uint64_t room = std::min<uint64_t>(max_words, 128 * avail_bytes + 256);
+  cpk_status st;
+  if ((st = ensure(&ctx->stage[0], &ctx->stage_size[0], room * 8 + 16)) != CPK_OK) return st;
+  if ((st = ensure(&ctx->stage[1], &ctx->stage_size[1], avail_bytes + 16)) != CPK_OK) return st;
+  if ((st = ensure(&ctx->stage[2], &ctx->stage_size[2], 80)) != CPK_OK) return st;
+  uint64_t* d_words = (uint64_t*)ctx->stage[0];
+  uint8_t* d_packed = (uint8_t*)ctx->stage[1];
+  uint64_t* d_in_off = (uint64_t*)ctx->stage[2];  // [2]
+  uint64_t* d_word_off = d_in_off + 2;            // [2]
+  uint64_t* d_in_end = d_word_off + 2;            // [1]
+  uint64_t* d_at = d_in_end + 1;                  // [1]
+  int32_t* d_status = (int32_t*)(d_at + 1);
+  const uint64_t offs[4] = {0, avail_bytes, 0, max_words};
+  hipStream_t s = nullptr;
+  if (hipMemcpyAsync(d_packed, h_packed, avail_bytes, hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipMemcpyAsync(d_in_off, offs, 32, hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipMemsetAsync(d_in_end, 0, 16, s) != hipSuccess)
+    return CPK_ERR_HIP;
+  // one exact-size chunk of max_words words (the flat-packed mode); with d_at given the
+  // terminal record also reports where a short or overshooting read stops
+  st = unpack_common(ctx, 1, d_packed, avail_bytes, d_in_off, 1, d_word_off, d_words, max_words,
+                     nullptr, d_status, d_at, 0, s, d_in_end);
+  if (st != CPK_OK) return st;
+  if ((st = cpk_sync(ctx, s)) != CPK_OK) return st;
+  uint64_t at[2] = {0, 0};  // in_end, words
+  int32_t ms = 0;
+  if (hipMemcpy(at, d_in_end, 16, hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemcpy(&ms, d_status, 4, hipMemcpyDeviceToHost) != hipSuccess)
+    return CPK_ERR_HIP;
+  if (ms == CPK_ERR_TRAILING_BYTES) ms = CPK_OK;  // the rest of the buffer is not ours
+  if (ms != CPK_OK && ms != CPK_ERR_PREMATURE_EOF && ms != CPK_ERR_RUN_OVERSHOOT)
+    return (cpk_status)ms;
+  if (ms == CPK_OK) at[1] = max_words;
+  if (at[0] > avail_bytes || at[1] > room) return CPK_ERR_INTERNAL;
+  *words_out = at[1];
+  *consumed_out = at[0];
+  if (h_words && at[1] &&
+      hipMemcpy(h_words, d_words, at[1] * 8, hipMemcpyDeviceToHost) != hipSuccess)
+    return CPK_ERR_HIP;
+  return (cpk_status)ms;
 }
 
 cpk_status cpk_unpacked_size_host(cpk_ctx* ctx, const uint8_t* h_packed, uint64_t nbytes,

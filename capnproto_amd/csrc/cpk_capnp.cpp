@@ -8,6 +8,8 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <exception>
+#include <utility>
 
 namespace cpk_capnp {
 
@@ -81,9 +83,10 @@ void OutputStream::write(ArrayPtr<const ArrayPtr<const byte>> pieces) {
   for (auto& p : pieces) write(p.begin(), p.size());
 }
 
-void InputStream::read(void* buffer, size_t bytes) {
-  const size_t n = tryRead(buffer, bytes, bytes);
-  if (n < bytes) fail(CPK_ERR_PREMATURE_EOF, "InputStream::read");
+size_t InputStream::read(void* buffer, size_t minBytes, size_t maxBytes) {
+  const size_t n = tryRead(buffer, minBytes, maxBytes);
+  if (n < minBytes) fail(CPK_ERR_PREMATURE_EOF, "InputStream::read");
+  return n;
 }
 
 void InputStream::skip(size_t bytes) {
@@ -129,8 +132,24 @@ void ArrayInputStream::skip(size_t bytes) {
   array_ = array_.slice(bytes, array_.size());
 }
 
+OwnFd& OwnFd::operator=(OwnFd&& o) noexcept {
+  if (this != &o) {
+    if (fd_ >= 0) ::close(fd_);
+    fd_ = o.fd_;
+    o.fd_ = -1;
+  }
+  return *this;
+}
+
+OwnFd::~OwnFd() {
+  if (fd_ >= 0) ::close(fd_);
+}
+
 FdBufferedInputStream::FdBufferedInputStream(int fd, size_t bufferSize)
     : fd_(fd), buf_(bufferSize) {}
+
+FdBufferedInputStream::FdBufferedInputStream(OwnFd fd, size_t bufferSize)
+    : owned_(std::move(fd)), fd_(owned_.get()), buf_(bufferSize) {}
 
 ArrayPtr<const byte> FdBufferedInputStream::tryGetReadBuffer() {
   if (begin_ == end_) {
@@ -225,124 +244,189 @@ void writePackedMessageToFd(int fd, ArrayPtr<const ArrayPtr<const word>> segment
 }
 
 // ---- unpack ----------------------------------------------------------------------------------
+namespace {
+
+// Byte length and word count of the record at v[q] (doc/encoding.md:296-349), for the few
+// boundaries in a buffer's last 9 bytes that the device does not report one by one.
+size_t rec_len(const byte* v, size_t q) {
+  const unsigned tag = v[q];
+  const size_t run = (tag == 0 || tag == 0xff) ? 1 : 0;
+  return 1 + (size_t)__builtin_popcount(tag) + run + (tag == 0xff ? 8 * (size_t)v[q + 9] : 0);
+}
+uint64_t rec_words(const byte* v, size_t q) {
+  const unsigned tag = v[q];
+  return 1 + (tag == 0 ? v[q + 1] : (tag == 0xff ? v[q + 9] : 0));
+}
+
+}  // namespace
+
+size_t _::PackedInputStream::readWords(uint64_t* dst, size_t minw, size_t maxw) {
+  // serialize-packed.c++:34-183.  Each pass hands the device one stream buffer V (with the
+  // start of a record the previous buffer cut in front of it) and gets back where the read
+  // stops in V: max words out, a run crossing max (overshoot), or the start of the record V
+  // cuts.  The reference also returns at the first record boundary with fewer than 10 bytes left
+  // in V once min words are out (:71-76); those boundaries are checked here from the device's
+  // word counts.
+  cpk_ctx* ctx = threadContext();
+  ArrayPtr<const byte> buf = inner_.tryGetReadBuffer();
+  if (buf.size() == 0) return 0;  // :48-51: nothing at all to read
+  std::vector<byte> carry;         // bytes of V already taken from the stream (a cut record)
+  size_t out = 0;
+  for (;;) {
+    const byte* v = buf.begin();
+    size_t vlen = buf.size();
+    const size_t carried = carry.size();
+    if (carried) {
+      carry.insert(carry.end(), buf.begin(), buf.end());
+      v = carry.data();
+      vlen = carry.size();
+    }
+    const uint64_t want = maxw - out;
+    // a record yields at least one word per 10 bytes, so max words never need more than
+    // 10 * want + 10 bytes (and then no boundary lies in V's last 9 bytes)
+    const size_t look = want < vlen / 10 ? (size_t)(10 * want + 10) : vlen;
+    uint64_t w = 0, c = 0;
+    const cpk_status st =
+        cpk_unpack_prefix_host(ctx, v, look, dst ? dst + out : nullptr, want, &w, &c);
+    if (st != CPK_OK && st != CPK_ERR_PREMATURE_EOF && st != CPK_ERR_RUN_OVERSHOOT)
+      fail(st, "PackedInputStream");
+    if (look < vlen && st == CPK_ERR_PREMATURE_EOF) fail(CPK_ERR_INTERNAL, "PackedInputStream");
+    auto consume = [&](size_t q) { inner_.skip(q - carried); };
+    const size_t s = vlen > 9 ? vlen - 9 : 0;  // boundaries at >= s leave < 10 bytes
+    if (look == vlen && c >= s && out + w >= minw) {
+      // the boundaries in [s, c]: walk from the record holding byte s (found by the device)
+      uint64_t b0 = 0, wb0 = 0;
+      if (s > 0) {
+        const cpk_status st0 = cpk_unpack_prefix_host(ctx, v, s, nullptr, want, &wb0, &b0);
+        if (st0 != CPK_OK && st0 != CPK_ERR_PREMATURE_EOF)
+          fail(st0 == CPK_ERR_RUN_OVERSHOOT ? CPK_ERR_INTERNAL : st0, "PackedInputStream");
+      }
+      uint64_t q = b0, wq = wb0;
+      if (q < s) {
+        wq += rec_words(v, q);
+        q += rec_len(v, q);
+      }
+      while (q <= c) {
+        // a raw run that crossed into this buffer and ends with it: the reference asks the
+        // stream for more before it looks at the boundary (:157-168)
+        const bool crossed = q == vlen && carried && v[0] == 0xff && 9 < carried && v[9] != 0 &&
+                             rec_len(v, 0) == vlen;
+        if (out + wq >= minw && !crossed) {
+          consume(q);
+          return out + wq;
+        }
+        if (q == c) break;
+        wq += rec_words(v, q);
+        q += rec_len(v, q);
+      }
+    }
+    if (st == CPK_OK) {
+      consume(c);
+      return maxw;
+    }
+    if (st == CPK_ERR_RUN_OVERSHOOT) fail(st, "PackedInputStream");
+    // V ends inside the record at c (or at c itself): keep its bytes and read on
+    out += w;
+    if (carried) {
+      carry.erase(carry.begin(), carry.begin() + (ptrdiff_t)c);
+    } else {
+      carry.assign(buf.begin() + c, buf.end());
+    }
+    inner_.skip(buf.size());
+    buf = inner_.tryGetReadBuffer();
+    if (buf.size() == 0) fail(CPK_ERR_PREMATURE_EOF, "PackedInputStream");  // :57
+  }
+}
+
 size_t _::PackedInputStream::tryRead(void* buffer, size_t minBytes, size_t maxBytes) {
-  // serialize-packed.c++:34-51
   if (maxBytes == 0) return 0;
   if (minBytes % 8 != 0 || maxBytes % 8 != 0)
     fail(CPK_ERR_INVALID_ARGUMENT, "PackedInputStream reads must be word-aligned.");
   if (minBytes > maxBytes) minBytes = maxBytes;
-  cpk_ctx* ctx = threadContext();
-  uint64_t* dst = static_cast<uint64_t*>(buffer);
-  std::vector<byte> acc;  // bytes already taken from the stream (the read spans buffers)
-  for (;;) {
-    ArrayPtr<const byte> buf = inner_.tryGetReadBuffer();
-    if (acc.empty() && buf.size() == 0) return 0;  // :48-51: nothing at all to read
-    const byte* data = buf.begin();
-    size_t avail = buf.size();
-    if (!acc.empty()) {
-      acc.insert(acc.end(), buf.begin(), buf.end());
-      data = acc.data();
-      avail = acc.size();
-    }
-    const size_t before = acc.empty() ? 0 : acc.size() - buf.size();
-    uint64_t used = 0;
-    cpk_status st = cpk_unpack_words_host(ctx, data, avail, dst, maxBytes / 8, &used);
-    if (st == CPK_ERR_PREMATURE_EOF && buf.size() > 0) {
-      // the records continue past what is buffered: take these bytes and refill
-      if (acc.empty()) acc.assign(buf.begin(), buf.end());
-      inner_.skip(buf.size());
-      continue;
-    }
-    if (st == CPK_ERR_PREMATURE_EOF) {
-      // the input has ended: what it holds is enough if it ends at a record boundary with at
-      // least minBytes of output (:65-80, the early return once out >= outMin)
-      uint64_t have = 0;
-      if (cpk_unpacked_size_host(ctx, data, avail, &have) == CPK_OK && have * 8 >= minBytes &&
-          have * 8 < maxBytes) {
-        check(cpk_unpack_words_host(ctx, data, avail, dst, have, &used), "PackedInputStream");
-        inner_.skip(used - before);
-        return have * 8;
-      }
-      fail(CPK_ERR_PREMATURE_EOF, "PackedInputStream");
-    }
-    check(st, "PackedInputStream");
-    inner_.skip(used - before);
-    return maxBytes;
-  }
+  return 8 * readWords(static_cast<uint64_t*>(buffer), minBytes / 8, maxBytes / 8);
 }
 
 void _::PackedInputStream::skip(size_t bytes) {
-  // serialize-packed.c++:185-299: the same parse without a destination -- decoded into scratch
-  // in one piece, since a run may not cross `bytes` but may cross any smaller piece
+  // serialize-packed.c++:185-299: the same parse with nothing stored -- the device decodes into
+  // its own scratch and no word comes back to the host
   if (bytes == 0) return;
   if (bytes % 8 != 0) fail(CPK_ERR_INVALID_ARGUMENT, "PackedInputStream reads must be word-aligned.");
-  std::vector<uint64_t> scratch(bytes / 8);
-  if (tryRead(scratch.data(), bytes, bytes) < bytes) fail(CPK_ERR_PREMATURE_EOF, "PackedInputStream");
+  if (readWords(nullptr, bytes / 8, bytes / 8) < bytes / 8)
+    fail(CPK_ERR_PREMATURE_EOF, "PackedInputStream");
 }
 
 PackedMessageReader::PackedMessageReader(BufferedInputStream& in, ReaderOptions options,
                                          ArrayPtr<word> scratch)
-    : options_(options) {
-  cpk_ctx* ctx = threadContext();
-  cpk_limits lim;
-  lim.traversal_limit_words = options.traversalLimitInWords;
-  std::vector<byte> acc;  // bytes already taken from the stream (the message spans buffers)
-  word* dst = scratch.begin();
-  size_t cap = scratch.size();
-  for (;;) {
-    ArrayPtr<const byte> buf = in.tryGetReadBuffer();
-    const byte* data = buf.begin();
-    size_t avail = buf.size();
-    if (!acc.empty()) {
-      acc.insert(acc.end(), buf.begin(), buf.end());
-      data = acc.data();
-      avail = acc.size();
-    }
-    if (avail == 0) fail(CPK_ERR_PREMATURE_EOF, "PackedMessageReader");
-    uint64_t nwords = 0, used = 0;
-    cpk_status st = cpk_read_packed_message_host(ctx, data, avail,
-                                                 reinterpret_cast<uint64_t*>(dst), cap, &nwords,
-                                                 &used, &lim);
-    if (st == CPK_ERR_CAPACITY) {
-      // serialize.c++:244-249: scratch too small -> the reader owns the space
-      owned_.resize(nwords);
-      dst = owned_.data();
-      cap = nwords;
-      st = cpk_read_packed_message_host(ctx, data, avail, reinterpret_cast<uint64_t*>(dst), cap,
-                                        &nwords, &used, &lim);
-    }
-    if (st == CPK_ERR_PREMATURE_EOF && buf.size() > 0) {
-      // the message continues past what is buffered: take these bytes and refill
-      if (acc.empty()) acc.assign(buf.begin(), buf.end());
-      in.skip(buf.size());
-      continue;
-    }
-    check(st, "PackedMessageReader");
-    // leave the stream right after the message
-    const size_t before = acc.empty() ? 0 : acc.size() - buf.size();
-    in.skip(used - before);
-    flat_ = ArrayPtr<const word>(dst, nwords);
-    break;
+    : _::PackedInputStream(in), options_(options) {
+  // serialize.c++:202-270
+  uint32_t first[2];
+  InputStream::read(first, 8);
+  uint32_t segmentCount = first[0] + 1;
+  const uint32_t segment0Size = first[1];
+  size_t totalWords = segment0Size;
+  if (first[0] >= 511) fail(CPK_ERR_TOO_MANY_SEGMENTS, "PackedMessageReader");  // :217
+  std::vector<uint32_t> moreSizes(segmentCount & ~1u);
+  if (segmentCount > 1) {
+    InputStream::read(moreSizes.data(), moreSizes.size() * 4);
+    for (uint32_t i = 0; i < segmentCount - 1; i++) totalWords += moreSizes[i];
   }
-  // segments from the table (serialize.c++:210-260)
-  const uint32_t* t = reinterpret_cast<const uint32_t*>(flat_.begin());
-  const uint32_t nseg = t[0] + 1;
-  size_t at = nseg / 2 + 1;
-  for (uint32_t i = 0; i < nseg; i++) {
-    const size_t n = t[i + 1];
-    segments_.push_back(ArrayPtr<const word>(flat_.begin() + at, n));
-    at += n;
+  if (totalWords > options.traversalLimitInWords)  // :235
+    fail(CPK_ERR_MESSAGE_TOO_LARGE, "PackedMessageReader");
+  if (scratch.size() < totalWords) {
+    owned_.resize(totalWords);
+    scratch = ArrayPtr<word>(owned_.data(), owned_.size());
+  }
+  segment0_ = ArrayPtr<const word>(scratch.begin(), segment0Size);
+  size_t offset = segment0Size;
+  for (uint32_t i = 0; i + 1 < segmentCount; i++) {
+    moreSegments_.push_back(ArrayPtr<const word>(scratch.begin() + offset, moreSizes[i]));
+    offset += moreSizes[i];
+  }
+  if (segmentCount == 1) {
+    InputStream::read(scratch.begin(), totalWords * 8);
+  } else {
+    readPos_ = reinterpret_cast<byte*>(scratch.begin());
+    readPos_ += InputStream::read(readPos_, segment0Size * 8, totalWords * 8);
   }
 }
 
-ArrayPtr<const word> PackedMessageReader::getSegment(unsigned id) const {
-  if (id >= segments_.size()) return nullptr;
-  return segments_[id];
+PackedMessageReader::~PackedMessageReader() noexcept(false) {
+  // serialize.c++:272-281: leave the stream after the message
+  if (readPos_ == nullptr) return;
+  const byte* allEnd = reinterpret_cast<const byte*>(moreSegments_.back().end());
+  if (std::uncaught_exceptions() > 0) {
+    try {
+      skip((size_t)(allEnd - readPos_));
+    } catch (...) {
+    }
+  } else {
+    skip((size_t)(allEnd - readPos_));
+  }
+}
+
+ArrayPtr<const word> PackedMessageReader::getSegment(unsigned id) {
+  // serialize.c++:283-302
+  if (id > moreSegments_.size()) return nullptr;
+  ArrayPtr<const word> segment = id == 0 ? segment0_ : moreSegments_[id - 1];
+  if (readPos_ != nullptr) {
+    const byte* segmentEnd = reinterpret_cast<const byte*>(segment.end());
+    if (readPos_ < segmentEnd) {
+      const byte* allEnd = reinterpret_cast<const byte*>(moreSegments_.back().end());
+      readPos_ += InputStream::read(readPos_, (size_t)(segmentEnd - readPos_),
+                                    (size_t)(allEnd - readPos_));
+    }
+  }
+  return segment;
 }
 
 PackedFdMessageReader::PackedFdMessageReader(int fd, ReaderOptions options,
                                              ArrayPtr<word> scratchSpace)
     : FdBufferedInputStream(fd),
+      PackedMessageReader(static_cast<FdBufferedInputStream&>(*this), options, scratchSpace) {}
+
+PackedFdMessageReader::PackedFdMessageReader(OwnFd fd, ReaderOptions options,
+                                             ArrayPtr<word> scratchSpace)
+    : FdBufferedInputStream(std::move(fd)),
       PackedMessageReader(static_cast<FdBufferedInputStream&>(*this), options, scratchSpace) {}
 
 size_t computeUnpackedSizeInWords(ArrayPtr<const byte> packedBytes) {

@@ -68,6 +68,7 @@ struct UnpackArgs {
   int32_t* status;
   uint64_t* size_out;           // mode 2
   uint64_t* in_end;             // optional: packed byte where each message actually ends
+  uint64_t* rec_pos;            // optional: packed byte of the record whose head is word i
   uint32_t mode;                // 0 messages, 1 exact-size chunks (flat-packed), 2 size only
   uint64_t ntiles;
   uint32_t* tile_counter;
@@ -114,6 +115,16 @@ hipError_t launch_unpack_header(const uint8_t* packed, const uint64_t* in_off, u
 hipError_t launch_unpack_stage(int stage, const UnpackArgs& a, hipStream_t stream);
 hipError_t launch_unpack_init(uint32_t mode, const uint64_t* in_off, const uint64_t* word_off,
                               uint64_t n, int32_t* status, uint64_t* size_out, hipStream_t stream);
+
+// Stream boundary discovery (cpk_stream.hip).  meta (device, 4 u64): [0] packed byte and [1]
+// word where the flat decode of the stream stopped, [2] its cpk_status; the walk follows the
+// segment tables from word 0 over the decoded words.
+hipError_t launch_set_u64x4(uint64_t* dst, uint64_t v0, uint64_t v1, uint64_t v2, uint64_t v3,
+                            hipStream_t stream);
+hipError_t launch_split_walk(const uint8_t* packed, uint64_t nbytes, const uint64_t* words,
+                             const uint64_t* rec_pos, const uint64_t* meta, uint64_t max_msgs,
+                             uint64_t limit, uint64_t* msg_word_off, uint64_t* msg_in_off,
+                             int32_t* status, uint64_t* nmsgs, hipStream_t stream);
 
 hipError_t launch_gen(int profile, uint64_t seed, uint64_t first_msg, uint64_t stride,
                       uint64_t nmsgs,

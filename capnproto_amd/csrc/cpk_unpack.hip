@@ -314,7 +314,20 @@ struct RunJob {
   uint32_t n;
   bool raw;
   uint64_t end;  // absolute packed byte after this record (terminal records: message end)
+  uint64_t bw;   // words of the message decoded at `end`
 };
+
+// The terminal record of message m: its end (stream readers), and, for the prefix reads of
+// PackedInputStream (size_out given in mode 1), where a failing read stops too -- the start of
+// the record that ends the input early or overshoots -- with the words decoded up to there.
+__device__ __forceinline__ void report_end(const UnpackArgs& a, uint64_t m, int32_t st,
+                                           const RunJob& job) {
+  if (!a.in_end) return;
+  const bool prefix = a.mode == 1 && a.size_out;
+  if (st == kOK || st == kTrailing || st == kCap || (prefix && (st == kEOF || st == kOvershoot)))
+    a.in_end[m] = job.end;
+  if (prefix) a.size_out[m] = job.bw;
+}
 
 __device__ __forceinline__ int32_t handle_record(const UnpackArgs& a, const uint8_t* d, int p,
                                                  uint64_t pabs, uint64_t wb, const MsgInfo& mi,
@@ -362,13 +375,19 @@ __device__ __forceinline__ int32_t handle_record(const UnpackArgs& a, const uint
     }
   }
   job->end = end;
+  job->bw = wb + 1 + cnt;
   if (st < 0) {
     if (wb + 1 + cnt == mi.total) st = end < mend ? kTrailing : kOK;
     else if (end >= mend) st = kEOF;
   }
+  if (trunc1 || trunc2 || trunc3 || over) {  // the read stops before this record
+    job->end = pabs;
+    job->bw = wb;
+  }
   if (st == kOK && !mi.fits) st = kCap;
   if (mi.fits && !trunc1) {
     a.words[mi.base + wb] = word;
+    if (a.rec_pos) a.rec_pos[mi.base + wb] = pabs;
     uint64_t n = cnt;
     if (over) n = mi.total - wb - 1;
     if (trunc3) {
@@ -1213,7 +1232,7 @@ __device__ __forceinline__ void expand_tile(const UnpackArgs& a, uint64_t t, con
           }
         } else if (st >= 0) {
           a.status[m] = st;
-          if (a.in_end && (st == kOK || st == kTrailing || st == kCap)) a.in_end[m] = job.end;
+          report_end(a, (uint64_t)m, st, job);
         }
       }
       run_jobs(a, job);
@@ -1304,6 +1323,7 @@ __device__ __forceinline__ void expand_tile(const UnpackArgs& a, uint64_t t, con
         if (act && !special) {
           uint64_t* const wp = a.words + (cbase + sb);
           wp[o] = word;
+          if (a.rec_pos) a.rec_pos[cbase + sb + o] = A + (uint32_t)p;
           if (cnt) {
             job.n = cnt;
             job.dst = cbase + sb + o + 1;
@@ -1324,6 +1344,7 @@ __device__ __forceinline__ void expand_tile(const UnpackArgs& a, uint64_t t, con
         special = act && (wb + w >= mtotal || A + p + len >= mend);
         if (act && !special) {
           a.words[mbase + wb] = word;
+          if (a.rec_pos) a.rec_pos[mbase + wb] = A + (uint32_t)p;
           if (cnt) {
             job.n = cnt;
             job.dst = mbase + wb + 1;
@@ -1344,7 +1365,7 @@ __device__ __forceinline__ void expand_tile(const UnpackArgs& a, uint64_t t, con
         const int32_t st = handle_record(a, d, p, pabs, wb, mi, &job, word);
         if (st >= 0) {
           a.status[m] = st;
-          if (a.in_end && (st == kOK || st == kTrailing || st == kCap)) a.in_end[m] = job.end;
+          report_end(a, (uint64_t)m, st, job);
         }
       }
       run_jobs(a, job);
@@ -1446,7 +1467,7 @@ __global__ __launch_bounds__(64) void fallback_kernel(UnpackArgs a) {
             const int32_t s = handle_record(a, d, p, pos + p, w0, mi, &job, word);
             if (s >= 0) {
               a.status[m] = s;
-              if (a.in_end && (s == kOK || s == kTrailing || s == kCap)) a.in_end[m] = job.end;
+              report_end(a, m, s, job);
               done = true;
             }
           }

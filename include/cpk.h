@@ -134,6 +134,28 @@ cpk_status cpk_unpack_messages(cpk_ctx* ctx, const uint8_t* d_packed, uint64_t t
                                uint64_t* d_msg_word_off, int32_t* d_status,
                                const cpk_limits* limits, void* stream);
 
+/* f1: stream boundary discovery.  d_packed[0, nbytes) holds packed
+ * messages back to back with unknown boundaries -- a file or socket buffer written by repeated
+ * writePackedMessage, read back by constructing one PackedMessageReader after another on the
+ * same stream (serialize-packed-test.c++:348-371).  The device decodes the stream into d_words
+ * (the flat messages back to back: table + segments each) and finds every message from the
+ * segment tables (serialize.c++:202-242), checking each the way that reader would.
+ * Outputs, all device, written asynchronously on `stream`:
+ *   *d_nmsgs                       n = messages read cleanly (at most max_msgs);
+ *   d_msg_word_off[0..n]           word offsets in d_words ([n] = end of message n-1);
+ *   d_msg_in_off[0..n]             packed byte offsets ([n] = bytes the n messages used);
+ *   d_status[0..n]                 CPK_OK for each message; [n] = why reading stopped: CPK_OK
+ *                                  (the input ended cleanly, or max_msgs), else the reference's
+ *                                  failure for the next message (PREMATURE_EOF, RUN_OVERSHOOT,
+ *                                  TOO_MANY_SEGMENTS, MESSAGE_TOO_LARGE) or CPK_ERR_CAPACITY
+ *                                  when it does not fit words_capacity.
+ * The three arrays need max_msgs + 1 entries.  limits may be NULL (reference defaults). */
+cpk_status cpk_split_packed_stream(cpk_ctx* ctx, const uint8_t* d_packed, uint64_t nbytes,
+                                   uint64_t* d_words, uint64_t words_capacity, uint64_t max_msgs,
+                                   uint64_t* d_msg_word_off, uint64_t* d_msg_in_off,
+                                   int32_t* d_status, uint64_t* d_nmsgs, const cpk_limits* limits,
+                                   void* stream);
+
 /* a4: computeUnpackedSizeInWords (serialize-packed.c++:482-508) for n independent buffers
  * d_packed[in_off[i] .. in_off[i+1]).  d_words_out[i] = total words; d_status[i] = CPK_OK or
  * CPK_ERR_INVALID_PACKED (then d_words_out[i] = 0). */
@@ -199,6 +221,17 @@ cpk_status cpk_pack_chunks_host(cpk_ctx* ctx, const uint64_t* h_words, uint64_t 
  * input did not end cleanly on a segment boundary."). */
 cpk_status cpk_unpack_words_host(cpk_ctx* ctx, const uint8_t* h_packed, uint64_t avail_bytes,
                                  uint64_t* h_words, uint64_t nwords, uint64_t* consumed_out);
+/* The device step of PackedInputStream::tryRead / skip (serialize-packed.c++:34-183, :185-299)
+ * over whatever one stream buffer holds: decodes whole records from the front of
+ * h_packed[0, avail_bytes) until max_words words are out (CPK_OK), a zero or raw run would cross
+ * max_words (CPK_ERR_RUN_OVERSHOOT), or the buffer ends first (CPK_ERR_PREMATURE_EOF).  In all
+ * three cases *consumed_out / *words_out are the record boundary where the read stopped -- for
+ * the two failures the start of the record that did not fit -- and the words decoded before it,
+ * which land in h_words (h_words may be NULL: a skip, nothing is copied back).  The stream
+ * caller keeps the unconsumed bytes in front of the next buffer and calls again. */
+cpk_status cpk_unpack_prefix_host(cpk_ctx* ctx, const uint8_t* h_packed, uint64_t avail_bytes,
+                                  uint64_t* h_words, uint64_t max_words, uint64_t* words_out,
+                                  uint64_t* consumed_out);
 /* computeUnpackedSizeInWords (serialize-packed.c++:482-508) of one host buffer. */
 cpk_status cpk_unpacked_size_host(cpk_ctx* ctx, const uint8_t* h_packed, uint64_t nbytes,
                                   uint64_t* words_out);

@@ -82,10 +82,11 @@ class BufferedOutputStream : public OutputStream {
 
 class InputStream {
  public:
-  virtual ~InputStream() = default;
+  virtual ~InputStream() noexcept(false) = default;  // kj/io.h: readers may throw on close
   virtual size_t tryRead(void* buffer, size_t minBytes, size_t maxBytes) = 0;
-  // kj/io.c++:53: "Premature EOF" when fewer than `bytes` arrive.
-  void read(void* buffer, size_t bytes);
+  // kj/io.c++:53: "Premature EOF" when fewer than minBytes arrive; returns the bytes read.
+  size_t read(void* buffer, size_t minBytes, size_t maxBytes);
+  void read(void* buffer, size_t bytes) { read(buffer, bytes, bytes); }
   virtual void skip(size_t bytes);
 };
 
@@ -139,14 +140,37 @@ class ArrayInputStream : public BufferedInputStream {
 
 // File descriptors (kj::FdInputStream / FdOutputStream + the buffered wrappers of kj/io.c++:
 // 145-239), used by PackedFdMessageReader / writePackedMessageToFd.
+// kj::OwnFd (kj/io.h): a file descriptor closed when the owner goes away.  Move-only.
+class OwnFd {
+ public:
+  OwnFd() : fd_(-1) {}
+  explicit OwnFd(int fd) : fd_(fd) {}
+  OwnFd(OwnFd&& o) noexcept : fd_(o.fd_) { o.fd_ = -1; }
+  OwnFd& operator=(OwnFd&& o) noexcept;
+  OwnFd(const OwnFd&) = delete;
+  OwnFd& operator=(const OwnFd&) = delete;
+  ~OwnFd();
+  int get() const { return fd_; }
+  int release() {
+    const int f = fd_;
+    fd_ = -1;
+    return f;
+  }
+
+ private:
+  int fd_;
+};
+
 class FdBufferedInputStream : public BufferedInputStream {
  public:
   explicit FdBufferedInputStream(int fd, size_t bufferSize = 65536);
+  explicit FdBufferedInputStream(OwnFd fd, size_t bufferSize = 65536);
   ArrayPtr<const byte> tryGetReadBuffer() override;
   size_t tryRead(void* buffer, size_t minBytes, size_t maxBytes) override;
   void skip(size_t bytes) override;
 
  private:
+  OwnFd owned_;
   int fd_;
   std::vector<byte> buf_;
   size_t begin_ = 0, end_ = 0;
@@ -188,11 +212,14 @@ class PackedOutputStream : public OutputStream {
 };
 
 // serialize-packed.h:37-47 (serialize-packed.c++:34-299).  Decodes packed input from `inner`
-// on the device, a whole number of records per call: tryRead fills up to maxBytes (whole words),
-// returning early only when the input ends at a record boundary with at least minBytes out;
-// "Premature end of packed input." when it ends before minBytes or inside a record; "Packed
-// input did not end cleanly on a segment boundary." when a run crosses maxBytes.  skip(bytes)
-// consumes exactly `bytes` unpacked bytes with the same checks.
+// on the device, whole records per call, with the reference's stopping rules: tryRead fills
+// up to maxBytes (whole words) and returns early only at a record boundary that leaves fewer
+// than 10 bytes in the current stream buffer once minBytes are out (:71-76) -- so it never
+// blocks for input it does not need; "Premature end of packed input." when the input ends
+// before minBytes or inside a record; "Packed input did not end cleanly on a segment boundary."
+// when a run crosses maxBytes.  skip(bytes) consumes exactly `bytes` unpacked bytes with the
+// same checks and copies nothing back from the device.  Each stream buffer is sent to the
+// device once (plus the few bytes of a record it cuts), so a read is O(bytes).
 class PackedInputStream : public InputStream {
  public:
   explicit PackedInputStream(BufferedInputStream& inner) : inner_(inner) {}
@@ -203,36 +230,45 @@ class PackedInputStream : public InputStream {
   void skip(size_t bytes) override;
 
  private:
+  // minWords..maxWords words into dst (NULL: decoded on the device and dropped); returns words
+  size_t readWords(uint64_t* dst, size_t minWords, size_t maxWords);
   BufferedInputStream& inner_;
 };
 
 }  // namespace _
 
-// serialize-packed.h:65-71 / serialize.h InputStreamMessageReader: reads one packed message
-// (segment table, then the segments) from the stream, leaving the stream positioned after it.
-class PackedMessageReader {
+// serialize-packed.h:65-71: a PackedInputStream read by InputStreamMessageReader
+// (serialize.c++:202-302).  The constructor reads the segment table and segment 0; later
+// segments are read lazily by getSegment (:283-302), and the destructor skips whatever was not
+// read so the stream is left right after the message (:272-281).  Segments go into
+// scratchSpace when it is large enough, else into space the reader owns (:244-249).
+class PackedMessageReader : private _::PackedInputStream {
  public:
   PackedMessageReader(BufferedInputStream& inputStream, ReaderOptions options = ReaderOptions(),
                       ArrayPtr<word> scratchSpace = nullptr);
-  virtual ~PackedMessageReader() = default;
-  size_t segmentCount() const { return segments_.size(); }
+  virtual ~PackedMessageReader() noexcept(false);
+  PackedMessageReader(const PackedMessageReader&) = delete;
+  PackedMessageReader& operator=(const PackedMessageReader&) = delete;
+  size_t segmentCount() const { return 1 + moreSegments_.size(); }
   // MessageReader::getSegment (message.h:100): null past the last segment.
-  ArrayPtr<const word> getSegment(unsigned id) const;
+  ArrayPtr<const word> getSegment(unsigned id);
   const ReaderOptions& getOptions() const { return options_; }
-  // The flat message (table + segments) the reader decoded, for callers that want it whole.
-  ArrayPtr<const word> getFlat() const { return flat_; }
 
  private:
   ReaderOptions options_;
   std::vector<word> owned_;
-  ArrayPtr<const word> flat_;
-  std::vector<ArrayPtr<const word>> segments_;
+  ArrayPtr<const word> segment0_;
+  std::vector<ArrayPtr<const word>> moreSegments_;
+  byte* readPos_ = nullptr;  // next byte of a lazily read multi-segment message
 };
 
-// serialize-packed.h:73-89: reads from a file descriptor.
+// serialize-packed.h:73-89: reads from a file descriptor (borrowed, or owned and closed with
+// the reader).
 class PackedFdMessageReader : private FdBufferedInputStream, public PackedMessageReader {
  public:
   PackedFdMessageReader(int fd, ReaderOptions options = ReaderOptions(),
+                        ArrayPtr<word> scratchSpace = nullptr);
+  PackedFdMessageReader(OwnFd fd, ReaderOptions options = ReaderOptions(),
                         ArrayPtr<word> scratchSpace = nullptr);
 };
 
@@ -241,6 +277,24 @@ void writePackedMessage(BufferedOutputStream& output,
                         ArrayPtr<const ArrayPtr<const word>> segments);
 void writePackedMessage(OutputStream& output, ArrayPtr<const ArrayPtr<const word>> segments);
 void writePackedMessageToFd(int fd, ArrayPtr<const ArrayPtr<const word>> segments);
+
+// serialize-packed.h:114-124: the MessageBuilder overloads -- any builder whose
+// getSegmentsForOutput() yields the segment list (arena.c++:300-329).
+template <typename Builder>
+auto writePackedMessage(BufferedOutputStream& output, Builder& builder)
+    -> decltype(builder.getSegmentsForOutput(), void()) {
+  writePackedMessage(output, builder.getSegmentsForOutput());
+}
+template <typename Builder>
+auto writePackedMessage(OutputStream& output, Builder& builder)
+    -> decltype(builder.getSegmentsForOutput(), void()) {
+  writePackedMessage(output, builder.getSegmentsForOutput());
+}
+template <typename Builder>
+auto writePackedMessageToFd(int fd, Builder& builder)
+    -> decltype(builder.getSegmentsForOutput(), void()) {
+  writePackedMessageToFd(fd, builder.getSegmentsForOutput());
+}
 
 // serialize-packed.h:107.
 size_t computeUnpackedSizeInWords(ArrayPtr<const byte> packedBytes);

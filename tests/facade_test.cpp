@@ -7,8 +7,11 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <fcntl.h>
+#include <signal.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <fstream>
 #include <iterator>
 #include <string>
@@ -121,6 +124,17 @@ static void fixtures(const std::string& dir, const char* unpacked_name, const ch
         "%s: computeUnpackedSizeInWords", packed_name);
 }
 
+// The reader's segments against a message's segments.
+static bool same_message(PackedMessageReader& r, const std::vector<ArrayPtr<const word>>& segs) {
+  if (r.segmentCount() != segs.size()) return false;
+  for (size_t i = 0; i < segs.size(); i++) {
+    auto s = r.getSegment((unsigned)i);
+    if (s.size() != segs[i].size() || memcmp(s.begin(), segs[i].begin(), 8 * s.size()) != 0)
+      return false;
+  }
+  return r.getSegment((unsigned)segs.size()).size() == 0;
+}
+
 // serialize-packed-test.c++:348-371: two messages back to back in one stream, the second read
 // after the first; also with a scratch space and through a file descriptor.
 static void two_messages(const std::string& dir) {
@@ -134,18 +148,33 @@ static void two_messages(const std::string& dir) {
   {
     std::vector<word> scratch(8);
     PackedMessageReader r1(in, ReaderOptions(), ArrayPtr<word>(scratch.data(), scratch.size()));
-    CHECK(r1.getFlat().size() * 8 == a.size() &&
-              memcmp(r1.getFlat().begin(), a.data(), a.size()) == 0,
-          "first message");
+    CHECK(same_message(r1, sa), "first message");
   }
   {
     PackedMessageReader r2(in);
-    CHECK(r2.getFlat().size() * 8 == b.size() &&
-              memcmp(r2.getFlat().begin(), b.data(), b.size()) == 0,
-          "second message");
-    CHECK(r2.segmentCount() == sb.size(), "second message segments");
+    CHECK(same_message(r2, sb), "second message");
   }
   CHECK(in.tryGetReadBuffer().size() == 0, "stream drained");
+
+  // lazy segments (serialize.c++:264-302): the multi-segment message first, only segment 0
+  // looked at -- the destructor skips the rest, so the next message reads cleanly
+  {
+    VectorOutputStream o2;
+    writePackedMessage(o2, ArrayPtr<const ArrayPtr<const word>>(sb.data(), sb.size()));
+    writePackedMessage(o2, ArrayPtr<const ArrayPtr<const word>>(sa.data(), sa.size()));
+    ArrayInputStream in2(o2.getArray());
+    {
+      std::vector<word> scratch(b.size() / 8);  // large enough: segments land in it
+      PackedMessageReader r1(in2, ReaderOptions(), ArrayPtr<word>(scratch.data(), scratch.size()));
+      auto s0 = r1.getSegment(0);
+      CHECK(s0.size() == sb[0].size() && memcmp(s0.begin(), sb[0].begin(), 8 * s0.size()) == 0 &&
+                (const void*)s0.begin() == (const void*)scratch.data(),
+            "lazy: segment 0 in the caller's scratch");
+    }
+    PackedMessageReader r2(in2);
+    CHECK(same_message(r2, sa), "lazy: next message after the destructor's skip");
+    CHECK(in2.tryGetReadBuffer().size() == 0, "lazy: stream drained");
+  }
 
   // through a pipe: the reader refills across small buffers
   int fds[2];
@@ -153,11 +182,21 @@ static void two_messages(const std::string& dir) {
     writePackedMessageToFd(fds[1], ArrayPtr<const ArrayPtr<const word>>(sb.data(), sb.size()));
     writePackedMessageToFd(fds[1], ArrayPtr<const ArrayPtr<const word>>(sa.data(), sa.size()));
     close(fds[1]);
-    PackedFdMessageReader f1(fds[0]);
-    CHECK(f1.getFlat().size() * 8 == b.size() &&
-              memcmp(f1.getFlat().begin(), b.data(), b.size()) == 0,
-          "fd: first message");
+    {
+      PackedFdMessageReader f1(fds[0]);
+      CHECK(same_message(f1, sb), "fd: first message");
+    }
     close(fds[0]);
+  }
+  // serialize-packed.h:82-83: the OwnFd overload closes the descriptor with the reader
+  if (pipe(fds) == 0) {
+    writePackedMessageToFd(fds[1], ArrayPtr<const ArrayPtr<const word>>(sa.data(), sa.size()));
+    close(fds[1]);
+    {
+      PackedFdMessageReader f2{OwnFd(fds[0])};
+      CHECK(same_message(f2, sa), "OwnFd: message");
+    }
+    CHECK(fcntl(fds[0], F_GETFD) == -1, "OwnFd: descriptor closed with the reader");
   }
 }
 
@@ -291,6 +330,178 @@ static void input_stream(const std::string& dir) {
   expect("0000", 16, 16, CPK_ERR_PREMATURE_EOF, 0, "input ends before minBytes");
 }
 
+// A stream that hands out fixed-size buffers (the buffer boundaries fall every `chunk` bytes
+// of the stream, like a buffered reader over a socket delivering that much at a time).
+class ChunkedInput : public BufferedInputStream {
+ public:
+  ChunkedInput(const std::vector<byte>& d, size_t chunk) : d_(d), chunk_(chunk) {}
+  ArrayPtr<const byte> tryGetReadBuffer() override {
+    const size_t end = std::min(d_.size(), (pos_ / chunk_ + 1) * chunk_);
+    return ArrayPtr<const byte>(d_.data() + pos_, end - pos_);
+  }
+  size_t tryRead(void* buffer, size_t minBytes, size_t maxBytes) override {
+    (void)minBytes;
+    const size_t n = std::min(maxBytes, d_.size() - pos_);
+    memcpy(buffer, d_.data() + pos_, n);
+    pos_ += n;
+    return n;
+  }
+  void skip(size_t bytes) override {
+    if (bytes > d_.size() - pos_) throw Exception(CPK_ERR_PREMATURE_EOF, "ChunkedInput::skip");
+    pos_ += bytes;
+  }
+  size_t pos() const { return pos_; }
+
+ private:
+  const std::vector<byte>& d_;
+  size_t chunk_, pos_ = 0;
+};
+
+// The reference's PackedInputStream::tryRead stopping rules (serialize-packed.c++:34-183),
+// restated over the same chunked stream as a model: returns the bytes produced and leaves
+// *pos where the reference leaves the stream; throws the reference's failure as a cpk_status.
+static size_t model_try_read(const std::vector<byte>& d, size_t chunk, size_t* pos, size_t minB,
+                             size_t maxB) {
+  auto chunk_end = [&](size_t p) { return std::min(d.size(), (p / chunk + 1) * chunk); };
+  size_t in = *pos, end = chunk_end(in), out = 0;
+  if (in == end) return 0;
+  auto refresh = [&]() {  // REFRESH_BUFFER
+    in = end;
+    end = chunk_end(in);
+    if (in == end) throw CPK_ERR_PREMATURE_EOF;
+  };
+  for (;;) {
+    unsigned tag;
+    if (end - in < 10) {
+      if (out >= minB) {
+        *pos = in;
+        return out;
+      }
+      if (end == in) {
+        refresh();
+        continue;
+      }
+      tag = d[in++];
+      for (int i = 0; i < 8; i++) {
+        if (tag & (1u << i)) {
+          if (in == end) refresh();
+          in++;
+        }
+        out++;
+      }
+      if (in == end && (tag == 0 || tag == 0xff)) refresh();
+    } else {
+      tag = d[in++];
+      in += __builtin_popcount(tag);
+      out += 8;
+    }
+    if (tag == 0 || tag == 0xff) {
+      const size_t run = 8 * (size_t)d[in++];
+      if (run > maxB - out) throw CPK_ERR_RUN_OVERSHOOT;
+      if (tag == 0 || end - in >= run) {
+        if (tag == 0xff) in += run;
+        out += run;
+      } else {
+        // the rest of the run is read straight from the stream, then a new buffer is required
+        const size_t rest = run - (end - in);
+        if (rest > d.size() - end) throw CPK_ERR_PREMATURE_EOF;
+        in = end + rest;
+        out += run;
+        if (out == maxB) {
+          *pos = in;
+          return maxB;
+        }
+        end = chunk_end(in);
+        if (in == end) throw CPK_ERR_PREMATURE_EOF;  // getReadBuffer() at the end of the stream
+        continue;
+      }
+    }
+    if (out == maxB) {
+      *pos = in;
+      return maxB;
+    }
+  }
+}
+
+// The façade's PackedInputStream against the model: same byte counts, same stream position,
+// same failures, for every buffer size and (min, max) shape, reading the stream to its end.
+static void stream_model(const std::string& dir) {
+  for (const char* name : {"packed", "segmented-packed"}) {
+    const std::vector<byte> packed = read_file(dir + "/" + name);
+    const std::vector<byte> msg = read_file(dir + (strcmp(name, "packed") ? "/segmented" : "/binary"));
+    for (size_t chunk : {1, 2, 7, 9, 10, 11, 16, 64, 100, 4096}) {
+      for (int shape = 0; shape < 5; shape++) {
+        ChunkedInput ci(packed, chunk);
+        _::PackedInputStream pin(ci);
+        size_t mpos = 0, done = 0;
+        bool ok = true;
+        for (int call = 0; call < 4096 && ok; call++) {
+          const size_t left = msg.size() - done;
+          size_t minB, maxB;
+          switch (shape) {
+            case 0: minB = maxB = left; break;                    // read()
+            case 1: minB = 8; maxB = left; break;                 // as much as is buffered
+            case 2: minB = 0; maxB = left; break;                 // whatever is at hand
+            case 3: minB = maxB = std::min<size_t>(left, 24); break;  // word triples
+            default: minB = 8; maxB = std::min<size_t>(left, 200); break;
+          }
+          if (maxB == 0) break;
+          int want = 0, got = 0;
+          size_t nm = 0, nf = 0;
+          try {
+            nm = model_try_read(packed, chunk, &mpos, minB, maxB);
+          } catch (cpk_status e) {
+            want = e;
+          }
+          std::vector<byte> buf(maxB);
+          try {
+            nf = pin.tryRead(buf.data(), minB, maxB);
+          } catch (const Exception& e) {
+            got = e.status();
+          }
+          ok = want == got && (want || (nm == nf && mpos == ci.pos() &&
+                                        memcmp(buf.data(), msg.data() + done, nf) == 0));
+          CHECK(ok, "%s chunk %zu shape %d call %d: model %zu B (err %d, pos %zu) vs facade %zu B (err %d, pos %zu)",
+                name, chunk, shape, call, nm, want, mpos, nf, got, ci.pos());
+          if (want || (nm == 0 && minB == 0 && mpos == packed.size())) break;
+          done += nf;
+          if (nf == 0 && minB == 0) break;
+        }
+      }
+    }
+  }
+  // PackedInputStream::skip over small buffers consumes exactly the skipped records
+  {
+    const std::vector<byte> packed = read_file(dir + "/packed"), msg = read_file(dir + "/binary");
+    ChunkedInput ci(packed, 7);
+    _::PackedInputStream pin(ci);
+    std::vector<byte> first(8);
+    pin.InputStream::read(first.data(), 8);
+    pin.skip(msg.size() - 8);
+    CHECK(ci.pos() == packed.size() && memcmp(first.data(), msg.data(), 8) == 0,
+          "skip over 7-byte buffers");
+  }
+  // tryRead(min < max) on a pipe whose writer stays open: returns what is there (:71-76)
+  // instead of waiting for bytes that may never come
+  int fds[2];
+  if (pipe(fds) == 0) {
+    const std::vector<byte> packed = read_file(dir + "/packed"), msg = read_file(dir + "/binary");
+    if (write(fds[1], packed.data(), packed.size()) != (ssize_t)packed.size()) g_fail++;
+    alarm(60);  // a hang fails the run instead of blocking it
+    FdBufferedInputStream fin(fds[0]);
+    _::PackedInputStream pin(fin);
+    std::vector<byte> buf(msg.size() + 4096);
+    const size_t n = pin.tryRead(buf.data(), 8, buf.size());
+    alarm(0);
+    size_t mpos = 0;
+    const size_t nm = model_try_read(packed, 65536, &mpos, 8, buf.size());
+    CHECK(n == nm && n >= 8 && memcmp(buf.data(), msg.data(), n) == 0,
+          "pipe left open: tryRead(8, %zu) returned %zu (model %zu)", buf.size(), n, nm);
+    close(fds[1]);
+    close(fds[0]);
+  }
+}
+
 // Config C1: samples/addressbook.c++ -- writeAddressBook packs with writePackedMessageToFd
 // (:75), printAddressBook reads with PackedFdMessageReader (:79).  tests/golden/addressbook.bin
 // is the sample's message, addressbook.packed the reference's bytes for it.
@@ -329,6 +540,7 @@ int main(int argc, char** argv) {
     two_messages(dir);
     errors(dir);
     input_stream(dir);
+    stream_model(dir);
     addressbook(dir);
   } catch (const Exception& e) {
     fprintf(stderr, "unexpected exception: %s\n", e.what());

@@ -1,0 +1,189 @@
+"""GPU parity for stream boundary discovery: cpk_split_packed_stream.
+
+Reference behaviour being matched: constructing one PackedMessageReader after another on the
+same packed stream (serialize-packed-test.c++:348-371; InputStreamMessageReader
+serialize.c++:202-302 over PackedInputStream serialize-packed.c++:34-183).  The expected split
+comes from the CPU oracle reading message after message from the front of the remaining bytes;
+words, word offsets, packed byte offsets and the reason reading stopped must all agree.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import cases
+import pyoracle as P
+from gpu_util import dev, host_u64
+
+pytestmark = pytest.mark.gpu
+G = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.fixture(scope="module")
+def codec():
+    import capnproto_amd
+
+    c = capnproto_amd.Codec(0)
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="module")
+def oracle():
+    return P.Oracle()
+
+
+def oracle_split(oracle, data: bytes, limit=P.DEFAULT_TRAVERSAL_LIMIT, max_msgs=1 << 30):
+    """The reference's reader loop: one message after another from the front of the stream."""
+    pos, woff, ioff, words = 0, [0], [0], []
+    stop = P.OK
+    while len(woff) - 1 < max_msgs:
+        if pos == len(data):
+            break
+        rest = data[pos:]
+        st, w, used = oracle.read_message(rest, limit, cap_words=300 + 8 * len(rest))
+        if st == P.CAPACITY:  # a highly compressed message: read it again with room for it
+            st, w, used = oracle.read_message(rest, limit, cap_words=300 + 130 * len(rest))
+        if st != P.OK:
+            stop = st
+            break
+        words.append(w)
+        pos += used
+        woff.append(woff[-1] + len(w))
+        ioff.append(pos)
+    flat = np.concatenate(words) if words else np.zeros(0, np.uint64)
+    return flat, np.array(woff), np.array(ioff), stop
+
+
+def gpu_split(codec, data: bytes, cap=None, max_msgs=None, limit=None):
+    arr = np.frombuffer(data, np.uint8).copy() if data else np.zeros(0, np.uint8)
+    if cap is None:
+        cap = 300 + 130 * len(data)
+    if max_msgs is None:
+        max_msgs = len(data) // 2 + 2
+    words, woff, ioff, st, n = codec.split_packed_stream(dev(codec, arr), cap, max_msgs,
+                                                         nbytes=len(data),
+                                                         traversal_limit_words=limit)
+    codec.sync()
+    n = int(n.item())
+    woff = woff[:n + 1].cpu().numpy()
+    return (host_u64(words)[:woff[-1]].copy(), woff, ioff[:n + 1].cpu().numpy(),
+            int(st[n].item()), st[:n].cpu().numpy())
+
+
+def check(codec, oracle, data, limit=P.DEFAULT_TRAVERSAL_LIMIT, max_msgs=None):
+    ew, ewoff, eioff, estop = oracle_split(oracle, data, limit,
+                                           max_msgs if max_msgs is not None else 1 << 30)
+    gw, gwoff, gioff, gstop, gst = gpu_split(codec, data, max_msgs=max_msgs, limit=limit)
+    assert len(gwoff) == len(ewoff), (len(gwoff) - 1, len(ewoff) - 1, gstop, estop)
+    assert (gst == P.OK).all()
+    assert gstop == estop, (gstop, estop)
+    assert (gwoff == ewoff).all()
+    assert (gioff == eioff).all()
+    assert gw.tobytes() == ew.tobytes()
+    return len(ewoff) - 1
+
+
+def test_two_messages_from_one_stream(codec, oracle):
+    """serialize-packed-test.c++:348-371 with the reference's own fixtures."""
+    rd = lambda n: open(os.path.join(G, n), "rb").read()  # noqa: E731
+    a, b = rd("packed"), rd("segmented-packed")
+    gw, woff, ioff, stop, _ = gpu_split(codec, a + b)
+    assert stop == P.OK and list(ioff) == [0, len(a), len(a) + len(b)]
+    assert gw.tobytes() == rd("binary") + rd("segmented")
+    assert list(woff) == [0, len(rd("binary")) // 8, (len(rd("binary")) + len(rd("segmented"))) // 8]
+    assert check(codec, oracle, b + a + a + b) == 4
+
+
+def test_empty_stream(codec, oracle):
+    gw, woff, ioff, stop, _ = gpu_split(codec, b"")
+    assert stop == P.OK and list(woff) == [0] and list(ioff) == [0]
+
+
+@pytest.mark.parametrize("profile", ["mixed", "bytes", "text"])
+def test_mixed_messages(codec, oracle, profile):
+    rng = np.random.default_rng(11 + len(profile))
+    msgs = []
+    for _ in range(300):
+        nseg = int(rng.integers(1, 12))
+        m = cases.flat_message(rng, nseg, rng.integers(0, 500, size=nseg), profile)
+        msgs.append(oracle.pack_flat(m)[0])
+    assert check(codec, oracle, b"".join(msgs)) == 300
+
+
+def test_uniform_stretches(codec, oracle):
+    """Same-size single-segment messages (the 64-per-step path), broken by other sizes, empty
+    segments and multi-segment messages."""
+    rng = np.random.default_rng(5)
+    msgs = []
+    for block in range(12):
+        size = int(rng.integers(0, 40)) if block % 3 else 0
+        for _ in range(int(rng.integers(1, 200))):
+            msgs.append(oracle.pack_flat(cases.flat_message(rng, 1, [size], "mixed"))[0])
+        nseg = int(rng.integers(1, 5))
+        msgs.append(oracle.pack_flat(cases.flat_message(rng, nseg, [size] * nseg, "bytes"))[0])
+    data = b"".join(msgs)
+    assert check(codec, oracle, data) == len(msgs)
+    assert check(codec, oracle, data, max_msgs=len(msgs) // 2) == len(msgs) // 2
+    assert check(codec, oracle, data, max_msgs=130) == 130
+
+
+def test_truncated_streams(codec, oracle):
+    rng = np.random.default_rng(8)
+    msgs = [oracle.pack_flat(cases.flat_message(rng, int(n), rng.integers(0, 60, size=int(n)),
+                                                p))[0]
+            for n, p in zip(rng.integers(1, 6, size=12), ["mixed", "text", "bytes"] * 4)]
+    data = b"".join(msgs)
+    cuts = sorted(set(int(c) for c in rng.integers(1, len(data), size=40)) |
+                  {1, 2, 9, 10, len(msgs[0]) - 1, len(msgs[0]) + 1, len(data) - 1})
+    for cut in cuts:
+        check(codec, oracle, data[:cut])
+
+
+def test_reader_failures(codec, oracle):
+    rng = np.random.default_rng(9)
+    good = [oracle.pack_flat(cases.flat_message(rng, 2, [5, 7], "mixed"))[0] for _ in range(3)]
+    # a header claiming 512 segments (serialize.c++:217)
+    too_many = oracle.pack_chunk(np.array([511 | (1 << 32)], np.uint64))
+    check(codec, oracle, b"".join(good) + too_many + good[0])
+    # a message larger than the traversal limit (serialize.c++:235)
+    big = oracle.pack_flat(cases.flat_message(rng, 1, [300], "mixed"))[0]
+    check(codec, oracle, good[0] + big + good[1], limit=100)
+    # a zero run that crosses the end of a message: table (1 seg of 1 word), then 00 01 -- the
+    # run carries one word into what would be the next message (serialize-packed.c++:128-131)
+    cross = bytes([0x10, 0x01, 0x00, 0x01])
+    check(codec, oracle, good[0] + cross + good[1])
+    # a zero run crossing the first word of a message (its first read is 8 bytes)
+    check(codec, oracle, good[0] + bytes([0x00, 0x03]) + good[1])
+    # a raw run whose count crosses the message end while its bytes are cut off
+    raw = bytes([0x10, 0x01, 0xff, 1, 2, 3, 4, 5, 6, 7, 8, 0x05, 9, 9])
+    check(codec, oracle, good[1] + raw)
+
+
+def test_capacity(codec, oracle):
+    rng = np.random.default_rng(10)
+    msgs = [cases.flat_message(rng, 1, [100], "mixed") for _ in range(6)]
+    data = b"".join(oracle.pack_flat(m)[0] for m in msgs)
+    cap = 3 * len(msgs[0]) + 5
+    gw, woff, ioff, stop, _ = gpu_split(codec, data, cap=cap)
+    assert len(woff) == 4 and stop == P.CAPACITY
+    assert gw.tobytes() == np.concatenate(msgs[:3]).tobytes()
+
+
+def test_large_uniform_stream(codec, oracle):
+    """4096 x 64 KiB messages (config C2's shape) in one stream: offsets against the oracle's
+    packed lengths, words against the generator."""
+    import torch
+
+    n, seg = 4096, 8191
+    off, total = codec.gen_offsets(n, 1, seg, seed=7)
+    words = codec.gen_messages("flat", off, total, 1, seed=7)
+    packed, poff, st = codec.pack_messages(words, off)
+    codec.sync()
+    nbytes = int(poff[-1].item())
+    w2, woff, ioff, status, cnt = codec.split_packed_stream(packed, total + 16, n + 1,
+                                                            nbytes=nbytes)
+    codec.sync()
+    assert int(cnt.item()) == n and int(status[n].item()) == P.OK
+    assert torch.equal(woff[:n + 1], off) and torch.equal(ioff[:n + 1], poff)
+    assert torch.equal(w2[:total], words[:total])
