@@ -75,6 +75,7 @@ def load_library():
         "cpk_unpack_messages": (C.c_int, [vp, vp, u64, vp, u64, vp, u64, vp, vp, vp, vp]),
         "cpk_unpacked_size": (C.c_int, [vp, vp, u64, vp, u64, vp, vp, vp]),
         "cpk_unpack_chunks": (C.c_int, [vp, vp, u64, vp, vp, u64, vp, u64, vp, vp]),
+        "cpk_pack_segments": (C.c_int, [vp, vp, vp, u64, vp, u64, vp, vp]),
         "cpk_split_packed_stream": (C.c_int, [vp, vp, u64, vp, u64, u64, vp, vp, vp, vp, vp,
                                               vp]),
         "cpk_pack_messages_host": (C.c_int, [vp, vp, u64, vp, u64, vp, u64, vp, vp]),
@@ -181,6 +182,23 @@ class Codec:
                                              _ptr(out), out.numel(), _ptr(chunk_out_off),
                                              self._stream(stream)), "cpk_pack_chunks")
         return out, chunk_out_off
+
+    def pack_segments(self, segments, out=None, stream=None):
+        """writePackedMessage over a list of device segments (int64 tensors, any addresses):
+        no host gather (include/cpk.h cpk_pack_segments).  Returns (out, nbytes tensor)."""
+        torch = self.torch
+        n = len(segments)
+        ptrs = (C.c_uint64 * max(n, 1))(*[s.data_ptr() for s in segments])
+        sizes = (C.c_uint64 * max(n, 1))(*[s.numel() for s in segments])
+        total = n // 2 + 1 + sum(s.numel() for s in segments)
+        if out is None:
+            out = torch.empty(self.packed_bound(total, n + 1) + 16, dtype=torch.uint8,
+                              device=self.device)
+        nbytes = torch.zeros(1, dtype=torch.int64, device=self.device)
+        self._check(self.lib.cpk_pack_segments(self.ctx, ptrs, sizes, n, _ptr(out), out.numel(),
+                                               _ptr(nbytes), self._stream(stream)),
+                    "cpk_pack_segments")
+        return out, nbytes
 
     # ------------------------------------------------------------------ unpack
     def unpack_messages(self, packed, msg_in_off, words_capacity, nbytes=None, words=None,

@@ -28,6 +28,11 @@ struct cpk_ctx {
   bool timing = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[CPK_TIMERS];
   std::vector<hipEvent_t> pool;
+  // cpk_pack_segments: pinned host staging for the segment list, free again once `meta_ev`
+  // (recorded after its upload) has completed
+  void* pinned = nullptr;
+  size_t pinned_size = 0;
+  hipEvent_t meta_ev = nullptr;
   // diagnostics: the last pack call's per-tile tables (cpk_debug_pack_tables)
   uint64_t* dbg_tile_bytes = nullptr;
   uint8_t* dbg_step_b = nullptr;
@@ -454,6 +459,8 @@ cpk_status cpk_destroy(cpk_ctx* ctx) {
   for (hipEvent_t e : ctx->pool) (void)hipEventDestroy(e);
   for (int i = 0; i < 4; i++)
     if (ctx->stage[i]) (void)hipFree(ctx->stage[i]);
+  if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+  if (ctx->meta_ev) (void)hipEventDestroy(ctx->meta_ev);
   delete ctx;
   return CPK_OK;
 }
@@ -495,6 +502,64 @@ cpk_status cpk_pack_messages(cpk_ctx* ctx, const uint64_t* d_words, uint64_t tot
                              void* stream) {
   return pack_common(ctx, d_words, total_words, d_msg_word_off, nmsgs, true, d_out, out_capacity,
                      d_msg_out_off, d_status, (hipStream_t)stream);
+}
+
+cpk_status cpk_pack_segments(cpk_ctx* ctx, const uint64_t* const* h_seg_ptrs,
+                             const uint64_t* h_seg_words, uint64_t nseg, uint8_t* d_out,
+                             uint64_t out_capacity, uint64_t* d_out_bytes, void* stream) {
+  if (!ctx || (nseg && (!h_seg_ptrs || !h_seg_words)) || !d_out_bytes)
+    return CPK_ERR_INVALID_ARGUMENT;
+  if (nseg == 0) return CPK_ERR_EMPTY_MESSAGE;  // serialize.c++:333
+  if (nseg > (1u << 20)) return CPK_ERR_INVALID_ARGUMENT;
+  if (hipSetDevice(ctx->device) != hipSuccess) return CPK_ERR_HIP;
+  hipStream_t s = (hipStream_t)stream;
+  const uint64_t tw = nseg / 2 + 1;
+  // meta: seg_ptr[nseg], chunk_off[nseg + 2], table[tw]
+  const uint64_t nmeta = nseg + (nseg + 2) + tw;
+  std::vector<uint64_t> chunk_off(nseg + 2);
+  chunk_off[0] = 0;
+  chunk_off[1] = tw;
+  for (uint64_t i = 0; i < nseg; i++) {
+    if (h_seg_words[i] > 0xffffffffull || (h_seg_words[i] && !h_seg_ptrs[i]))
+      return CPK_ERR_INVALID_ARGUMENT;
+    chunk_off[i + 2] = chunk_off[i + 1] + h_seg_words[i];
+  }
+  const uint64_t total = chunk_off[nseg + 1];
+  cpk_status st;
+  // the previous call's upload must have left the pinned buffer before it is refilled
+  if (ctx->meta_ev && hipEventSynchronize(ctx->meta_ev) != hipSuccess) return CPK_ERR_HIP;
+  if (ctx->pinned_size < nmeta * 8) {
+    if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+    ctx->pinned = nullptr;
+    ctx->pinned_size = 0;
+    if (hipHostMalloc(&ctx->pinned, nmeta * 8 + 4096, 0) != hipSuccess) return CPK_ERR_HIP;
+    ctx->pinned_size = nmeta * 8 + 4096;
+  }
+  if (!ctx->meta_ev && hipEventCreateWithFlags(&ctx->meta_ev, hipEventDisableTiming) != hipSuccess)
+    return CPK_ERR_HIP;
+  uint64_t* h = (uint64_t*)ctx->pinned;
+  for (uint64_t i = 0; i < nseg; i++) h[i] = (uint64_t)(uintptr_t)h_seg_ptrs[i];
+  memcpy(h + nseg, chunk_off.data(), (nseg + 2) * 8);
+  uint32_t* t32 = (uint32_t*)(h + nseg + nseg + 2);  // serializeSegmentTable, serialize.c++:311-330
+  memset(t32, 0, tw * 8);
+  t32[0] = (uint32_t)(nseg - 1);
+  for (uint64_t i = 0; i < nseg; i++) t32[i + 1] = (uint32_t)h_seg_words[i];
+  // device: meta, then the flat message, then the chunk output offsets
+  const size_t need = align16(nmeta * 8) + align16(total * 8) + (nseg + 2) * 8 + 64;
+  if ((st = ensure(&ctx->stage[3], &ctx->stage_size[3], need)) != CPK_OK) return st;
+  uint64_t* d_meta = (uint64_t*)ctx->stage[3];
+  uint64_t* d_flat = (uint64_t*)((char*)d_meta + align16(nmeta * 8));
+  uint64_t* d_chunk_out = (uint64_t*)((char*)d_flat + align16(total * 8));
+  if (hipMemcpyAsync(d_meta, h, nmeta * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipEventRecord(ctx->meta_ev, s) != hipSuccess)
+    return CPK_ERR_HIP;
+  if (cpk::launch_gather_segments(d_meta, (uint32_t)nseg, total, d_flat, s) != hipSuccess)
+    return CPK_ERR_HIP;
+  st = pack_common(ctx, d_flat, total, d_meta + nseg, nseg + 1, false, d_out, out_capacity,
+                   d_chunk_out, nullptr, s);
+  if (st != CPK_OK) return st;
+  return hip_status(hipMemcpyAsync(d_out_bytes, d_chunk_out + nseg + 1, 8,
+                                   hipMemcpyDeviceToDevice, s));
 }
 
 cpk_status cpk_pack_messages_host(cpk_ctx* ctx, const uint64_t* h_words, uint64_t total_words,

@@ -126,6 +126,9 @@ hipError_t launch_split_walk(const uint8_t* packed, uint64_t nbytes, const uint6
                              uint64_t limit, uint64_t* msg_word_off, uint64_t* msg_in_off,
                              int32_t* status, uint64_t* nmsgs, hipStream_t stream);
 
+hipError_t launch_gather_segments(const uint64_t* meta, uint32_t nseg, uint64_t total,
+                                  uint64_t* out, hipStream_t stream);
+
 hipError_t launch_gen(int profile, uint64_t seed, uint64_t first_msg, uint64_t stride,
                       uint64_t nmsgs,
                       uint32_t nseg, const uint64_t* off, uint64_t* words, hipStream_t stream);

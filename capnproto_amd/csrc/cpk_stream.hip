@@ -164,7 +164,43 @@ __global__ __launch_bounds__(64) void split_walk_kernel(Flat F, const uint64_t* 
   }
 }
 
+// ---- framing without a host gather ----------------------------------------------------------
+// writePackedMessage(getSegmentsForOutput()) with the segments where the builder keeps them
+// (serialize-packed.h:92-98, arena.c++:300-329): the segment table and every segment are copied
+// into one flat message in HBM (coalesced: each block takes 2048 consecutive output words and
+// finds its segment once), which the pack kernels then take as nseg + 1 chunks.
+// meta: seg_ptr[nseg], chunk_off[nseg + 2] (0, table words, then each segment's end), table[tw].
+__global__ __launch_bounds__(256) void gather_kernel(const uint64_t* __restrict__ meta,
+                                                     uint32_t nseg, uint64_t* __restrict__ out) {
+  const uint64_t* const* seg_ptr = reinterpret_cast<const uint64_t* const*>(meta);
+  const uint64_t* chunk_off = meta + nseg;
+  const uint64_t* table = chunk_off + nseg + 2;
+  const uint64_t tw = chunk_off[1], total = chunk_off[nseg + 1];
+  const uint64_t base = (uint64_t)blockIdx.x * 2048;
+  if (base >= total) return;
+  // the chunk holding the block's first word: last c with chunk_off[c] <= base
+  uint32_t lo = 0, hi = nseg + 1;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) / 2;
+    if (chunk_off[mid] <= base) lo = mid;
+    else hi = mid;
+  }
+  uint32_t c = lo;
+  for (uint64_t i = base + threadIdx.x; i < base + 2048 && i < total; i += 256) {
+    while (chunk_off[c + 1] <= i) c++;
+    out[i] = c == 0 ? table[i] : seg_ptr[c - 1][i - chunk_off[c]];
+  }
+  (void)tw;
+}
+
 }  // namespace
+
+hipError_t launch_gather_segments(const uint64_t* meta, uint32_t nseg, uint64_t total,
+                                  uint64_t* out, hipStream_t stream) {
+  if (total == 0) return hipSuccess;
+  gather_kernel<<<(unsigned)((total + 2047) / 2048), 256, 0, stream>>>(meta, nseg, out);
+  return hipGetLastError();
+}
 
 hipError_t launch_set_u64x4(uint64_t* dst, uint64_t v0, uint64_t v1, uint64_t v2, uint64_t v3,
                             hipStream_t stream) {

@@ -115,6 +115,19 @@ cpk_status cpk_pack_messages(cpk_ctx* ctx, const uint64_t* d_words, uint64_t tot
                              uint8_t* d_out, uint64_t out_capacity, uint64_t* d_msg_out_off,
                              int32_t* d_status, void* stream);
 
+/* a7 without a host gather: writePackedMessage(output, builder.getSegmentsForOutput())
+ * (serialize-packed.h:92-98, serialize-packed.c++:460-464) with the segments left where the
+ * message builder keeps them (BuilderArena::getSegmentsForOutput, arena.c++:300-329).
+ * h_seg_ptrs[i] is a DEVICE pointer to segment i and h_seg_words[i] its size in words (host
+ * arrays of nseg entries, read during the call).  The segment table (serialize.c++:311-330) and
+ * the segments are gathered into the context's device staging and packed as nseg + 1 chunks into
+ * d_out; *d_out_bytes (device u64) receives the packed size.  Asynchronous on `stream`; output
+ * capacity overflow is reported by cpk_sync.  nseg == 0 is CPK_ERR_EMPTY_MESSAGE
+ * (serialize.c++:333). */
+cpk_status cpk_pack_segments(cpk_ctx* ctx, const uint64_t* const* h_seg_ptrs,
+                             const uint64_t* h_seg_words, uint64_t nseg, uint8_t* d_out,
+                             uint64_t out_capacity, uint64_t* d_out_bytes, void* stream);
+
 /* ------------------------------------------------------------------------------------------
  * UNPACK (device-resident)
  *

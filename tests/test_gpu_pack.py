@@ -167,3 +167,31 @@ def test_capacity_error(codec):
     with pytest.raises(capnproto_amd.CpkError) as ei:
         codec.sync()
     assert ei.value.status == capnproto_amd.CAPACITY
+
+
+@pytest.mark.parametrize("profile", ["mixed", "bytes", "text"])
+def test_pack_segments_device_list(codec, oracle, profile):
+    """writePackedMessage(getSegmentsForOutput()) with every segment in its own device
+    allocation (cpk_pack_segments: no host gather) -- bytes equal the oracle's."""
+    import capnproto_amd
+
+    rng = np.random.default_rng(21 + len(profile))
+    for nseg in (1, 2, 3, 16, 130):
+        sizes = rng.integers(0, 2500, size=nseg)
+        sizes[rng.random(nseg) < 0.2] = 0
+        segs = [cases.random_words(rng, int(s), profile) for s in sizes]
+        tw = nseg // 2 + 1
+        table = np.zeros(2 * tw, "<u4")
+        table[0] = nseg - 1
+        table[1:nseg + 1] = sizes
+        flat = np.concatenate([table.view("<u8")] + [np.asarray(s, "<u8") for s in segs])
+        want, st = oracle.pack_flat(flat)
+        assert st == P.OK
+        dsegs = [dev(codec, s) for s in segs]
+        out, nb = codec.pack_segments(dsegs)
+        codec.sync()
+        n = int(nb.item())
+        assert host_u8(out[:n]).tobytes() == want, (nseg, n, len(want))
+    with pytest.raises(capnproto_amd.CpkError) as e:
+        codec.pack_segments([])
+    assert e.value.status == capnproto_amd.EMPTY_MESSAGE
