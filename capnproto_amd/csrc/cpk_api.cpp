@@ -50,8 +50,9 @@ unsigned long long* debug_stamps(int which) {
   static const bool on = getenv("CPK_STAMPS") && atoi(getenv("CPK_STAMPS")) != 0;
   if (!on) return nullptr;
   if (!bufs[which]) {
-    if (hipMalloc((void**)&bufs[which], 16 * 8) != hipSuccess) return nullptr;
-    if (hipMemset(bufs[which], 0, 16 * 8) != hipSuccess) return nullptr;
+    const size_t bytes = (size_t)cpk::kStampSlots * cpk::kStampRows * 8;
+    if (hipMalloc((void**)&bufs[which], bytes) != hipSuccess) return nullptr;
+    if (hipMemset(bufs[which], 0, bytes) != hipSuccess) return nullptr;
   }
   return bufs[which];
 }
@@ -123,6 +124,7 @@ struct PackScratch {
   uint32_t* counter;
   uint64_t* desc;
   uint64_t* gdesc;
+  uint64_t* hdesc;
   uint32_t* gcnt;
   uint32_t* state;
   uint64_t* bits;
@@ -143,6 +145,7 @@ PackScratch carve_pack(void* base, uint64_t N, uint64_t ntiles) {
   s.counter = c.take<uint32_t>(4);
   s.desc = c.take<uint64_t>(ntiles);
   s.gdesc = c.take<uint64_t>((ntiles + 63) / 64);
+  s.hdesc = c.take<uint64_t>((ntiles + 4095) / 4096);
   s.gcnt = c.take<uint32_t>((ntiles + 63) / 64);
   s.state = c.take<uint32_t>(ntiles);
   s.bits = c.take<uint64_t>((N + 63) / 64);
@@ -167,7 +170,8 @@ cpk_status pack_common(cpk_ctx* ctx, const uint64_t* d_words, uint64_t N, const 
                        uint64_t* d_out_off, int32_t* d_status, hipStream_t stream) {
   if (!ctx || (!d_off && n) || (!d_words && N) || (!d_out && cap)) return CPK_ERR_INVALID_ARGUMENT;
   if (hipSetDevice(ctx->device) != hipSuccess) return CPK_ERR_HIP;
-  const uint64_t T = 64ull * (cpk::pack_v2() ? cpk::pack2_steps() : cpk::pack_steps());
+  const bool v3 = cpk::pack_v3();
+  const uint64_t T = v3 ? 1024 : 64ull * (cpk::pack_v2() ? cpk::pack2_steps() : cpk::pack_steps());
   const uint64_t ntiles = (N + T - 1) / T;
   cpk_status st = ensure(&ctx->scratch, &ctx->scratch_size, pack_scratch_bytes(N, ntiles));
   if (st != CPK_OK) return st;
@@ -203,6 +207,7 @@ cpk_status pack_common(cpk_ctx* ctx, const uint64_t* d_words, uint64_t N, const 
   a.tile_counter = s.counter;
   a.desc = s.desc;
   a.gdesc = s.gdesc;
+  a.hdesc = s.hdesc;
   a.gcnt = s.gcnt;
   a.state = s.state;
   a.tile_b = s.tile_b;
@@ -217,9 +222,11 @@ cpk_status pack_common(cpk_ctx* ctx, const uint64_t* d_words, uint64_t N, const 
   a.stamps = cpk::debug_stamps(0);
   a.debug_skip = cpk::debug_skip();
   TimedLaunch tl(ctx, 0, stream);
-  if (cpk::pack_v2()) {
+  if (v3) {
+    e = cpk::launch_pack_tiles3(a, stream);
+  } else if (cpk::pack_v2()) {
     e = cpk::launch_pack_tiles2(a, stream);
-  } else if (cpk::pack_fused() || a.stamps) {
+  } else if (cpk::pack_fused() || a.stamps) {  // (stamps: single-pass kernel only)
     e = cpk::launch_pack_tiles(a, stream);
   } else {
     // count pass -> scan of tile byte counts -> emit pass
@@ -940,8 +947,13 @@ extern "C" cpk_status cpk_debug_stamps(int which, uint64_t* out16) {
   unsigned long long* b = cpk::debug_stamps(which);
   if (!b || !out16) return CPK_ERR_INVALID_ARGUMENT;
   if (hipDeviceSynchronize() != hipSuccess) return CPK_ERR_HIP;
-  if (hipMemcpy(out16, b, 16 * 8, hipMemcpyDeviceToHost) != hipSuccess) return CPK_ERR_HIP;
-  if (hipMemset(b, 0, 16 * 8) != hipSuccess) return CPK_ERR_HIP;
+  // rows of kStampSlots slots (spread by block), summed here
+  std::vector<uint64_t> rows((size_t)cpk::kStampSlots * cpk::kStampRows);
+  if (hipMemcpy(rows.data(), b, rows.size() * 8, hipMemcpyDeviceToHost) != hipSuccess)
+    return CPK_ERR_HIP;
+  for (int i = 0; i < 16; i++) out16[i] = 0;
+  for (size_t r = 0; r < rows.size(); r++) out16[r % cpk::kStampSlots] += rows[r];
+  if (hipMemset(b, 0, rows.size() * 8) != hipSuccess) return CPK_ERR_HIP;
   return CPK_OK;
 }
 

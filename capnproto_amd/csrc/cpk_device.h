@@ -10,6 +10,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "cpk_kernels.h"
+
 namespace cpk {
 
 constexpr int kWave = 64;
@@ -363,7 +365,6 @@ __device__ __forceinline__ void publish_incl(uint64_t* desc, uint64_t* gdesc, ui
 // Diagnostic phase stamps (env CPK_STAMPS=1 selects a separately instantiated kernel; the
 // production kernels contain no stamp).  Lane 0 adds per-phase s_memtime deltas into its own
 // debug buffer, never into outputs.
-constexpr int kStampSlots = 16;
 __device__ __forceinline__ uint64_t stamp_now() {
   // no s_waitcnt: a phase ends where the wave gets to, memory still in flight (forcing the wait
   // at every mark serialised the loads the phases are meant to overlap)
@@ -398,9 +399,10 @@ struct Stamps {
   }
   __device__ __forceinline__ void flush() {
     if constexpr (ON) {
+      unsigned long long* row = buf + kStampSlots * (blockIdx.x & (kStampRows - 1));
       if (lane_id() == 0 && buf)
-        for (int i = 0; i < kStampSlots - 1; i++)
-          if (acc[i]) atomicAdd(buf + i, (unsigned long long)acc[i]);
+        for (int i = 0; i < kStampSlots; i++)
+          if (acc[i]) atomicAdd(row + i, (unsigned long long)acc[i]);
     }
   }
 };

@@ -28,6 +28,7 @@ struct PackTileArgs {
   uint32_t* tile_counter;
   uint64_t* desc;              // ntiles look-back descriptors
   uint64_t* gdesc;             // per 64-tile group look-back descriptors
+  uint64_t* hdesc;             // per 64-group unit look-back descriptors (cpk_pack3.hip)
   uint32_t* gcnt;              // per group arrival tickets
   uint32_t* state;             // ntiles exit budgets (0x80000000 | budget)
   // two-pass form: count pass -> (entry budget, bytes) per tile; scan -> output offsets
@@ -47,6 +48,9 @@ hipError_t launch_pack_tiles(const PackTileArgs& a, hipStream_t stream);
 int pack2_steps();  // words per tile = 64 * pack2_steps()
 bool pack_v2();
 hipError_t launch_pack_tiles2(const PackTileArgs& a, hipStream_t stream);
+// lane-serial kernel (cpk_pack3.hip): 64 lanes x 16 consecutive words per tile
+bool pack_v3();
+hipError_t launch_pack_tiles3(const PackTileArgs& a, hipStream_t stream);
 hipError_t launch_pack_stage(int stage, const PackTileArgs& a, hipStream_t stream);
 hipError_t launch_message_bits(const uint64_t* words, const uint64_t* off, uint64_t n,
                                uint64_t* bits, int32_t* status, hipStream_t stream);
@@ -105,6 +109,11 @@ struct UnpackArgs {
 constexpr int kUnpackIndex = 0, kUnpackResolve = 1, kUnpackExpand = 2, kUnpackFallback = 3;
 
 uint32_t debug_skip();
+
+// Diagnostic stamp buffers: kStampRows rows of kStampSlots u64 (a block adds into row
+// blockIdx % kStampRows, so the atomics of the waves stay apart); cpk_debug_stamps sums rows.
+constexpr int kStampSlots = 16;
+constexpr int kStampRows = 256;
 
 // Diagnostic stamp buffers (env CPK_STAMPS=1): [0] pack, [1] unpack; kStampSlots u64 each.
 unsigned long long* debug_stamps(int which);

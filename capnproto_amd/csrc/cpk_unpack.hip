@@ -438,10 +438,12 @@ __device__ __forceinline__ void run_jobs(const UnpackArgs& a, const RunJob& job)
 enum : int { kDbgUnsettled = 0, kDbgTableMiss, kDbgWalkFail, kDbgWalks, kDbgFlagged,
              kDbgUmaskTiles, kDbgMergeSteps, kDbgSettleIters, kDbgWalkSteps, kDbgWalkStepsMax };
 __device__ __forceinline__ void dbg_count(const UnpackArgs& a, int slot) {
-  if (a.stamps) atomicAdd(a.stamps + slot, 1ull);
+  if (a.stamps) atomicAdd(a.stamps + kStampSlots * (blockIdx.x & (kStampRows - 1)) + slot, 1ull);
 }
 __device__ __forceinline__ void dbg_add(const UnpackArgs& a, int slot, uint64_t v) {
-  if (a.stamps && lane_id() == 0) atomicAdd(a.stamps + slot, (unsigned long long)v);
+  if (a.stamps && lane_id() == 0)
+    atomicAdd(a.stamps + kStampSlots * (blockIdx.x & (kStampRows - 1)) + slot,
+              (unsigned long long)v);
 }
 
 __device__ __forceinline__ void flag_message(const UnpackArgs& a, uint64_t m) {
@@ -636,6 +638,7 @@ __device__ __forceinline__ uint64_t make_dep(uint32_t tag) {
 }
 
 // 3. Index: one wave per tile, chain 0 + merge table (see the file comment).
+template <bool STAMPS>
 __global__ __launch_bounds__(256) void index_kernel(UnpackArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds_data[4][kB + kPad];
   __shared__ uint64_t lds_ms[4][64];  // message starts, then chain-0 masks (merge table)
@@ -643,6 +646,10 @@ __global__ __launch_bounds__(256) void index_kernel(UnpackArgs a) {
   const int wv = (int)uniform32(threadIdx.x >> 6);
   const uint64_t t = (uint64_t)blockIdx.x * 4 + wv;
   if (t >= a.ntiles) return;
+  Stamps<STAMPS> stm;
+  stm.start(a.stamps2);
+  uint64_t rt0 = 0;
+  if constexpr (STAMPS) rt0 = __builtin_amdgcn_s_memrealtime();
   uint8_t* d = lds_data[wv];
   uint64_t* lds_tm = lds_ms[wv];
   const uint64_t P = a.nbytes;
@@ -651,21 +658,26 @@ __global__ __launch_bounds__(256) void index_kernel(UnpackArgs a) {
   Staged stg;
   stage_load(a, A, stg);
   const uint64_t mfirst = uniform64(a.tile_first[t]);
+  stm.mark(0);
   stage_store(stg, d);
+  stm.mark(1);
   int nms_tile_after;
   (void)tile_msg_starts(a, A, mfirst, lds_ms[wv], &nms_tile_after, nullptr);
   const SubTile st = make_subtile(A, P, lds_ms[wv][l], nms_tile_after);
+  stm.mark(2);
 
   // ---- chain 0: speculative walks, then the lane fixed point for entry 0 --------------------
   uint64_t chain = 0, runm = 0;
   int sx = kDead;
   if (!(a.debug_skip & 4) && st.s < st.pend) sx = walk(d, st, st.s, 0, &chain, &runm);
+  stm.mark(3);
   int e = st.s;
   uint64_t tm = 0;
   int out = 0;
   int siters = 0;
   const bool settled =
       (a.debug_skip & 4) ? true : settle(d, st, chain, sx, 0, e, tm, out, runm, &siters);
+  stm.mark(4);
   if (a.stamps) {
     const uint32_t nrec = __popcll(chain);
     dbg_add(a, kDbgSettleIters, (uint64_t)siters);
@@ -710,6 +722,7 @@ __global__ __launch_bounds__(256) void index_kernel(UnpackArgs a) {
   a.t_wex[t * 64 + l] = Wex;
   lds_tm[l] = tm;
   lane_handoff();
+  stm.mark(5);
 
   // ---- merge table: lane e (1..15) walks the chain entered at byte e until it meets chain 0;
   //      a chain that never does (parity-locked or raw-run data) is walked to the tile end
@@ -767,6 +780,7 @@ __global__ __launch_bounds__(256) void index_kernel(UnpackArgs a) {
       delta = (int32_t)(ww - w0);
     }
   }
+  stm.mark(6);
   const uint32_t umask = (uint32_t)ballot(l >= 1 && l < kTab && !merged);
   if (a.stamps) {
     dbg_add(a, kDbgMergeSteps, readlane32(wave_incl_max32((uint32_t)msteps), 63));
@@ -780,6 +794,13 @@ __global__ __launch_bounds__(256) void index_kernel(UnpackArgs a) {
     a.t_wpost[t] = wpost;
     a.t_umask[t] = umask;
     a.t_flags[t] = (settled ? 0u : kTileUnsettled) | (tile_has_start ? kTileHasStart : 0u);
+  }
+  stm.mark(7);
+  if constexpr (STAMPS) {
+    stm.acc[13] = __builtin_amdgcn_s_memrealtime() - rt0;  // 100 MHz: calibrates the phases
+    stm.acc[14] = 1;
+    stm.acc[15] = 1;
+    stm.flush();
   }
 }
 
@@ -1527,7 +1548,10 @@ hipError_t launch_unpack_stage(int stage, const UnpackArgs& a, hipStream_t strea
   const unsigned wave_blocks = (unsigned)((a.ntiles + 3) / 4);
   switch (stage) {
     case kUnpackIndex:
-      hipLaunchKernelGGL(index_kernel, dim3(wave_blocks), dim3(256), 0, stream, a);
+      if (a.stamps2)
+        hipLaunchKernelGGL(index_kernel<true>, dim3(wave_blocks), dim3(256), 0, stream, a);
+      else
+        hipLaunchKernelGGL(index_kernel<false>, dim3(wave_blocks), dim3(256), 0, stream, a);
       break;
     case kUnpackResolve:
       hipLaunchKernelGGL(resolve1_kernel, dim3((unsigned)((a.ntiles + 255) / 256)), dim3(256), 0,

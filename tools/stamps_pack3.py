@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Diagnostic: per-phase cycles of unpack index_kernel (run with CPK_STAMPS=1)."""
+"""Diagnostic: per-phase cycles of the lane-serial pack kernel (CPK_PACK3=1 CPK_STAMPS=1)."""
 import ctypes as C
 import os
 import sys
@@ -15,23 +15,21 @@ L = codec.lib
 L.cpk_debug_stamps.argtypes = [C.c_int, C.POINTER(C.c_uint64)]
 off, total = codec.gen_offsets(n, nseg=nseg, seg_words=sw, seed=20261015)
 words = codec.gen_messages(prof, off, total, nseg=nseg, seed=20261015)
-packed, moff, st = codec.pack_messages(words, off)
-codec.sync()
-P = int(moff[-1].item())
 codec.timing(True)
 for rep in range(3):
     out = (C.c_uint64 * 16)()
-    L.cpk_debug_stamps(2, out)
+    L.cpk_debug_stamps(0, out)
     codec.timing_read_all()
-    codec.unpack_messages(packed, moff, total, nbytes=P)
+    packed, moff, st = codec.pack_messages(words, off)
     codec.sync()
-    L.cpk_debug_stamps(2, out)
+    L.cpk_debug_stamps(0, out)
     tm = codec.timing_read_all()
-print("index kernel ms (stamps build):", round(tm["unpack_index"][0], 4))
-print("wave lifetime us (s_memrealtime):", round(out[13] / max(out[15], 1) / 100, 2))
-names = ["stage issue", "stage wait+store", "msg starts", "walk", "settle", "word counts+stores", "merge table", "tables"]
+print(cfg, "pack kernel ms (stamps build):", round(tm["pack"][0], 4))
 tiles = out[15] or 1
-tot = sum(out[i] for i in range(8))
-print(cfg, "tiles", tiles, "cycles/tile", round(tot / tiles))
+print("wave lifetime us:", round(out[13] / tiles / 100, 2))
+names = ["loads issue", "classes(+load wait)", "look-ahead", "cover/entry", "entry wait",
+         "count+publish", "emission", "look-back", "flush", "positions"]
+tot = sum(out[i] for i in range(10))
+print("cycles/tile", round(tot / tiles))
 for i, nm in enumerate(names):
-    print(f"  {nm:20s} {out[i] / tiles:10.0f}  {100 * out[i] / max(tot, 1):5.1f}%")
+    print(f"  {nm:22s} {out[i] / tiles:10.0f}  {100 * out[i] / max(tot, 1):5.1f}%")
