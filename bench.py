@@ -70,6 +70,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=8.0,
                     help="CPU-baseline budget (bounded sample of the same workload)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-graph", action="store_true",
+                    help="time eager launches instead of the step captured as one HIP graph")
     ap.add_argument("--no-verify", action="store_true",
                     help="skip the manifest hash check (the device round trip is still checked)")
     ap.add_argument("--host-inclusive", action="store_true",
@@ -307,14 +309,31 @@ def run_config(name, args, steps, warmup, rank, world, dist, codec):
         codec.unpack_messages(packed, moff, total, nbytes=P, words=back, msg_word_off=woff,
                               status=ust)
 
+    # The timed step is one HIP graph (pack + unpack, every launch and scratch memset of the
+    # step), captured once and replayed: the same kernels on the same buffers, minus the host's
+    # per-launch submission gaps.  --no-graph times the eager launches instead.
+    run = step
+    graph = None
+    if not args.no_graph:
+        step()  # every lazily sized scratch buffer and launch setting exists before capture
+        codec.sync()
+        try:
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                step()
+            run = graph.replay
+        except Exception as e:  # noqa: BLE001 -- fall back to eager launches, say so
+            print(f"bench: graph capture failed ({e}); timing eager launches", file=sys.stderr)
+            graph = None
+            run = step
     for _ in range(warmup):
-        step()
+        run()
     codec.sync()
     torch.cuda.synchronize()
     barrier()
     t0 = time.perf_counter()
     for _ in range(steps):
-        step()
+        run()
     torch.cuda.synchronize()
     barrier()
     t1 = time.perf_counter()
@@ -322,13 +341,20 @@ def run_config(name, args, steps, warmup, rank, world, dist, codec):
     dt = t1 - t0
 
     # correctness of what was timed: exact round trip + statuses, then the reference's hashes
-    ok = bool((pst == 0).all().item() and (ust == 0).all().item() and torch.equal(woff, off)
-              and torch.equal(back[:total], words[:total]))
+    checks = {"pack_status": bool((pst == 0).all().item()),
+              "unpack_status": bool((ust == 0).all().item()),
+              "word_offsets": torch.equal(woff, off),
+              "words": torch.equal(back[:total], words[:total])}
+    ok = all(checks.values())
+    if not ok:
+        print(f"bench: {name}: round trip check failed: {checks}", file=sys.stderr)
     man = None if args.no_verify else manifest_entry(name, cfg, args.seed, first, stride, n)
     ref_ok = None
     if man is not None:
         ref_ok = (man["packed_bytes"] == P and sha_dev(packed[:P]) == man["sha256_packed"]
                   and sha_dev(moff) == man["sha256_out_off"])
+        if not ref_ok:
+            print(f"bench: {name}: packed bytes differ from the reference manifest", file=sys.stderr)
         ok = ok and ref_ok
 
     # per-kernel durations: a second pass of the same steps with HIP events around every tile
@@ -347,7 +373,7 @@ def run_config(name, args, steps, warmup, rank, world, dist, codec):
     res = {"name": name, "cfg": cfg, "n": n, "U": U, "P": P, "first": first, "stride": stride,
            "mode": mode, "dt_max": red["dt_max"], "U_all": red["unpacked_all"],
            "ok_all": red["ok_all"], "ref_checked": man is not None, "ref_ok": ref_ok,
-           "kms": kms, "steps": steps, "warmup": warmup}
+           "kms": kms, "steps": steps, "warmup": warmup, "graph": graph is not None}
     res["tensors"] = (words, off, packed, moff, total, cap)
     return res
 
@@ -394,6 +420,7 @@ def summarize(res, world, copy_gbps):
             "profile": cfg["profile"],
             "shard": res["mode"],
             "parallelism": f"dp{world} (independent message shards, no data-path collective)",
+            "launch": "hip graph (one per step)" if res.get("graph") else "eager",
         },
         "parity": ("bit-exact round trip; packed bytes SHA-256 == reference "
                    "(tests/golden/manifest.json)" if res["ref_checked"] else

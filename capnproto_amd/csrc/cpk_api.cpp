@@ -176,22 +176,25 @@ cpk_status pack_common(cpk_ctx* ctx, const uint64_t* d_words, uint64_t N, const 
   cpk_status st = ensure(&ctx->scratch, &ctx->scratch_size, pack_scratch_bytes(N, ntiles));
   if (st != CPK_OK) return st;
   PackScratch s = carve_pack(ctx->scratch, N, ntiles);
-  if (hipMemsetAsync(ctx->scratch, 0, s.zero_bytes, stream) != hipSuccess) return CPK_ERR_HIP;
+  if (cpk::launch_fill(ctx->scratch, s.zero_bytes, 0, stream) != hipSuccess) return CPK_ERR_HIP;
+  cpk::TileFirstJob tf;  // tile_first for the requested output positions, in the same launch
+  tf.pos = d_off;
+  tf.npos = n;
+  tf.ntiles = (d_out_off && n && N) ? ntiles : 0;
+  tf.T = T;
+  tf.out = s.tile_first;
   if (N == 0) {
-    if (d_out_off && hipMemsetAsync(d_out_off, 0, (n + 1) * 8, stream) != hipSuccess)
+    if (d_out_off && cpk::launch_fill(d_out_off, (n + 1) * 8, 0, stream) != hipSuccess)
       return CPK_ERR_HIP;
     if (messages && n)
-      return hip_status(cpk::launch_message_bits(d_words, d_off, n, s.bits, d_status, stream));
+      return hip_status(cpk::launch_message_bits(d_words, d_off, n, s.bits, d_status, tf, stream));
     return CPK_OK;
   }
   if (messages && n == 0) return CPK_ERR_INVALID_ARGUMENT;  // words outside any message
-  hipError_t e = messages ? cpk::launch_message_bits(d_words, d_off, n, s.bits, d_status, stream)
-                          : cpk::launch_chunk_bits(d_off, n, N, s.bits, stream);
+  hipError_t e = messages
+                     ? cpk::launch_message_bits(d_words, d_off, n, s.bits, d_status, tf, stream)
+                     : cpk::launch_chunk_bits(d_off, n, N, s.bits, tf, stream);
   if (e != hipSuccess) return CPK_ERR_HIP;
-  if (d_out_off && n) {
-    e = cpk::launch_tile_first(d_off, n, ntiles, T, s.tile_first, stream);
-    if (e != hipSuccess) return CPK_ERR_HIP;
-  }
   cpk::PackTileArgs a;
   a.words = d_words;
   a.nwords = N;
@@ -327,14 +330,20 @@ cpk_status unpack_common(cpk_ctx* ctx, uint32_t mode, const uint8_t* d_packed, u
   cpk_status st = ensure(&ctx->scratch, &ctx->scratch_size, probe.total + 64);
   if (st != CPK_OK) return st;
   UnpackScratch s = carve_unpack(ctx->scratch, ntiles, n);
-  if (hipMemsetAsync(ctx->scratch, 0, s.zero_bytes, stream) != hipSuccess) return CPK_ERR_HIP;
+  if (cpk::launch_fill(ctx->scratch, s.zero_bytes, 0, stream) != hipSuccess) return CPK_ERR_HIP;
   const uint64_t* word_off = d_word_off_in;
   hipError_t e = hipSuccess;
+  cpk::TileFirstJob tf;  // each tile's first message, in the same launch as the headers
+  tf.pos = d_in_off;
+  tf.npos = n;
+  tf.ntiles = ntiles;
+  tf.T = B;
+  tf.out = s.tile_first;
   if (mode == 0) {
     if (!d_word_off_out) return CPK_ERR_INVALID_ARGUMENT;
-    if (n == 0) return hip_status(hipMemsetAsync(d_word_off_out, 0, 8, stream));
+    if (n == 0) return hip_status(cpk::launch_fill(d_word_off_out, 8, 0, stream));
     e = cpk::launch_unpack_header(d_packed, d_in_off, n, limit, s.flat, s.hdr_status, d_status,
-                                  stream);
+                                  tf, stream);
     if (e != hipSuccess) return CPK_ERR_HIP;
     e = cpk::launch_exclusive_scan(s.flat, n, d_word_off_out, s.scan_counter, s.scan_desc,
                                    ctx->err, stream);
@@ -342,12 +351,10 @@ cpk_status unpack_common(cpk_ctx* ctx, uint32_t mode, const uint8_t* d_packed, u
     word_off = d_word_off_out;
   } else {
     if (n == 0) return CPK_OK;
-    e = cpk::launch_unpack_init(mode, d_in_off, word_off, n, d_status, d_size_out, stream);
+    e = cpk::launch_unpack_init(mode, d_in_off, word_off, n, d_status, d_size_out, tf, stream);
     if (e != hipSuccess) return CPK_ERR_HIP;
   }
   if (ntiles == 0) return CPK_OK;
-  e = cpk::launch_tile_first(d_in_off, n, ntiles, B, s.tile_first, stream);
-  if (e != hipSuccess) return CPK_ERR_HIP;
   cpk::UnpackArgs a;
   a.packed = d_packed;
   a.nbytes = P;
@@ -652,7 +659,7 @@ cpk_status cpk_split_packed_stream(cpk_ctx* ctx, const uint8_t* d_packed, uint64
   hipError_t e = cpk::launch_set_u64x4(state, 0, nbytes, 0, words_capacity, s);
   if (e == hipSuccess) e = cpk::launch_set_u64x4(meta, 0, 0, CPK_ERR_PREMATURE_EOF, 0, s);
   if (e == hipSuccess && words_capacity)
-    e = hipMemsetAsync(rec_pos, 0xff, words_capacity * 8, s);
+    e = cpk::launch_fill(rec_pos, words_capacity * 8, 0xff, s);
   if (e != hipSuccess) return CPK_ERR_HIP;
   if (nbytes) {
     // the whole stream as one flat chunk of up to words_capacity words, stopping at the first
@@ -876,7 +883,7 @@ cpk_status cpk_unpack_prefix_host(cpk_ctx* ctx, const uint8_t* h_packed, uint64_
   hipStream_t s = nullptr;
   if (hipMemcpyAsync(d_packed, h_packed, avail_bytes, hipMemcpyHostToDevice, s) != hipSuccess ||
       hipMemcpyAsync(d_in_off, offs, 32, hipMemcpyHostToDevice, s) != hipSuccess ||
-      hipMemsetAsync(d_in_end, 0, 16, s) != hipSuccess)
+      cpk::launch_fill(d_in_end, 16, 0, s) != hipSuccess)
     return CPK_ERR_HIP;
   // one exact-size chunk of max_words words (the flat-packed mode); with d_at given the
   // terminal record also reports where a short or overshooting read stops
@@ -1024,7 +1031,7 @@ cpk_status cpk_gen_offsets(cpk_ctx* ctx, uint64_t seed, uint64_t first_msg,
   uint64_t* desc = c.take<uint64_t>(nt);
   const size_t zero = c.off;
   uint64_t* sizes = c.take<uint64_t>(nmsgs + 1);
-  if (hipMemsetAsync(ctx->scratch, 0, zero, s) != hipSuccess) return CPK_ERR_HIP;
+  if (cpk::launch_fill(ctx->scratch, zero, 0, s) != hipSuccess) return CPK_ERR_HIP;
   if (cpk::launch_gen_sizes(seed, first_msg, msg_stride ? msg_stride : 1, nmsgs, nseg, seg_words, sizes, s) != hipSuccess)
     return CPK_ERR_HIP;
   if (cpk::launch_exclusive_scan(sizes, nmsgs, d_msg_word_off, counter, desc, ctx->err, s) !=

@@ -177,6 +177,27 @@ __device__ __forceinline__ uint32_t wait_nonzero32(const uint32_t* p, uint32_t* 
   return uniform32(v);
 }
 
+// Blocks past `first_block` of a prologue kernel compute tile_first (TileFirstJob, cpk_kernels.h):
+// binary search of each tile's start in the sorted positions.  True when this block did so.
+__device__ __forceinline__ bool run_tile_first(const TileFirstJob& tf, uint32_t first_block) {
+  if (blockIdx.x < first_block) return false;
+  const uint64_t t = (uint64_t)(blockIdx.x - first_block) * blockDim.x + threadIdx.x;
+  if (t < tf.ntiles) {
+    const uint64_t key = t * tf.T;
+    uint64_t lo = 0, hi = tf.npos + 1;
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (tf.pos[mid] < key) lo = mid + 1;
+      else hi = mid;
+    }
+    tf.out[t] = lo;
+  }
+  return true;
+}
+inline unsigned tile_first_blocks(const TileFirstJob& tf) {
+  return (unsigned)((tf.ntiles + 255) / 256);
+}
+
 // Decoupled look-back (exclusive prefix of tile aggregates) for tile `t` by one wave.
 // desc[i] = flags | value; AGG = this tile's own aggregate, INCL = inclusive prefix.
 // Segmented variant: when `seg_bit` is non-zero, a descriptor value carrying that bit marks a

@@ -52,12 +52,18 @@ hipError_t launch_pack_tiles2(const PackTileArgs& a, hipStream_t stream);
 bool pack_v3();
 hipError_t launch_pack_tiles3(const PackTileArgs& a, hipStream_t stream);
 hipError_t launch_pack_stage(int stage, const PackTileArgs& a, hipStream_t stream);
+// tile_first (first i with pos[i] >= tile start, per tile) as extra blocks of a prologue
+// kernel: one launch fewer per call.  ntiles == 0: no such job.
+struct TileFirstJob {
+  const uint64_t* pos;
+  uint64_t npos, ntiles, T;
+  uint64_t* out;
+};
 hipError_t launch_message_bits(const uint64_t* words, const uint64_t* off, uint64_t n,
-                               uint64_t* bits, int32_t* status, hipStream_t stream);
+                               uint64_t* bits, int32_t* status, const TileFirstJob& tf,
+                               hipStream_t stream);
 hipError_t launch_chunk_bits(const uint64_t* off, uint64_t n, uint64_t N, uint64_t* bits,
-                             hipStream_t stream);
-hipError_t launch_tile_first(const uint64_t* pos, uint64_t npos, uint64_t ntiles, uint64_t T,
-                             uint64_t* tile_first, hipStream_t stream);
+                             const TileFirstJob& tf, hipStream_t stream);
 
 struct UnpackArgs {
   const uint8_t* packed;        // batch of packed bytes
@@ -120,14 +126,17 @@ unsigned long long* debug_stamps(int which);
 
 hipError_t launch_unpack_header(const uint8_t* packed, const uint64_t* in_off, uint64_t n,
                                 uint64_t limit, uint64_t* flat, int32_t* hdr_status,
-                                int32_t* status, hipStream_t stream);
+                                int32_t* status, const TileFirstJob& tf, hipStream_t stream);
 hipError_t launch_unpack_stage(int stage, const UnpackArgs& a, hipStream_t stream);
 hipError_t launch_unpack_init(uint32_t mode, const uint64_t* in_off, const uint64_t* word_off,
-                              uint64_t n, int32_t* status, uint64_t* size_out, hipStream_t stream);
+                              uint64_t n, int32_t* status, uint64_t* size_out,
+                              const TileFirstJob& tf, hipStream_t stream);
 
 // Stream boundary discovery (cpk_stream.hip).  meta (device, 4 u64): [0] packed byte and [1]
 // word where the flat decode of the stream stopped, [2] its cpk_status; the walk follows the
 // segment tables from word 0 over the decoded words.
+// Fills nbytes at p (8-byte aligned) with value: the codec's scratch zeroing.
+hipError_t launch_fill(void* p, uint64_t nbytes, uint8_t value, hipStream_t stream);
 hipError_t launch_set_u64x4(uint64_t* dst, uint64_t v0, uint64_t v1, uint64_t v2, uint64_t v3,
                             hipStream_t stream);
 hipError_t launch_split_walk(const uint8_t* packed, uint64_t nbytes, const uint64_t* words,

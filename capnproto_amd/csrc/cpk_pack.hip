@@ -672,7 +672,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S <= 8 ? 6 
 __global__ void message_bits_kernel(const uint64_t* __restrict__ words,
                                     const uint64_t* __restrict__ off, uint64_t n,
                                     unsigned long long* __restrict__ bits,
-                                    int32_t* __restrict__ status) {
+                                    int32_t* __restrict__ status, TileFirstJob tf,
+                                    uint32_t tf_block) {
+  if (run_tile_first(tf, tf_block)) return;
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint64_t w0 = off[i], w1 = off[i + 1];
@@ -706,7 +708,9 @@ __global__ void message_bits_kernel(const uint64_t* __restrict__ words,
 }
 
 __global__ void chunk_bits_kernel(const uint64_t* __restrict__ off, uint64_t n, uint64_t N,
-                                  unsigned long long* __restrict__ bits) {
+                                  unsigned long long* __restrict__ bits, TileFirstJob tf,
+                                  uint32_t tf_block) {
+  if (run_tile_first(tf, tf_block)) return;
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i == 0 && N > 0) atomicOr(bits, 1ull);  // word 0 always starts a chunk
   if (i >= n) return;
@@ -715,19 +719,6 @@ __global__ void chunk_bits_kernel(const uint64_t* __restrict__ off, uint64_t n, 
 }
 
 // tile_first[t] = first index i in [0, npos] with pos[i] >= t*T (binary search).
-__global__ void tile_first_kernel(const uint64_t* __restrict__ pos, uint64_t npos, uint64_t ntiles,
-                                  uint64_t T, uint64_t* __restrict__ tile_first) {
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= ntiles) return;
-  const uint64_t key = t * T;
-  uint64_t lo = 0, hi = npos + 1;
-  while (lo < hi) {
-    const uint64_t mid = (lo + hi) >> 1;
-    if (pos[mid] < key) lo = mid + 1;
-    else hi = mid;
-  }
-  tile_first[t] = lo;
-}
 
 }  // namespace
 
@@ -818,27 +809,23 @@ hipError_t launch_pack_tiles(const PackTileArgs& a, hipStream_t stream) {
 }
 
 hipError_t launch_message_bits(const uint64_t* words, const uint64_t* off, uint64_t n,
-                               uint64_t* bits, int32_t* status, hipStream_t stream) {
-  if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(message_bits_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
-                     words, off, n, (unsigned long long*)bits, status);
+                               uint64_t* bits, int32_t* status, const TileFirstJob& tf,
+                               hipStream_t stream) {
+  const unsigned nb = (unsigned)((n + 255) / 256);
+  if (nb + tile_first_blocks(tf) == 0) return hipSuccess;
+  hipLaunchKernelGGL(message_bits_kernel, dim3(nb + tile_first_blocks(tf)), dim3(256), 0, stream,
+                     words, off, n, (unsigned long long*)bits, status, tf, nb);
   return hipGetLastError();
 }
 
 hipError_t launch_chunk_bits(const uint64_t* off, uint64_t n, uint64_t N, uint64_t* bits,
-                             hipStream_t stream) {
-  if (n == 0 && N == 0) return hipSuccess;
-  hipLaunchKernelGGL(chunk_bits_kernel, dim3((unsigned)((n + 256) / 256)), dim3(256), 0, stream,
-                     off, n, N, (unsigned long long*)bits);
+                             const TileFirstJob& tf, hipStream_t stream) {
+  const unsigned nb = (n == 0 && N == 0) ? 0u : (unsigned)((n + 256) / 256);
+  if (nb + tile_first_blocks(tf) == 0) return hipSuccess;
+  hipLaunchKernelGGL(chunk_bits_kernel, dim3(nb + tile_first_blocks(tf)), dim3(256), 0, stream,
+                     off, n, N, (unsigned long long*)bits, tf, nb);
   return hipGetLastError();
 }
 
-hipError_t launch_tile_first(const uint64_t* pos, uint64_t npos, uint64_t ntiles, uint64_t T,
-                             uint64_t* tile_first, hipStream_t stream) {
-  if (ntiles == 0) return hipSuccess;
-  hipLaunchKernelGGL(tile_first_kernel, dim3((unsigned)((ntiles + 255) / 256)), dim3(256), 0,
-                     stream, pos, npos, ntiles, T, tile_first);
-  return hipGetLastError();
-}
 
 }  // namespace cpk

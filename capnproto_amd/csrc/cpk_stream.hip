@@ -31,6 +31,18 @@ __global__ void set4_kernel(uint64_t* d, uint64_t v0, uint64_t v1, uint64_t v2, 
   }
 }
 
+// Scratch zeroing as a kernel: every buffer the codec fills is 8-byte aligned.  (Inside a
+// captured hipGraph, memset nodes that share a destination -- the pack and the unpack scratch
+// are one buffer -- were observed to replay with the wrong extent; a kernel node is a kernel.)
+__global__ void fill_kernel(uint8_t* __restrict__ p, uint64_t n, uint8_t value) {
+  const uint64_t v8 = 0x0101010101010101ull * value;
+  const uint64_t nw = n / 8;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nw;
+       i += (uint64_t)gridDim.x * blockDim.x)
+    ((uint64_t*)p)[i] = v8;
+  if (blockIdx.x == 0 && threadIdx.x < n - 8 * nw) p[8 * nw + threadIdx.x] = value;
+}
+
 struct Flat {
   const uint8_t* packed;
   uint64_t nbytes;
@@ -199,6 +211,17 @@ hipError_t launch_gather_segments(const uint64_t* meta, uint32_t nseg, uint64_t 
                                   uint64_t* out, hipStream_t stream) {
   if (total == 0) return hipSuccess;
   gather_kernel<<<(unsigned)((total + 2047) / 2048), 256, 0, stream>>>(meta, nseg, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_fill(void* p, uint64_t nbytes, uint8_t value, hipStream_t stream) {
+  if (nbytes == 0) return hipSuccess;
+  if ((uintptr_t)p & 7) return hipErrorInvalidValue;
+  const uint64_t nw = nbytes / 8;
+  uint64_t blocks = (nw + 255) / 256;
+  if (blocks < 1) blocks = 1;
+  if (blocks > 4096) blocks = 4096;
+  fill_kernel<<<(unsigned)blocks, 256, 0, stream>>>((uint8_t*)p, nbytes, value);
   return hipGetLastError();
 }
 

@@ -104,7 +104,8 @@ __device__ int32_t decode_exact(const uint8_t* b, uint64_t& p, uint64_t end, uin
 __global__ void header_kernel(const uint8_t* __restrict__ packed,
                               const uint64_t* __restrict__ in_off, uint64_t n, uint64_t limit,
                               uint64_t* __restrict__ flat, int32_t* __restrict__ hdr_status,
-                              int32_t* __restrict__ status) {
+                              int32_t* __restrict__ status, TileFirstJob tf, uint32_t tf_block) {
+  if (run_tile_first(tf, tf_block)) return;
   const uint64_t m = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= n) return;
   uint64_t p = in_off[m];
@@ -1510,7 +1511,9 @@ __global__ __launch_bounds__(64) void fallback_kernel(UnpackArgs a) {
 // exactly word_off[m+1]-word_off[m] words; size-only buffers start at 0 words.
 __global__ void init_kernel(uint32_t mode, const uint64_t* __restrict__ in_off,
                             const uint64_t* __restrict__ word_off, uint64_t n,
-                            int32_t* __restrict__ status, uint64_t* __restrict__ size_out) {
+                            int32_t* __restrict__ status, uint64_t* __restrict__ size_out,
+                            TileFirstJob tf, uint32_t tf_block) {
+  if (run_tile_first(tf, tf_block)) return;
   const uint64_t m = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= n) return;
   const bool empty = in_off[m + 1] == in_off[m];
@@ -1527,19 +1530,21 @@ __global__ void init_kernel(uint32_t mode, const uint64_t* __restrict__ in_off,
 
 hipError_t launch_unpack_init(uint32_t mode, const uint64_t* in_off, const uint64_t* word_off,
                               uint64_t n, int32_t* status, uint64_t* size_out,
-                              hipStream_t stream) {
-  if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(init_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, mode,
-                     in_off, word_off, n, status, size_out);
+                              const TileFirstJob& tf, hipStream_t stream) {
+  const unsigned nb = (unsigned)((n + 255) / 256);
+  if (nb + tile_first_blocks(tf) == 0) return hipSuccess;
+  hipLaunchKernelGGL(init_kernel, dim3(nb + tile_first_blocks(tf)), dim3(256), 0, stream, mode,
+                     in_off, word_off, n, status, size_out, tf, nb);
   return hipGetLastError();
 }
 
 hipError_t launch_unpack_header(const uint8_t* packed, const uint64_t* in_off, uint64_t n,
                                 uint64_t limit, uint64_t* flat, int32_t* hdr_status,
-                                int32_t* status, hipStream_t stream) {
-  if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(header_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
-                     packed, in_off, n, limit, flat, hdr_status, status);
+                                int32_t* status, const TileFirstJob& tf, hipStream_t stream) {
+  const unsigned nb = (unsigned)((n + 255) / 256);
+  if (nb + tile_first_blocks(tf) == 0) return hipSuccess;
+  hipLaunchKernelGGL(header_kernel, dim3(nb + tile_first_blocks(tf)), dim3(256), 0, stream,
+                     packed, in_off, n, limit, flat, hdr_status, status, tf, nb);
   return hipGetLastError();
 }
 
