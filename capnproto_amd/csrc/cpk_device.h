@@ -78,6 +78,10 @@ template <int CTRL, int ROWS>
 __device__ __forceinline__ uint32_t dpp_src(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWS, 0xf, true);
 }
+// Lane l receives lane l - 1's v (DPP wave_shr:1, GFX9); lane 0 receives `fill`.
+__device__ __forceinline__ uint32_t wave_shr1_32(uint32_t v, uint32_t fill = 0) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)fill, (int)v, 0x138, 0xf, 0xf, false);
+}
 template <class Op>
 __device__ __forceinline__ uint32_t wave_scan32(uint32_t v, Op op) {
   v = op(v, dpp_src<0x111, 0xf>(v));

@@ -232,7 +232,8 @@ __device__ __forceinline__ void finish3(const PackTileArgs& a, uint32_t* wst, co
 }
 
 template <bool STAMPS>
-__global__ __launch_bounds__(256) void pack3_kernel(PackTileArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void pack3_kernel(
+    PackTileArgs a) {
   // per wave: the staging slot, then one trash dword per lane
   __shared__ __attribute__((aligned(16))) uint32_t stg_all[4][kSlotDw + 64];
   __shared__ uint64_t sel_tab[256];

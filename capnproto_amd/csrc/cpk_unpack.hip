@@ -143,15 +143,30 @@ __device__ __forceinline__ int rec_len(uint32_t tag, uint32_t cnt) {
   return 1 + __popc(tag) + ((tag == 0 || tag == 0xff) ? 1 : 0) + (tag == 0xff ? 8 * (int)cnt : 0);
 }
 
-// Record length at tile position p given the staged bytes (no clipping).
+// Index staging layout: sub-tile l (tile bytes [64l, 64l + 64)) is row l of kRow bytes, its 64
+// bytes followed by a copy of the next 12, so every byte a walk step reads (p, p + 1, p + 9)
+// lies in p's row.  Rows start 19 dwords apart: lanes walking their own sub-tiles in step hit 32
+// distinct banks (at a 64-byte stride every lane's row began on bank 0 or 16: 16-way conflicts).
+#ifndef CPK_INDEX_ROW
+#define CPK_INDEX_ROW 64
+#endif
+constexpr int kRow = CPK_INDEX_ROW;  // 64: plain layout (A/B builds only)
+constexpr int kRowBytes = 64 * kRow + 16;
+__device__ __forceinline__ const uint8_t* ix(const uint8_t* d, int p) {
+  return d + p + (kRow - 64) * (p >> 6);
+}
+
+// Record length at tile position p given the staged rows (no clipping).
 __device__ __forceinline__ int record_len(const uint8_t* d, int p) {
-  return rec_len(d[p], d[p + 9]);
+  const uint8_t* q = ix(d, p);
+  return rec_len(q[0], q[9]);
 }
 
 struct SubTile {
   int s, end, vend;  // sub-tile [s, end); walks stop at vend = min(end, batch end)
   uint64_t msw;      // message-start bits of the sub-tile
   int nms_after;     // first message start >= end (tile-relative; may be >= kB)
+  bool no_starts;    // wave-uniform: no message start in any sub-tile of the tile
   int pend;          // batch end, tile-relative
 };
 
@@ -169,13 +184,31 @@ __device__ __forceinline__ int next_start_after(const SubTile& st, int q) {
 __device__ __forceinline__ int walk(const uint8_t* d, const SubTile& st, int p, uint64_t stop,
                                     uint64_t* marks, uint64_t* runs = nullptr) {
   uint64_t m = 0, rm = 0;
+  if (st.no_starts) {
+    // no message start in the tile: the only clip is the first start after the sub-tile, where
+    // the walk ends anyway (most tiles of large messages)
+    while (p < st.vend) {
+      const uint64_t bit = 1ull << (p - st.s);
+      m |= bit;
+      const uint8_t* q = ix(d, p);
+      const uint32_t tag = q[0];
+      if (tag == 0 || tag == 0xff) rm |= bit;
+      const int np = p + rec_len(tag, q[9]);
+      p = np < st.nms_after ? np : st.nms_after;
+      if (p < st.vend && ((stop >> (p - st.s)) & 1)) break;
+    }
+    *marks = m;
+    if (runs) *runs = rm;
+    return p >= st.pend ? kDead : p;
+  }
   int nm = next_start_after(st, p);
   while (p < st.vend) {
     const uint64_t bit = 1ull << (p - st.s);
     m |= bit;
-    const uint32_t tag = d[p];
+    const uint8_t* q = ix(d, p);
+    const uint32_t tag = q[0];
     if (tag == 0 || tag == 0xff) rm |= bit;
-    int np = p + record_len(d, p);
+    int np = p + rec_len(tag, q[9]);
     if (np >= nm) {
       np = nm;
       nm = np < st.end ? next_start_after(st, np) : st.nms_after;
@@ -198,10 +231,21 @@ __device__ __forceinline__ int walk(const uint8_t* d, const SubTile& st, int p, 
 __device__ __forceinline__ bool settle(const uint8_t* d, const SubTile& st, uint64_t chain,
                                        int sx, int E, int& e, uint64_t& tm, int& out,
                                        uint64_t& runm, int* iters = nullptr) {
-  const int l = lane_id();
+  // round 0, every lane entered at its own start, needs no walk: the speculative chain itself
+  // (a sub-tile past the batch end passes nothing on)
+  bool pass = e >= st.end || e >= st.pend;
+  out = pass ? (e >= st.pend ? kDead : e) : sx;
+  tm = pass ? 0ull : chain;
   for (int iter = 0; iter < 96; iter++) {
     if (iters) *iters = iter + 1;
-    const bool pass = e >= st.end || e >= st.pend;
+    // the largest exit of the earlier lanes (wave_shr:1 of the inclusive max: no LDS trip)
+    const uint32_t incl = wave_incl_max32(pass ? 0u : (uint32_t)out);
+    const int prev = (int)wave_shr1_32(incl);
+    int en = lane_id() == 0 ? E : (prev > E ? prev : E);
+    if (lane_id() > 0 && en < st.s) en = st.s;
+    if (!ballot(en != e)) return true;
+    e = en;
+    pass = e >= st.end || e >= st.pend;
     if (pass) {
       out = e >= st.pend ? kDead : e;
       tm = 0;
@@ -220,12 +264,6 @@ __device__ __forceinline__ bool settle(const uint8_t* d, const SubTile& st, uint
         tm = wm;
       }
     }
-    const uint32_t incl = wave_incl_max32(pass ? 0u : (uint32_t)out);
-    const int prev = (int)shfl32(incl, l > 0 ? l - 1 : 0);
-    int en = l == 0 ? E : (prev > E ? prev : E);
-    if (l > 0 && en < st.s) en = st.s;
-    if (!ballot(en != e)) return true;
-    e = en;
   }
   return false;
 }
@@ -547,6 +585,33 @@ __device__ __forceinline__ void stage_load(const UnpackArgs& a, uint64_t A, Stag
   }
 }
 
+// The same bytes into the index rows (kRow layout): dword stores (rows are 4-byte aligned),
+// and the lane holding the first 16 bytes of row r + 1 also writes their first 12 as row r's tail.
+__device__ __forceinline__ void stage_store_rows(const Staged& sg, uint8_t* d) {
+  const int l = lane_id();
+#pragma unroll
+  for (int k = 0; k < kStageVecs; k++) {
+    const int o = 16 * (64 * k + l);
+    if (o < kB + kPad) {
+      const int row = o >> 6, c = o & 63;
+      if (row < 64) {
+        uint32_t* q = (uint32_t*)(d + kRow * row + c);
+        q[0] = sg.v[k].x;
+        q[1] = sg.v[k].y;
+        q[2] = sg.v[k].z;
+        q[3] = sg.v[k].w;
+      }
+      if (c == 0 && row > 0) {
+        uint32_t* q = (uint32_t*)(d + kRow * (row - 1) + 64);
+        q[0] = sg.v[k].x;
+        q[1] = sg.v[k].y;
+        q[2] = sg.v[k].z;
+      }
+    }
+  }
+  lane_handoff();  // other lanes read these bytes next
+}
+
 __device__ __forceinline__ void stage_tile(const UnpackArgs& a, uint64_t A, uint8_t* d) {
   Staged sg;
   stage_load(a, A, sg);
@@ -613,15 +678,13 @@ __device__ __forceinline__ SubTile make_subtile(uint64_t A, uint64_t P, uint64_t
   st.pend = (P - A) < (uint64_t)kDead ? (int)(P - A) : kDead;
   st.vend = st.end < st.pend ? st.end : st.pend;
   st.msw = msw;
+  // the next lane holding a message start, and its first one
+  const uint64_t hs = ballot(st.msw != 0);
+  st.no_starts = hs == 0;
+  const uint64_t above = hs & ~mask_le(l);
   const int fs = st.msw ? st.s + lowest_bit(st.msw) : 0x7fffffff;
-  int v = fs;
-#pragma unroll
-  for (int dd = 1; dd < 64; dd <<= 1) {
-    const int o = (int)shfl32((uint32_t)v, l + dd <= 63 ? l + dd : l);
-    if (l + dd <= 63) v = o < v ? o : v;
-  }
-  const int nxt = (int)shfl32((uint32_t)v, l < 63 ? l + 1 : 63);
-  st.nms_after = (l < 63 && nxt != 0x7fffffff) ? nxt : nms_tile_after;
+  const int nxt = (int)shfl32((uint32_t)fs, above ? lowest_bit(above) : l);
+  st.nms_after = above ? nxt : nms_tile_after;
   return st;
 }
 
@@ -638,14 +701,19 @@ __device__ __forceinline__ uint64_t make_dep(uint32_t tag) {
   return sel;
 }
 
-// 3. Index: one wave per tile, chain 0 + merge table (see the file comment).
+// 3. Index: one wave per tile, chain 0 + merge table (see the file comment).  Two waves per
+// workgroup: 10.5 KiB of LDS each, 15 workgroups (30 waves) per CU.
+#ifndef CPK_INDEX_WAVES
+#define CPK_INDEX_WAVES 2
+#endif
+constexpr int kIndexWaves = CPK_INDEX_WAVES;
 template <bool STAMPS>
-__global__ __launch_bounds__(256) void index_kernel(UnpackArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds_data[4][kB + kPad];
-  __shared__ uint64_t lds_ms[4][64];  // message starts, then chain-0 masks (merge table)
+__global__ __launch_bounds__(64 * kIndexWaves) void index_kernel(UnpackArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds_data[kIndexWaves][kRowBytes];
+  __shared__ uint64_t lds_ms[kIndexWaves][64];  // message starts, then chain-0 masks
   const int l = lane_id();
   const int wv = (int)uniform32(threadIdx.x >> 6);
-  const uint64_t t = (uint64_t)blockIdx.x * 4 + wv;
+  const uint64_t t = (uint64_t)blockIdx.x * kIndexWaves + wv;
   if (t >= a.ntiles) return;
   Stamps<STAMPS> stm;
   stm.start(a.stamps2);
@@ -660,7 +728,8 @@ __global__ __launch_bounds__(256) void index_kernel(UnpackArgs a) {
   stage_load(a, A, stg);
   const uint64_t mfirst = uniform64(a.tile_first[t]);
   stm.mark(0);
-  stage_store(stg, d);
+  if constexpr (kRow == 64) stage_store(stg, d);
+  else stage_store_rows(stg, d);
   stm.mark(1);
   int nms_tile_after;
   (void)tile_msg_starts(a, A, mfirst, lds_ms[wv], &nms_tile_after, nullptr);
@@ -705,8 +774,8 @@ __global__ __launch_bounds__(256) void index_kernel(UnpackArgs a) {
     while (rr) {
       const int b = lowest_bit(rr);
       rr &= rr - 1;
-      const int p = st.s + b;
-      const uint32_t c = d[p + 1 + __popc(d[p])];
+      const uint8_t* q = ix(d, st.s + b);
+      const uint32_t c = q[1 + __popc(q[0])];
       w_all += c;
       if ((pre_m >> b) & 1) w_pre += c;
       if (has_ms && b >= lastms) w_post += c;
@@ -742,7 +811,8 @@ __global__ __launch_bounds__(256) void index_kernel(UnpackArgs a) {
       }
       // the four reads of a step are independent: one LDS round trip per record
       const uint64_t mk = lds_tm[p >> 6];
-      const uint32_t tag = d[p], c1 = d[p + 1], c9 = d[p + 9];
+      const uint8_t* q = ix(d, p);
+      const uint32_t tag = q[0], c1 = q[1], c9 = q[9];
       asm volatile("" ::"v"(tag), "v"(c1), "v"(c9));  // keep the reads ahead of the branch
       if ((mk >> (p & 63)) & 1) {
         m = p;
@@ -774,8 +844,8 @@ __global__ __launch_bounds__(256) void index_kernel(UnpackArgs a) {
         while (r2) {
           const int bb = lowest_bit(r2);
           r2 &= r2 - 1;
-          const int q = 64 * (m >> 6) + bb;
-          w0 += d[q + 1 + __popc(d[q])];
+          const uint8_t* q = ix(d, 64 * (m >> 6) + bb);
+          w0 += q[1 + __popc(q[0])];
         }
       }
       delta = (int32_t)(ww - w0);
@@ -1551,12 +1621,15 @@ hipError_t launch_unpack_header(const uint8_t* packed, const uint64_t* in_off, u
 hipError_t launch_unpack_stage(int stage, const UnpackArgs& a, hipStream_t stream) {
   if (a.ntiles == 0) return hipSuccess;
   const unsigned wave_blocks = (unsigned)((a.ntiles + 3) / 4);
+  const unsigned index_blocks = (unsigned)((a.ntiles + kIndexWaves - 1) / kIndexWaves);
   switch (stage) {
     case kUnpackIndex:
       if (a.stamps2)
-        hipLaunchKernelGGL(index_kernel<true>, dim3(wave_blocks), dim3(256), 0, stream, a);
+        hipLaunchKernelGGL(index_kernel<true>, dim3(index_blocks), dim3(64 * kIndexWaves), 0,
+                           stream, a);
       else
-        hipLaunchKernelGGL(index_kernel<false>, dim3(wave_blocks), dim3(256), 0, stream, a);
+        hipLaunchKernelGGL(index_kernel<false>, dim3(index_blocks), dim3(64 * kIndexWaves), 0,
+                           stream, a);
       break;
     case kUnpackResolve:
       hipLaunchKernelGGL(resolve1_kernel, dim3((unsigned)((a.ntiles + 255) / 256)), dim3(256), 0,
