@@ -357,7 +357,7 @@ void _::PackedInputStream::skip(size_t bytes) {
 
 PackedMessageReader::PackedMessageReader(BufferedInputStream& in, ReaderOptions options,
                                          ArrayPtr<word> scratch)
-    : _::PackedInputStream(in), options_(options) {
+    : MessageReader(options), _::PackedInputStream(in) {
   // serialize.c++:202-270
   uint32_t first[2];
   InputStream::read(first, 8);

@@ -16,7 +16,9 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <future>
 #include <memory>
+#include <optional>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -198,6 +200,19 @@ struct ReaderOptions {
 void setDevice(int device);
 cpk_ctx* threadContext();
 
+// message.h:95-130 MessageReader, the part the packed path fills in: segments by id (null past
+// the last one) and the options the message was read with.
+class MessageReader {
+ public:
+  explicit MessageReader(ReaderOptions options) : options_(options) {}
+  virtual ~MessageReader() noexcept(false) = default;
+  virtual ArrayPtr<const word> getSegment(unsigned id) = 0;
+  const ReaderOptions& getOptions() const { return options_; }
+
+ private:
+  ReaderOptions options_;
+};
+
 namespace _ {  // private
 
 // serialize-packed.h:49-63.  Each write() is one chunk, packed by the device.
@@ -242,7 +257,7 @@ class PackedInputStream : public InputStream {
 // segments are read lazily by getSegment (:283-302), and the destructor skips whatever was not
 // read so the stream is left right after the message (:272-281).  Segments go into
 // scratchSpace when it is large enough, else into space the reader owns (:244-249).
-class PackedMessageReader : private _::PackedInputStream {
+class PackedMessageReader : public MessageReader, private _::PackedInputStream {
  public:
   PackedMessageReader(BufferedInputStream& inputStream, ReaderOptions options = ReaderOptions(),
                       ArrayPtr<word> scratchSpace = nullptr);
@@ -251,11 +266,9 @@ class PackedMessageReader : private _::PackedInputStream {
   PackedMessageReader& operator=(const PackedMessageReader&) = delete;
   size_t segmentCount() const { return 1 + moreSegments_.size(); }
   // MessageReader::getSegment (message.h:100): null past the last segment.
-  ArrayPtr<const word> getSegment(unsigned id);
-  const ReaderOptions& getOptions() const { return options_; }
+  ArrayPtr<const word> getSegment(unsigned id) override;
 
  private:
-  ReaderOptions options_;
   std::vector<word> owned_;
   ArrayPtr<const word> segment0_;
   std::vector<ArrayPtr<const word>> moreSegments_;
@@ -298,6 +311,66 @@ auto writePackedMessageToFd(int fd, Builder& builder)
 
 // serialize-packed.h:107.
 size_t computeUnpackedSizeInWords(ArrayPtr<const byte> packedBytes);
+
+// ---- async message streams (serialize-async.h:42-108) with packed framing ------------------
+// std::future stands in for kj::Promise and std::unique_ptr for kj::Own.  File descriptors
+// attached to messages (the fdSpace / fds overloads, SCM_RIGHTS over capability streams) are not
+// carried: they are no part of the packed path.
+class MessageStream {
+ public:
+  virtual ~MessageStream() = default;
+  // serialize-async.h:54-57: the next message, or null at a clean end of the stream (the input
+  // ends before the message's first byte).  scratchSpace must outlive the returned reader.
+  virtual std::future<std::unique_ptr<MessageReader>> tryReadMessage(
+      ReaderOptions options = ReaderOptions(), ArrayPtr<word> scratchSpace = nullptr) = 0;
+  // serialize-async.c++:518-529: like tryReadMessage, but "Premature EOF." at the end.
+  virtual std::future<std::unique_ptr<MessageReader>> readMessage(
+      ReaderOptions options = ReaderOptions(), ArrayPtr<word> scratchSpace = nullptr) = 0;
+  // serialize-async.h:78-83.  The segments must stay valid until the future is ready.
+  virtual std::future<void> writeMessage(ArrayPtr<const ArrayPtr<const word>> segments) = 0;
+  // serialize-async.h:88-93: a batch of messages, written back to back in one go.
+  virtual std::future<void> writeMessages(
+      ArrayPtr<const ArrayPtr<const ArrayPtr<const word>>> messages) = 0;
+  template <typename Builder>
+  auto writeMessage(Builder& builder) -> decltype(builder.getSegmentsForOutput(),
+                                                  std::future<void>()) {
+    return writeMessage(builder.getSegmentsForOutput());
+  }
+  // serialize-async.h:95: SO_SNDBUF of the underlying socket, if it is one.
+  virtual std::optional<int> getSendBufferSize() = 0;
+  // serialize-async.h:105: shut down the write end (after every write already started).
+  virtual std::future<void> end() = 0;
+};
+
+// The packed counterpart of AsyncIoMessageStream (serialize-async.h:110-133) over a socket, pipe
+// or file descriptor: what a writePackedMessage / PackedMessageReader pair exchanges, with each
+// call running on the stream's own reader or writer thread (reads in order, writes in order,
+// the two directions independent).  Reads decode on the device exactly as PackedMessageReader
+// does, taking from the stream only the bytes of the message; a batch write packs every message
+// of the batch in one device call and issues one write(2).
+class PackedMessageStream final : public MessageStream {
+ public:
+  explicit PackedMessageStream(int fd, size_t bufferSizeInWords = 8192);
+  explicit PackedMessageStream(OwnFd fd, size_t bufferSizeInWords = 8192);
+  ~PackedMessageStream() override;  // waits for the operations already started
+  PackedMessageStream(const PackedMessageStream&) = delete;
+  PackedMessageStream& operator=(const PackedMessageStream&) = delete;
+
+  std::future<std::unique_ptr<MessageReader>> tryReadMessage(
+      ReaderOptions options = ReaderOptions(), ArrayPtr<word> scratchSpace = nullptr) override;
+  std::future<std::unique_ptr<MessageReader>> readMessage(
+      ReaderOptions options = ReaderOptions(), ArrayPtr<word> scratchSpace = nullptr) override;
+  std::future<void> writeMessage(ArrayPtr<const ArrayPtr<const word>> segments) override;
+  std::future<void> writeMessages(
+      ArrayPtr<const ArrayPtr<const ArrayPtr<const word>>> messages) override;
+  using MessageStream::writeMessage;
+  std::optional<int> getSendBufferSize() override;
+  std::future<void> end() override;
+
+ private:
+  struct Impl;
+  std::unique_ptr<Impl> impl_;
+};
 
 }  // namespace cpk_capnp
 

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Diagnostic: per-phase cycles of the lane-serial pack kernel (CPK_PACK3=1 CPK_STAMPS=1)."""
+"""Diagnostic: per-phase cycles of the lane-serial pack kernel (CPK_STAMPS=1)."""
 import ctypes as C
 import os
 import sys
@@ -25,11 +25,11 @@ for rep in range(3):
     L.cpk_debug_stamps(0, out)
     tm = codec.timing_read_all()
 print(cfg, "pack kernel ms (stamps build):", round(tm["pack"][0], 4))
-tiles = out[15] or 1
-print("wave lifetime us:", round(out[13] / tiles / 100, 2))
-names = ["loads issue", "classes(+load wait)", "look-ahead", "cover/entry", "entry wait",
-         "count+publish", "emission", "look-back", "flush", "positions"]
-tot = sum(out[i] for i in range(10))
-print("cycles/tile", round(tot / tiles))
+waves = out[15] or 1  # acc[15] = 1 per (persistent) wave
+print("wave lifetime us:", round(out[13] / waves / 100, 2))
+names = ["loads issue", "classes (+load wait)", "look-ahead", "cover/publish exit", "entry wait",
+         "bytes+publish agg", "finish prev (look-back, flush)", "emission", "tail"]
+tot = sum(out[i] for i in range(9))
+print("cycles/wave", round(tot / waves))
 for i, nm in enumerate(names):
-    print(f"  {nm:22s} {out[i] / tiles:10.0f}  {100 * out[i] / max(tot, 1):5.1f}%")
+    print(f"  {nm:32s} {out[i] / waves:12.0f}  {100 * out[i] / max(tot, 1):5.1f}%")
