@@ -48,6 +48,7 @@ constexpr uint64_t kSegBit = 1ull << 61;
 constexpr int kTab = 16;                    // merge-table slots per tile
 constexpr int kTabWalk = 10;                // entries 1..9 are walked (a record that is not a
                                             // raw run ends at most 9 bytes into the next tile)
+constexpr int kMergeCap = 48;               // merge-walk records before the jump walk
 constexpr uint32_t kTileUnsettled = 1;      // lane fixed point hit its iteration cap
 constexpr uint32_t kTileHasStart = 2;       // a message starts inside the tile
 constexpr int kWalkCap = 4096;              // records a resolve thread walks before giving up
@@ -475,7 +476,8 @@ __device__ __forceinline__ void run_jobs(const UnpackArgs& a, const RunJob& job)
 
 // Diagnostic counters (env CPK_STAMPS=1 only; a.stamps is NULL otherwise).
 enum : int { kDbgUnsettled = 0, kDbgTableMiss, kDbgWalkFail, kDbgWalks, kDbgFlagged,
-             kDbgUmaskTiles, kDbgMergeSteps, kDbgSettleIters, kDbgWalkSteps, kDbgWalkStepsMax };
+             kDbgUmaskTiles, kDbgMergeSteps, kDbgSettleIters, kDbgWalkSteps, kDbgWalkStepsMax,
+             kDbgMerge64, kDbgMerge256, kDbgMerge1k, kDbgSettle8, kDbgSettle24 };
 __device__ __forceinline__ void dbg_count(const UnpackArgs& a, int slot) {
   if (a.stamps) atomicAdd(a.stamps + kStampSlots * (blockIdx.x & (kStampRows - 1)) + slot, 1ull);
 }
@@ -751,6 +753,8 @@ __global__ __launch_bounds__(64 * kIndexWaves) void index_kernel(UnpackArgs a) {
   if (a.stamps) {
     const uint32_t nrec = __popcll(chain);
     dbg_add(a, kDbgSettleIters, (uint64_t)siters);
+    if (siters > 8) dbg_add(a, kDbgSettle8, 1);
+    if (siters > 24) dbg_add(a, kDbgSettle24, 1);
     dbg_add(a, kDbgWalkSteps, readlane32(wave_incl_sum32(nrec), 63));
     dbg_add(a, kDbgWalkStepsMax, readlane32(wave_incl_max32(nrec), 63));
   }
@@ -800,13 +804,16 @@ __global__ __launch_bounds__(64 * kIndexWaves) void index_kernel(UnpackArgs a) {
   uint32_t ww = 0;
   bool merged = true;
   int msteps = 0;
+  bool open = false;  // still walking after kMergeCap records
   if (!(a.debug_skip & 8) && l >= 1 && l < kTabWalk) {
-    for (int k = 0; k < 2 * kB; k++) {
+    open = true;
+    for (int k = 0; k < kMergeCap; k++) {
       msteps = k;
       if (p >= fms) {
         if (fms < kB) m = fms;           // every chain restarts at the first message start
         else if (p == (int)x0) m = kB;   // left the tile at chain 0's exit
         else merged = false;
+        open = false;
         break;
       }
       // the four reads of a step are independent: one LDS round trip per record
@@ -816,11 +823,65 @@ __global__ __launch_bounds__(64 * kIndexWaves) void index_kernel(UnpackArgs a) {
       asm volatile("" ::"v"(tag), "v"(c1), "v"(c9));  // keep the reads ahead of the branch
       if ((mk >> (p & 63)) & 1) {
         m = p;
+        open = false;
         break;
       }
       const uint32_t cnt = tag == 0 ? c1 : (tag == 0xff ? c9 : 0u);
       ww += 1 + cnt;
       p += rec_len(tag, cnt);
+    }
+  }
+  if (ballot(open)) {
+    // Rare: chains that run on beside chain 0 for hundreds of records (interleaved chains that
+    // meet late or never).  Walked record by record such a chain costs one LDS round trip per
+    // record across the tile, and that one wave set the kernel's tail.  Every lane now also
+    // walks a second chain B of its sub-tile -- from its first byte chain 0 does not start a
+    // record at, until it meets chain 0 -- and a walk that lands on B jumps straight to B's end
+    // (B's exit, or the chain-0 record where B meets it), adding B's records and run counts.
+    const uint64_t vm = st.vend <= st.s ? 0ull : (st.vend >= st.s + 64 ? ~0ull
+                                                                     : mask_lt(st.vend - st.s));
+    const uint64_t notA = ~tm & vm;
+    uint64_t chB = 0, rB = 0;
+    int xB = kDead;
+    if (notA) xB = walk(d, st, st.s + lowest_bit(notA), tm, &chB, &rB);
+    rB &= chB;
+    for (int k = kMergeCap; k < 2 * kB && ballot(open); k++) {
+      // every lane takes part in the shuffles (an inactive source lane would read as 0)
+      const int j = open ? (p >> 6 < 63 ? p >> 6 : 63) : l;
+      const uint64_t Bj = shfl64(chB, j), rBj = shfl64(rB, j);
+      const int xBj = (int)shfl32((uint32_t)xB, j);
+      if (open) {
+        msteps = k;
+        if (p >= fms) {
+          if (fms < kB) m = fms;
+          else if (p == (int)x0) m = kB;
+          else merged = false;
+          open = false;
+        } else {
+          const uint64_t mk = lds_tm[p >> 6];
+          const uint8_t* q = ix(d, p);
+          const uint32_t tag = q[0], c1 = q[1], c9 = q[9];
+          const int b = p & 63;
+          if ((mk >> b) & 1) {
+            m = p;
+            open = false;
+          } else if ((Bj >> b) & 1) {
+            const uint64_t on = ~mask_lt(b);
+            ww += __popcll(Bj & on);
+            uint64_t rr = rBj & on;
+            while (rr) {
+              const uint8_t* r = ix(d, 64 * j + lowest_bit(rr));
+              rr &= rr - 1;
+              ww += r[1 + __popc(r[0])];
+            }
+            p = xBj;  // kDead: B ran into the batch end (as chain 0 then did: x0 == kDead)
+          } else {
+            const uint32_t cnt = tag == 0 ? c1 : (tag == 0xff ? c9 : 0u);
+            ww += 1 + cnt;
+            p += rec_len(tag, cnt);
+          }
+        }
+      }
     }
   }
   // chain-0 words before the merge point (all lanes take part in the shuffles)
@@ -854,7 +915,11 @@ __global__ __launch_bounds__(64 * kIndexWaves) void index_kernel(UnpackArgs a) {
   stm.mark(6);
   const uint32_t umask = (uint32_t)ballot(l >= 1 && l < kTab && !merged);
   if (a.stamps) {
-    dbg_add(a, kDbgMergeSteps, readlane32(wave_incl_max32((uint32_t)msteps), 63));
+    const uint32_t mx = readlane32(wave_incl_max32((uint32_t)msteps), 63);
+    dbg_add(a, kDbgMergeSteps, mx);
+    if (mx > 64) dbg_add(a, kDbgMerge64, 1);
+    if (mx > 256) dbg_add(a, kDbgMerge256, 1);
+    if (mx > 1024) dbg_add(a, kDbgMerge1k, 1);
     if (umask) dbg_add(a, kDbgUmaskTiles, 1);
   }
   if (l < kTab) a.t_delta[t * kTab + l] = delta;
@@ -1174,7 +1239,7 @@ __device__ __forceinline__ void expand_tile(const UnpackArgs& a, uint64_t t, con
     if (pre_ok && E < fms) {
       aux[l] = tm;
       lane_handoff();
-      if (l == 0) {
+      if (l == 0 && !(a.debug_skip & 128)) {  // (diagnostic: 128 skips the patch walk)
         // the reads of a step are independent (one LDS round trip per record); the walked
         // starts of a sub-tile collect in a register until the walk leaves it
         int p = (int)E;
@@ -1641,7 +1706,9 @@ hipError_t launch_unpack_stage(int stage, const UnpackArgs& a, hipStream_t strea
       hipLaunchKernelGGL(expand_kernel, dim3(wave_blocks), dim3(256), 0, stream, a);
       break;
     default:
-      hipLaunchKernelGGL(fallback_kernel, dim3(2048), dim3(64), 0, stream, a);
+      // a small grid: it only loops over the (rare) flagged messages, and an empty launch of
+      // thousands of workgroups costs microseconds
+      hipLaunchKernelGGL(fallback_kernel, dim3(128), dim3(64), 0, stream, a);
       break;
   }
   return hipGetLastError();

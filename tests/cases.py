@@ -32,6 +32,13 @@ def random_words(rng, n, profile="mixed"):
         return b.view("<u8").copy()
     if profile == "zeros":
         return np.zeros(n, "<u8")
+    if profile == "locked":
+        # one non-zero byte per word, itself a power of two: every record is 2 bytes and every
+        # data byte, read as a tag, is a 2-byte record too -- the chains through the odd and the
+        # even bytes never meet (parity-locked packed data)
+        b = np.zeros((n, 8), np.uint8)
+        b[np.arange(n), rng.integers(0, 8, size=n)] = (1 << rng.integers(0, 8, size=n)).astype(np.uint8)
+        return b.reshape(-1).view("<u8").copy()
     # "mixed": a run-length mixture of every word class.
     out = np.zeros(n, "<u8")
     i = 0

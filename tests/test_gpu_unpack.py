@@ -87,6 +87,28 @@ def test_large_messages_multi_tile(codec, oracle):
     check_against_oracle(codec, oracle, msgs)
 
 
+def test_parity_locked_chains(codec, oracle):
+    """Packed data whose record chains from odd and even bytes never meet, over many tiles and
+    across message starts: the index kernel's capped merge walks hand such entries to the
+    lane-parallel two-chain resolution (entry_chain), and resolve / expand must still follow the
+    true chain."""
+    rng = np.random.default_rng(31)
+    msgs = []
+    for n in (20000, 3000, 1, 2, 700, 16000, 5, 9000):
+        parts = [cases.random_words(rng, n, "locked")]
+        if n > 100:  # a lock that ends: ordinary data after it
+            parts.append(cases.random_words(rng, 200, "mixed"))
+            parts.append(cases.random_words(rng, n // 2, "locked"))
+        w = np.concatenate(parts)
+        m = np.concatenate([np.array([len(w) << 32], "<u8"), w])
+        msgs.append(oracle.pack_flat(m)[0])
+    check_against_oracle(codec, oracle, msgs)
+    # small messages in front shift every lock against the 4 KiB tile grid
+    for k in (1, 2, 3):
+        tiny = oracle.pack_flat(cases.flat_message(rng, 1, [k], "mixed"))[0]
+        check_against_oracle(codec, oracle, [tiny] + msgs[::-1])
+
+
 def test_error_cases(codec, oracle):
     rng = np.random.default_rng(21)
     msgs = []

@@ -28,7 +28,7 @@ codec.sync()
 names = {0: ["passA", "lookahead+exit", "entry wait", "count+publish", "passB", "finish(prev)"],
          1: ["unsettled tiles", "table misses", "walk fails", "walks", "flagged msgs",
              "umask tiles", "merge steps (max/tile)", "settle iters", "walk records (sum)",
-             "walk records (max/tile)"]}
+             "walk records (max/tile)", "merge walk > 64", "> 256", "> 1024", "settle > 8 rounds", "> 24"]}
 for which in (0, 1):
     out = (C.c_uint64 * 16)()
     if L.cpk_debug_stamps(which, out) != 0:
