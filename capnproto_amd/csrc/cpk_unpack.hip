@@ -1234,19 +1234,20 @@ __device__ __forceinline__ void expand_tile(const UnpackArgs& a, uint64_t t, con
   // ---- chain 0 -> the true chain: starts before the merge point come from a walk from E ----
   if (E > 0) {
     const bool pre_ok = readlane32(win.ok, 0) != 0;  // message holding the tile's first byte
-    int m = (int)fms;
+    int m = (a.debug_skip & 128) ? 0 : (int)fms;  // (diagnostic 128: chain 0 as is)
     aux[64 + l] = 0;
     if (pre_ok && E < fms) {
       aux[l] = tm;
       lane_handoff();
+      uint64_t* fix = aux + 64;
+      int p = (int)E, cur = (int)E >> 6, steps = 0;
+      uint64_t fm = 0;
+      bool done = true;
       if (l == 0 && !(a.debug_skip & 128)) {  // (diagnostic: 128 skips the patch walk)
         // the reads of a step are independent (one LDS round trip per record); the walked
         // starts of a sub-tile collect in a register until the walk leaves it
-        int p = (int)E;
-        uint64_t* fix = aux + 64;
-        int cur = p >> 6;
-        uint64_t fm = 0;
-        while (p < (int)fms && p < kB) {
+        done = false;
+        while (p < (int)fms && p < kB && steps < kMergeCap) {
           const uint64_t mk = aux[p >> 6];
           const uint32_t tg = d[p], c9 = d[p + 9];
           asm volatile("" ::"v"(tg), "v"(c9));
@@ -1258,7 +1259,43 @@ __device__ __forceinline__ void expand_tile(const UnpackArgs& a, uint64_t t, con
           }
           fm |= 1ull << (p & 63);
           p += rec_len(tg, c9);
+          steps++;
         }
+        done = steps < kMergeCap;
+      }
+      if (!readlane32(done, 0)) {
+        // rare: the entry's chain runs on beside chain 0 (as in index_kernel's merge table):
+        // continue by jumping along each sub-tile's second chain B, all lanes in step with
+        // lane 0's walk (its position is uniform, so the lookups are readlanes)
+        p = (int)readlane32((uint32_t)p, 0);
+        cur = (int)readlane32((uint32_t)cur, 0);
+        fm = readlane64(fm, 0);
+        const SubTile st = make_subtile(A, a.nbytes, msw, kB + kPad);
+        const uint64_t vm = st.vend <= st.s ? 0ull : (st.vend >= st.s + 64 ? ~0ull
+                                                                         : mask_lt(st.vend - st.s));
+        const uint64_t notA = ~tm & vm;
+        uint64_t chB = 0;
+        int xB = kDead;
+        if (notA) xB = walk(d, st, st.s + lowest_bit(notA), tm, &chB);
+        for (int k = 0; k < 2 * kB && p < (int)fms && p < kB; k++) {
+          const int j = p >> 6, b = p & 63;
+          if ((readlane64(tm, j) >> b) & 1) break;
+          if (j != cur) {
+            if (l == 0) fix[cur] = fm;
+            fm = 0;
+            cur = j;
+          }
+          const uint64_t Bj = readlane64(chB, j);
+          if ((Bj >> b) & 1) {
+            fm |= Bj & ~mask_lt(b);
+            p = (int)readlane32((uint32_t)xB, j);
+          } else {
+            fm |= 1ull << b;
+            p += rec_len(d[p], d[p + 9]);
+          }
+        }
+      }
+      if (l == 0 && !(a.debug_skip & 128)) {
         fix[cur] = fm;
         m = p < (int)fms ? p : (int)fms;
       }
