@@ -258,6 +258,7 @@ struct UnpackScratch {
   uint64_t* desc;
   uint64_t* gdesc;
   uint64_t* tile_first;
+  uint64_t* tile_firstpos;
   uint64_t* flat;
   int32_t* hdr_status;
   uint32_t* fail_list;
@@ -293,6 +294,7 @@ UnpackScratch carve_unpack(void* base, uint64_t ntiles, uint64_t n) {
   s.desc = c.take<uint64_t>(ntiles);
   s.gdesc = c.take<uint64_t>((ntiles + 63) / 64);
   s.tile_first = c.take<uint64_t>(ntiles);
+  s.tile_firstpos = c.take<uint64_t>(ntiles);
   s.flat = c.take<uint64_t>(n + 1);
   s.hdr_status = c.take<int32_t>(n);
   s.fail_list = c.take<uint32_t>(n);
@@ -339,6 +341,7 @@ cpk_status unpack_common(cpk_ctx* ctx, uint32_t mode, const uint8_t* d_packed, u
   tf.ntiles = ntiles;
   tf.T = B;
   tf.out = s.tile_first;
+  tf.outpos = s.tile_firstpos;
   if (mode == 0) {
     if (!d_word_off_out) return CPK_ERR_INVALID_ARGUMENT;
     if (n == 0) return hip_status(cpk::launch_fill(d_word_off_out, 8, 0, stream));
@@ -361,6 +364,7 @@ cpk_status unpack_common(cpk_ctx* ctx, uint32_t mode, const uint8_t* d_packed, u
   a.in_off = d_in_off;
   a.nmsgs = n;
   a.tile_first = s.tile_first;
+  a.tile_firstpos = s.tile_firstpos;
   a.word_off = mode == 2 ? nullptr : word_off;
   a.hdr_status = mode == 0 ? s.hdr_status : nullptr;
   a.words = d_words;

@@ -195,6 +195,7 @@ __device__ __forceinline__ bool run_tile_first(const TileFirstJob& tf, uint32_t 
       else hi = mid;
     }
     tf.out[t] = lo;
+    if (tf.outpos) tf.outpos[t] = lo <= tf.npos ? tf.pos[lo] : ~0ull;
   }
   return true;
 }

@@ -58,6 +58,7 @@ struct TileFirstJob {
   const uint64_t* pos;
   uint64_t npos, ntiles, T;
   uint64_t* out;
+  uint64_t* outpos = nullptr;  // optional: pos[out[t]] (~0 past the end)
 };
 hipError_t launch_message_bits(const uint64_t* words, const uint64_t* off, uint64_t n,
                                uint64_t* bits, int32_t* status, const TileFirstJob& tf,
@@ -109,6 +110,7 @@ struct UnpackArgs {
   uint64_t* g_notok;            // per 64 tiles: optimistic entry did not merge
   uint64_t* g_start;            // per 64 tiles: tile holds a message start
   uint32_t* t_ent;              // true entry (tile-relative)
+  const uint64_t* tile_firstpos;  // in_off[tile_first[t]]: the first message start >= tile start
 };
 
 // Unpack stages (launch_unpack_stage), in launch order.

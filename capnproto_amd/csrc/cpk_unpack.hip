@@ -726,16 +726,31 @@ __global__ __launch_bounds__(64 * kIndexWaves) void index_kernel(UnpackArgs a) {
   const uint64_t P = a.nbytes;
   const uint64_t A = t * kB;
 
+  // this tile's and the next tile's first message (and where it starts), with the tile's bytes:
+  // a tile holding at most one message start (the batch end counts) needs no message window
+  const bool lastt = t + 1 >= a.ntiles;
+  const uint64_t mf0 = a.tile_first[t], mf1 = lastt ? a.nmsgs + 1 : a.tile_first[t + 1];
+  const uint64_t fp0 = a.tile_firstpos[t], fp1 = lastt ? ~0ull : a.tile_firstpos[t + 1];
   Staged stg;
   stage_load(a, A, stg);
-  const uint64_t mfirst = uniform64(a.tile_first[t]);
+  const uint64_t mfirst = uniform64(mf0);
+  const uint64_t nstarts = uniform64(mf1) - mfirst;
   stm.mark(0);
   if constexpr (kRow == 64) stage_store(stg, d);
   else stage_store_rows(stg, d);
   stm.mark(1);
   int nms_tile_after;
-  (void)tile_msg_starts(a, A, mfirst, lds_ms[wv], &nms_tile_after, nullptr);
-  const SubTile st = make_subtile(A, P, lds_ms[wv][l], nms_tile_after);
+  uint64_t msw;
+  if (nstarts <= 1) {
+    const uint64_t f0 = uniform64(fp0), f1 = uniform64(fp1);
+    const uint64_t after = nstarts ? f1 : f0;  // first start at or after the tile end
+    nms_tile_after = (int)((after < P ? after : P) - A);
+    msw = (nstarts && (f0 - A) >> 6 == (uint64_t)l) ? 1ull << ((f0 - A) & 63) : 0ull;
+  } else {
+    (void)tile_msg_starts(a, A, mfirst, lds_ms[wv], &nms_tile_after, nullptr);
+    msw = lds_ms[wv][l];
+  }
+  const SubTile st = make_subtile(A, P, msw, nms_tile_after);
   stm.mark(2);
 
   // ---- chain 0: speculative walks, then the lane fixed point for entry 0 --------------------
