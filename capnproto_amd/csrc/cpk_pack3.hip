@@ -45,6 +45,10 @@ constexpr int kT = 64 * kK;            // words per tile
 // then one trash dword per lane for the stores a lane does not need.
 constexpr int kStgCap = 10 * kT;
 constexpr int kSlotDw = (16 + kStgCap + 48) / 4;  // the staging slot, in dwords
+#ifndef CPK_P3_SEL_AHEAD
+#define CPK_P3_SEL_AHEAD 1
+#endif
+constexpr bool kSelAhead = CPK_P3_SEL_AHEAD != 0;
 
 __device__ __forceinline__ uint32_t tag_of(uint32_t lo, uint32_t hi) {
   const uint32_t m7 = 0x7f7f7f7fu;
@@ -147,16 +151,21 @@ __device__ __forceinline__ void flush_slot(const PackTileArgs& a, uint32_t* stg,
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   const uint8_t* const sb = (const uint8_t*)stg;
   if (n) {
-    const uint64_t A0 = (uint64_t)(uintptr_t)a.out + dst;
+    // global pointers (a.out + offset), never through an integer: a pointer rebuilt from an
+    // integer is generic, and flat stores count against lgkmcnt, so every LDS wait behind them
+    // (the emission that follows) would have to wait for the stores as well
+    uint8_t* const o0 = a.out + dst;
+    const uint64_t A0 = (uint64_t)(uintptr_t)o0;
     const uint64_t A1 = A0 + n;
     const uint64_t al = (A0 + 15) & ~15ull;
-    const uint64_t hl = al < A1 ? al : A1;
-    if (A0 + l < hl) *(uint8_t*)(uintptr_t)(A0 + l) = sb[16 + l];
+    const uint32_t head = (uint32_t)((al < A1 ? al : A1) - A0);  // bytes before 16-byte alignment
+    if ((uint32_t)l < head) o0[l] = sb[16 + l];
     if (A1 > al) {
-      const uint64_t top = A1 & ~15ull;
-      const uint32_t nblk = (uint32_t)((top - al) >> 4);
-      const uint32_t so0 = 16u + (uint32_t)(al - A0);
+      const uint32_t body = (uint32_t)((A1 & ~15ull) - A0);  // end of the aligned stores
+      const uint32_t nblk = (body - head) >> 4;
+      const uint32_t so0 = 16u + head;
       const uint32_t rr = so0 & 3u;
+      u32x4* const ob = (u32x4*)(o0 + head);
       for (uint32_t i = l; i < nblk; i += 64) {
         const uint32_t d = (so0 >> 2) + 4 * i;
         const uint32_t v0 = stg[d], v1 = stg[d + 1], v2 = stg[d + 2], v3 = stg[d + 3],
@@ -166,9 +175,9 @@ __device__ __forceinline__ void flush_slot(const PackTileArgs& a, uint32_t* stg,
         v.y = __builtin_amdgcn_alignbyte(v2, v1, rr);
         v.z = __builtin_amdgcn_alignbyte(v3, v2, rr);
         v.w = __builtin_amdgcn_alignbyte(v4, v3, rr);
-        *(u32x4*)(uintptr_t)(al + 16ull * i) = v;
+        ob[i] = v;
       }
-      if (top + l < A1) *(uint8_t*)(uintptr_t)(top + l) = sb[16 + (uint32_t)(top - A0) + l];
+      if (body + (uint32_t)l < n) o0[body + l] = sb[16 + body + l];
     }
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -420,10 +429,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void p
       uint32_t na = s0 & 3u;   // bytes of that dword before the pending ones (0 = none)
       uint32_t acc = 0;
       const uint32_t lbase = (uint32_t)(kK * l);
+      // the selector of word k + 1 is read before word k's stores (kSelAhead): the wait for it
+      // then covers only the read, not the stores behind it
+      uint64_t sel_next = kSelAhead ? sel_tab[tags[0] & 0xffu] : 0;
 #pragma unroll
       for (int k = 0; k < kK; k++) {
         const uint32_t lo = xlo[k], hi = xhi[k];
         const uint32_t tg = (tags[k >> 2] >> (8 * (k & 3))) & 0xffu;
+        uint64_t sel;
+        if (kSelAhead) {
+          sel = sel_next;
+          if (k + 1 < kK) sel_next = sel_tab[(tags[(k + 1) >> 2] >> (8 * ((k + 1) & 3))) & 0xffu];
+        } else {
+          sel = sel_tab[tg];
+        }
         const uint32_t nz = __popc(tg);
         const bool cvk = (cv.cov >> k) & 1, zhk = (cv.zh >> k) & 1, fhk = (cv.fh >> k) & 1;
         const bool vk = (V >> k) & 1;
@@ -431,7 +450,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void p
         const uint32_t after = SY & (0xfffeu << k);
         const uint32_t ns = after ? lbase + (uint32_t)__builtin_ctz(after) : nsl;
         const uint32_t cnt = min(ns - (lbase + (uint32_t)k) - 1u, 255u);
-        const uint64_t sel = sel_tab[tg];
         const uint32_t c8 = cnt << 8;
         uint32_t r0 = __builtin_amdgcn_perm(hi, lo, (uint32_t)sel) | tg | (zhk ? c8 : 0u);
         uint32_t r1 = __builtin_amdgcn_perm(hi, lo, (uint32_t)(sel >> 32));
