@@ -49,6 +49,10 @@ constexpr int kSlotDw = (16 + kStgCap + 48) / 4;  // the staging slot, in dwords
 #define CPK_P3_SEL_AHEAD 1
 #endif
 constexpr bool kSelAhead = CPK_P3_SEL_AHEAD != 0;
+#ifndef CPK_P3_EMIT2
+#define CPK_P3_EMIT2 1
+#endif
+constexpr bool kEmit2 = CPK_P3_EMIT2 != 0;
 
 __device__ __forceinline__ uint32_t tag_of(uint32_t lo, uint32_t hi) {
   const uint32_t m7 = 0x7f7f7f7fu;
@@ -243,14 +247,14 @@ __device__ __forceinline__ void finish3(const PackTileArgs& a, uint32_t* wst, co
 template <bool STAMPS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void pack3_kernel(
     PackTileArgs a) {
-  // per wave: the staging slot, then one trash dword per lane
-  __shared__ __attribute__((aligned(16))) uint32_t stg_all[4][kSlotDw + 64];
+  // per wave: the staging slot, then four trash dwords per lane
+  __shared__ __attribute__((aligned(16))) uint32_t stg_all[4][kSlotDw + 256];
   __shared__ uint64_t sel_tab[256];
   const int l = lane_id();
   const int wv = (int)uniform32(threadIdx.x >> 6);
   uint32_t* const wst = stg_all[wv];
   sel_tab[threadIdx.x] = make_sel(threadIdx.x);
-  for (int i = l; i < (kSlotDw + 64) / 4; i += 64) ((u32x4*)wst)[i] = (u32x4){0, 0, 0, 0};
+  for (int i = l; i < (kSlotDw + 256) / 4; i += 64) ((u32x4*)wst)[i] = (u32x4){0, 0, 0, 0};
   __syncthreads();
   const uint64_t nwaves = (uint64_t)gridDim.x * 4;
   const uint64_t N = a.nwords;
@@ -486,10 +490,57 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void p
       if (na) atomicOr(stg + pos, acc);  // the last partial dword (the next lane may share it)
     };
 
+    // Offset-indexed emission (kEmit2): every record is OR-ed into the slot at its own byte
+    // offset, up to 4 dwords (bytes past a record are zero, so OR-ing a whole window never
+    // disturbs a neighbour's bytes, and the slot is zero before a tile is staged) -- no byte carry
+    // runs from one record to the next, and the windows' dwords are immediate offsets from one
+    // address.  Words past the batch end are zero, not covered and not heads: they OR zeros.
+    auto emit2 = [&](uint32_t* stg) {
+      uint32_t o = 16u + loff;  // slot byte of the lane's next record
+      const uint32_t lbase = (uint32_t)(kK * l);
+      uint64_t sel_next = sel_tab[tags[0] & 0xffu];
+#pragma unroll
+      for (int k = 0; k < kK; k++) {
+        const uint32_t lo = xlo[k], hi = xhi[k];
+        const uint32_t tg = (tags[k >> 2] >> (8 * (k & 3))) & 0xffu;
+        const uint64_t sel = sel_next;
+        if (k + 1 < kK) sel_next = sel_tab[(tags[(k + 1) >> 2] >> (8 * ((k + 1) & 3))) & 0xffu];
+        const uint32_t nz = ((k < 8 ? nzA >> (4 * k) : nzB >> (4 * (k - 8)))) & 15u;
+        const bool cvk = (cv.cov >> k) & 1, zhk = (cv.zh >> k) & 1, fhk = (cv.fh >> k) & 1;
+        const uint32_t after = SY & (0xfffeu << k);
+        const uint32_t ns = after ? lbase + (uint32_t)__builtin_ctz(after) : nsl;
+        const uint32_t c8 = min(ns - (lbase + (uint32_t)k) - 1u, 255u) << 8;
+        uint32_t r0 = __builtin_amdgcn_perm(hi, lo, (uint32_t)sel) | tg | (zhk ? c8 : 0u);
+        uint32_t r1 = __builtin_amdgcn_perm(hi, lo, (uint32_t)(sel >> 32));
+        uint32_t r2 = fhk ? ((hi >> 24) | c8) : 0u;
+        uint32_t L = 1u + nz + ((zhk || fhk) ? 1u : 0u);
+        if (cvk) {
+          r0 = lo;
+          r1 = hi;
+          r2 = 0;
+          L = ((Rm >> k) & 1) ? 8u : 0u;
+        }
+        const uint32_t sh = 8u * (o & 3u);
+        // an empty record (covered zero word) ORs into the lane's own trash window: a zero
+        // stretch would otherwise put every lane's atomics on the same slot dwords
+        uint32_t* const w = L ? stg + (o >> 2) : wst + kSlotDw + 4 * l;
+        const uint64_t q01 = (((uint64_t)r1 << 32) | r0) << sh;
+        const uint64_t q12 = (((uint64_t)r2 << 32) | r1) << sh;
+        const uint32_t w3 = (uint32_t)(((uint64_t)r2 << sh) >> 32);
+        atomicOr(w, (uint32_t)q01);
+        atomicOr(w + 1, (uint32_t)(q01 >> 32));
+        atomicOr(w + 2, (uint32_t)(q12 >> 32));
+        if (ballot(w3 != 0)) atomicOr(w + 3, w3);
+        o += L;
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+
     // the previous tile: its look-back, stores and positions
     if (p_on) finish3(a, wst, pend);
     stm.mark(6);
-    emit(wst, true, 0u);
+    if (kEmit2) emit2(wst);
+    else emit(wst, true, 0u);
     stm.mark(7);
     pend.t = t;
     pend.agg = agg;
