@@ -141,6 +141,15 @@ __device__ __forceinline__ uint64_t compact_nonzero(uint64_t x) {
 // (it reasons per lane and may otherwise reorder a lane's access past another lane's).
 __device__ __forceinline__ void lane_handoff() { asm volatile("" ::: "memory"); }
 
+// A zero the compiler cannot see through: added to a uniform index, it keeps a load in a VGPR
+// (a uniform load is otherwise moved to SGPRs with v_readfirstlane right behind it, i.e. waited
+// for at once).
+__device__ __forceinline__ uint32_t opaque_zero() {
+  uint32_t z;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+  return z;
+}
+
 // Bit masks.
 __device__ __forceinline__ uint64_t mask_le(int l) { return (2ull << l) - 1; }   // bits 0..l
 __device__ __forceinline__ uint64_t mask_lt(int l) { return (1ull << l) - 1; }   // bits 0..l-1

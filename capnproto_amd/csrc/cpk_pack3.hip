@@ -282,8 +282,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void p
     const uint64_t w0 = tbase + (uint64_t)kK * l;  // the lane's first word
 
     // ---- words: lane l takes words 16l .. 16l+15 of the tile (16-byte loads) ----------------
+    // Every load of a full tile is unconditional and none is waited for here: vector loads
+    // retire in order, and the compiler waits for all of them right behind a load whose value
+    // it moves to an SGPR, or at the join behind a load under a branch.  So uniform values come
+    // through scalar loads (their own counter) and lane-varying guards become clamped addresses
+    // with the value selected afterwards; the partial last tile's loads are waited for inside
+    // its own branch.
     uint32_t xlo[kK], xhi[kK];
-    if (w0 + kK <= N) {
+    if (nvalid == kT) {
       const u32x4* src = (const u32x4*)(a.words + w0);
 #pragma unroll
       for (int i = 0; i < kK / 2; i++) {
@@ -301,17 +307,37 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void p
         xhi[k] = (uint32_t)(x >> 32);
       }
     }
-    const uint64_t cbw = (tbase >> 6) + (uint64_t)(l >> 2) < nbitw
-                             ? a.chunk_bits[(tbase >> 6) + (uint64_t)(l >> 2)] : 0;
-    const uint64_t pw = tbase > 0 ? a.words[tbase - 1] : 0;
+    const uint64_t cbi = (tbase >> 6) + (uint64_t)(l >> 2);
+    const uint64_t cb0 = a.chunk_bits[cbi < nbitw ? cbi : nbitw - 1];
+    // the word before the tile (lane 0 only; a lane-varying address keeps it in a VGPR)
+    const uint64_t pw0 = a.words[l == 0 && tbase > 0 ? tbase - 1 : w0 < N ? w0 : N - 1];
     // first look-ahead words (see below), loaded with the tile
     const uint64_t ga = tend + l;
-    const uint64_t xa = ga < N ? a.words[ga] : 0;
-    const uint64_t ca = (tend >> 6) < nbitw ? a.chunk_bits[tend >> 6] : 0;
+    const uint64_t xa0 = a.words[ga < N ? ga : N - 1];
+    const uint32_t z0 = opaque_zero();
+    const uint64_t cai = (tend >> 6) + z0;
+    const uint64_t ca0 = a.chunk_bits[cai < nbitw ? cai : nbitw - 1];
     // requested positions of the tile (message starts): the first 64, needed at the end
-    const uint64_t pidx = a.pos ? uniform64(a.tile_first[t]) : 0;
-    const uint64_t p0 = (a.pos && pidx + l <= a.npos) ? a.pos[pidx + l] : ~0ull;
+    typedef const __attribute__((address_space(4))) uint64_t cu64;
+    const uint64_t pidx = a.pos ? *((cu64*)a.tile_first + t) : 0;  // scalar load
+    const uint64_t pi = pidx + l;
+    const bool pv = a.pos && pi <= a.npos;
+    const uint64_t p00 = (a.pos ? a.pos : a.words)[pv ? pi : 0];
+    const uint64_t cbw = cbi < nbitw ? cb0 : 0;
+    const uint64_t pw = tbase > 0 ? pw0 : 0;
+    const uint64_t xa = ga < N ? xa0 : 0;
+    const uint64_t ca = cai < nbitw ? ca0 : 0;
+    const uint64_t p0 = pv ? p00 : ~0ull;
     stm.mark(0);
+#if CPK_P3_LOADONLY
+    {  // diagnostic only (no output): the kernel's loads alone
+      uint32_t x = 0;
+      for (int k = 0; k < kK; k++) x ^= xlo[k] ^ xhi[k];
+      x ^= (uint32_t)cbw ^ (uint32_t)pw ^ (uint32_t)xa ^ (uint32_t)ca ^ (uint32_t)p0;
+      if (x == 0x9e3779b9u) a.err[0] = x;
+      continue;
+    }
+#endif
 
     // ---- classes ----------------------------------------------------------------------------
     uint32_t Zm = 0, Rm = 0, Fm = 0, nzsum = 0, nzA = 0, nzB = 0;

@@ -1194,9 +1194,14 @@ __device__ __forceinline__ void expand_fetch(const UnpackArgs& a, uint64_t t, Ex
   f.fms = uniform32(a.t_fms[t]);
   const uint64_t g = t / kGroup;
   const int j = (int)(t - g * kGroup);
-  f.d1 = l < j ? (a.desc[t - 1 - (uint64_t)l] & kDescValue) : 0;
+  // both look-back loads unconditional (clamped addresses): under a branch, the first one got
+  // its wait before the second was issued -- two round trips instead of one
   const int64_t G = (int64_t)g - 1;
-  f.d2 = G - l >= 0 ? (a.gdesc[G - l] & kDescValue) : 0;
+  const bool u1 = l < j, u2 = G - l >= 0;
+  const uint64_t r1 = a.desc[u1 ? t - 1 - (uint64_t)l : t];
+  const uint64_t r2 = a.gdesc[u2 ? (uint64_t)(G - l) : 0];
+  f.d1 = u1 ? (r1 & kDescValue) : 0;
+  f.d2 = u2 ? (r2 & kDescValue) : 0;
 }
 
 // Exclusive (segmented) word prefix of tile t from the final tile / group values of
