@@ -455,21 +455,25 @@ __device__ __forceinline__ void run_jobs(const UnpackArgs& a, const RunJob& job)
     const uint64_t dst = readlane64(job.dst, j);
     const uint64_t src = readlane64(job.src, j);
     const bool raw = readlane32(job.raw, j);
-    for (uint32_t k = l; k < n; k += 64) {
-      uint64_t v = 0;
-      if (raw) {
-        const uint64_t s = src + 8ull * k;
-        const uint64_t al = s & ~7ull;
-        const uint32_t sh = (uint32_t)(s & 7);
-        if (al + 16 <= a.nbytes) {
-          const uint64_t v0 = *(const uint64_t*)(a.packed + al);
-          const uint64_t v1 = *(const uint64_t*)(a.packed + al + 8);
-          v = sh ? (v0 >> (8 * sh)) | (v1 << (64 - 8 * sh)) : v0;
-        } else {
-          v = load_u64_unaligned(a.packed + s);
-        }
+    if (!raw) {
+      for (uint32_t k = l; k < n; k += 64) a.words[dst + k] = 0;
+      continue;
+    }
+    // raw run: every load of a 256-word block is issued before its stores (one round trip per
+    // block instead of one per 64 words), each from a clamped index inside the run's bytes;
+    // the words are unaligned 8-byte loads (the target's unaligned access mode)
+    for (uint32_t k0 = 0; k0 < n; k0 += 256) {
+      uint64_t v[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const uint32_t k = k0 + 64 * i + l;
+        __builtin_memcpy(&v[i], a.packed + src + 8ull * (k < n ? k : n - 1), 8);
       }
-      a.words[dst + k] = v;
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const uint32_t k = k0 + 64 * i + l;
+        if (k < n) a.words[dst + k] = v[i];
+      }
     }
   }
 }
@@ -506,26 +510,24 @@ struct MsgWin {
 };
 
 __device__ __forceinline__ void load_win(const UnpackArgs& a, int64_t mw, MsgWin& w) {
+  // every load unconditional, from a clamped index (entries past the batch select their defaults
+  // afterwards): loads under branches each got their own wait, three round trips in a row
   const int64_t m = mw + lane_id();
+  const bool v = m >= 0 && (uint64_t)m < a.nmsgs;
+  const uint64_t mc = v ? (uint64_t)m : 0;
+  const uint64_t mn = mc + 1 <= a.nmsgs ? mc + 1 : a.nmsgs;
+  const uint64_t* const wo = a.word_off ? a.word_off : a.in_off;
+  const int32_t* const hs = a.hdr_status ? a.hdr_status : (const int32_t*)a.fail_flag;
+  const uint64_t s0 = a.in_off[mc], e0 = a.in_off[mn];
+  const uint64_t b0 = wo[mc], b1 = wo[mn];
+  const int32_t h = hs[mc];
+  const uint32_t ff = a.fail_flag[mc];
   w.mw = mw;
-  if (m >= 0 && (uint64_t)m < a.nmsgs) {
-    w.start = a.in_off[m];
-    w.end = a.in_off[m + 1];
-    if (a.word_off) {
-      w.base = a.word_off[m];
-      w.total = a.word_off[m + 1] - w.base;
-    } else {
-      w.base = 0;
-      w.total = ~0ull >> 2;
-    }
-    w.ok = (a.hdr_status ? a.hdr_status[m] == kOK : 1) && a.fail_flag[m] == 0;
-  } else {
-    w.start = ~0ull;
-    w.end = ~0ull;
-    w.base = 0;
-    w.total = 0;
-    w.ok = 0;
-  }
+  w.start = v ? s0 : ~0ull;
+  w.end = v ? e0 : ~0ull;
+  w.base = v && a.word_off ? b0 : 0;
+  w.total = !v ? 0 : (a.word_off ? b1 - b0 : ~0ull >> 2);
+  w.ok = v && (a.hdr_status ? h == kOK : true) && ff == 0;
 }
 
 // Starts only (index_kernel needs no more of the window).
