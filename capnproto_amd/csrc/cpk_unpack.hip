@@ -445,7 +445,11 @@ __device__ __forceinline__ int32_t handle_record(const UnpackArgs& a, const uint
 }
 
 // Writes the pending runs of a batch with the whole wave (coalesced).
-__device__ __forceinline__ void run_jobs(const UnpackArgs& a, const RunJob& job) {
+// d: the wave's LDS copy of packed bytes [dbase, dbase + dlen): a raw run whose bytes lie inside
+// it is copied from there (no global round trip per run; dlen 0: always from global memory).
+__device__ __forceinline__ void run_jobs(const UnpackArgs& a, const RunJob& job,
+                                         const uint8_t* d = nullptr, uint64_t dbase = 0,
+                                         uint32_t dlen = 0) {
   uint64_t pend = ballot(job.n != 0);
   const int l = lane_id();
   while (pend) {
@@ -457,6 +461,18 @@ __device__ __forceinline__ void run_jobs(const UnpackArgs& a, const RunJob& job)
     const bool raw = readlane32(job.raw, j);
     if (!raw) {
       for (uint32_t k = l; k < n; k += 64) a.words[dst + k] = 0;
+      continue;
+    }
+    if (src >= dbase && src - dbase + 8ull * n + 4 <= dlen) {
+      const uint32_t o0 = (uint32_t)(src - dbase);
+      const uint32_t* const d32 = (const uint32_t*)d;
+      for (uint32_t k = l; k < n; k += 64) {
+        const uint32_t o = o0 + 8 * k, q = o >> 2, sh = o & 3;
+        const uint32_t q0 = d32[q], q1 = d32[q + 1], q2 = d32[q + 2];
+        const uint32_t lo = __builtin_amdgcn_alignbyte(q1, q0, sh);
+        const uint32_t hi = __builtin_amdgcn_alignbyte(q2, q1, sh);
+        a.words[dst + k] = ((uint64_t)hi << 32) | lo;
+      }
       continue;
     }
     // raw run: every load of a 256-word block is issued before its stores (one round trip per
@@ -1451,7 +1467,7 @@ __device__ __forceinline__ void expand_tile(const UnpackArgs& a, uint64_t t, con
           report_end(a, (uint64_t)m, st, job);
         }
       }
-      run_jobs(a, job);
+      run_jobs(a, job, d, A, (uint32_t)(kB + kPad));
       base_key = readlane32(km, 63);
       sum += readlane32(inc, 63);
     }
@@ -1584,7 +1600,7 @@ __device__ __forceinline__ void expand_tile(const UnpackArgs& a, uint64_t t, con
           report_end(a, (uint64_t)m, st, job);
         }
       }
-      run_jobs(a, job);
+      run_jobs(a, job, d, A, (uint32_t)(kB + kPad));
       base_key = readlane32(km, 63);
       sum += readlane32(inc, 63);
       if (msb) {

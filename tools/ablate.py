@@ -10,7 +10,7 @@ import capnproto_amd  # noqa: E402
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "c2"
 n, nseg, sw, prof = {"c2": (4096, 1, 8191, "flat"), "c3": (1 << 18, 1, 511, "flat"),
-                     "c4": (32, 16, 524288, "pointer")}[cfg]
+                     "c4": (32, 16, 524288, "pointer"), "c5": (1 << 19, 1, 0, "mixed")}[cfg]
 codec = capnproto_amd.Codec(0)
 off, total = codec.gen_offsets(n, nseg=nseg, seg_words=sw, seed=20261015)
 words = codec.gen_messages(prof, off, total, nseg=nseg, seed=20261015)
