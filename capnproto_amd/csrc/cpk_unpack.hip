@@ -485,10 +485,13 @@ __device__ __forceinline__ void run_jobs(const UnpackArgs& a, const RunJob& job,
         const uint32_t k = k0 + 64 * i + l;
         __builtin_memcpy(&v[i], a.packed + src + 8ull * (k < n ? k : n - 1), 8);
       }
+      // unconditional stores: a lane past the run end loaded word n - 1 (clamped) and writes
+      // that same value to it again -- a skipped store would leave its load outstanding, and
+      // the next batch would wait for it before reusing the register
 #pragma unroll
       for (int i = 0; i < 4; i++) {
         const uint32_t k = k0 + 64 * i + l;
-        if (k < n) a.words[dst + k] = v[i];
+        a.words[dst + (k < n ? k : n - 1)] = v[i];
       }
     }
   }
