@@ -236,7 +236,11 @@ __device__ __forceinline__ void positions3(const PackTileArgs& a, const Staged3&
 
 // Look-back, stores and positions of a staged tile.
 __device__ __forceinline__ void finish3(const PackTileArgs& a, uint32_t* wst, const Staged3& s) {
+#if CPK_P3_NOLB
+  const uint64_t excl = 0;  // diagnostic only (output wrong): the look-back's share of the time
+#else
   const uint64_t excl = lookback2(a.desc, a.gdesc, s.t, 0, a.err);
+#endif
   publish_incl(a.desc, a.gdesc, s.t, a.ntiles, excl + s.agg);
   const bool over = excl + s.agg > a.out_capacity;
   if (over && lane_id() == 0) raise_error(a.err, kErrCapacity);
