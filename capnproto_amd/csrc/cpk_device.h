@@ -276,13 +276,23 @@ __device__ __forceinline__ uint64_t lookback(const uint64_t* desc, uint64_t t, u
   return excl;
 }
 
+__device__ __forceinline__ uint64_t stamp_now() {
+  // no s_waitcnt: a phase ends where the wave gets to, memory still in flight (forcing the wait
+  // at every mark serialised the loads the phases are meant to overlap)
+  asm volatile("" ::: "memory");
+  const uint64_t t = __builtin_amdgcn_s_memtime();
+  asm volatile("" ::: "memory");
+  return t;
+}
+
 // ---------------------------------------------------------------------------------------------
 // Two-level decoupled look-back.
 //
 // Tiles are grouped 64 to a group.  Every tile publishes its aggregate (AGG) in desc[t]; the
-// last tile of a group to do so (ticket: atomicAdd on gcnt[g]) combines the group's 64
-// aggregates in order and publishes the group aggregate in gdesc[g]; the group's last tile
-// publishes the group's inclusive prefix there once it knows its own.  A tile then needs one
+// group's last tile combines the group's 64 aggregates in order and publishes the group
+// aggregate in gdesc[g] (an arrival ticket instead -- whichever tile counts last -- measured
+// slower: the winner's extra round trip made the group aggregates later), and publishes the
+// group's inclusive prefix there once it knows its own.  A tile then needs one
 // hop over the tiles before it in its group and, unless an inclusive prefix is found there, one
 // hop over up to 64 group descriptors (4096 tiles): with thousands of tiles in flight the
 // inclusive front no longer has to crawl one window per fabric round trip.
@@ -357,7 +367,11 @@ __device__ __forceinline__ void publish_agg(uint64_t* desc, uint64_t* gdesc, uin
 
 // Exclusive prefix of tile t (after publish_agg).  Publishes nothing.
 __device__ __forceinline__ uint64_t lookback2(const uint64_t* desc, const uint64_t* gdesc,
-                                              uint64_t t, uint64_t seg_bit, uint32_t* err) {
+                                              uint64_t t, uint64_t seg_bit, uint32_t* err,
+                                              uint64_t* dbg = nullptr) {
+  // dbg (diagnostic builds only): [0] look-backs that went past the group, [1] group windows
+  // read, [2] cycles in the in-group hop, [3] cycles in the group hops
+  const uint64_t t0 = dbg ? stamp_now() : 0;
   const int l = lane_id();
   const uint64_t g = t / kGroup;
   const int j = (int)(t - g * kGroup);  // predecessors inside the group
@@ -369,13 +383,21 @@ __device__ __forceinline__ uint64_t lookback2(const uint64_t* desc, const uint64
     const uint64_t sb = ballot(stop);
     const int k = sb ? lowest_bit(sb) : j - 1;
     if (j > 0) excl = reduce_nearest(use ? (d & kDescValue) : 0, k, seg_bit);
+    if (dbg) dbg[2] += stamp_now() - t0;
     if (sb || g == 0) return excl & ~seg_bit;
     if (excl & seg_bit) return excl & ~seg_bit;
   }
+  const uint64_t t1 = dbg ? stamp_now() : 0;
+  if (dbg) dbg[0]++;
   // group-level: groups g-1, g-2, ...
   int64_t G = (int64_t)g - 1;
   while (G >= 0) {
+    if (dbg) dbg[1]++;
     const bool use = G - l >= 0;
+    if (dbg) {  // diagnostic: group descriptors not yet published at the first read
+      const uint64_t d0 = use ? load_agent(gdesc + (G - l)) : kDescIncl;
+      dbg[1] += 1000 * (uint64_t)__popcll(ballot((d0 & kDescFlags) == 0));
+    }
     const uint64_t d = load_ready(gdesc + (use ? G - l : 0), use, err);
     const bool stop = !use || ((d & kDescFlags) == kDescIncl) || (seg_bit && (d & seg_bit));
     const uint64_t sb = ballot(stop);
@@ -385,6 +407,7 @@ __device__ __forceinline__ uint64_t lookback2(const uint64_t* desc, const uint64
     if (sb) break;
     G -= 64;
   }
+  if (dbg) dbg[3] += stamp_now() - t1;
   return excl & ~seg_bit;
 }
 
@@ -400,14 +423,6 @@ __device__ __forceinline__ void publish_incl(uint64_t* desc, uint64_t* gdesc, ui
 // Diagnostic phase stamps (env CPK_STAMPS=1 selects a separately instantiated kernel; the
 // production kernels contain no stamp).  Lane 0 adds per-phase s_memtime deltas into its own
 // debug buffer, never into outputs.
-__device__ __forceinline__ uint64_t stamp_now() {
-  // no s_waitcnt: a phase ends where the wave gets to, memory still in flight (forcing the wait
-  // at every mark serialised the loads the phases are meant to overlap)
-  asm volatile("" ::: "memory");
-  const uint64_t t = __builtin_amdgcn_s_memtime();
-  asm volatile("" ::: "memory");
-  return t;
-}
 template <bool ON>
 struct Stamps {
   // deltas accumulate in registers; flush() adds them to the debug buffer once (a global atomic

@@ -235,12 +235,15 @@ __device__ __forceinline__ void positions3(const PackTileArgs& a, const Staged3&
 }
 
 // Look-back, stores and positions of a staged tile.
-__device__ __forceinline__ void finish3(const PackTileArgs& a, uint32_t* wst, const Staged3& s) {
+template <bool STAMPS>
+__device__ __forceinline__ void finish3(const PackTileArgs& a, uint32_t* wst, const Staged3& s,
+                                        Stamps<STAMPS>& stm) {
 #if CPK_P3_NOLB
   const uint64_t excl = 0;  // diagnostic only (output wrong): the look-back's share of the time
 #else
-  const uint64_t excl = lookback2(a.desc, a.gdesc, s.t, 0, a.err);
+  const uint64_t excl = lookback2(a.desc, a.gdesc, s.t, 0, a.err, STAMPS ? stm.acc + 10 : nullptr);
 #endif
+  stm.mark(9);
   publish_incl(a.desc, a.gdesc, s.t, a.ntiles, excl + s.agg);
   const bool over = excl + s.agg > a.out_capacity;
   if (over && lane_id() == 0) raise_error(a.err, kErrCapacity);
@@ -276,7 +279,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void p
   // staged in it.  One extra turn finishes the last tile.
   for (uint64_t t = (uint64_t)blockIdx.x * 4 + wv;; t += nwaves) {
     if (t >= a.ntiles) {
-      if (p_on) finish3(a, wst, pend);
+      if (p_on) finish3(a, wst, pend, stm);
       break;
     }
     stm.restart();
@@ -567,7 +570,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void p
     };
 
     // the previous tile: its look-back, stores and positions
-    if (p_on) finish3(a, wst, pend);
+    if (p_on) finish3(a, wst, pend, stm);
     stm.mark(6);
     if (kEmit2) emit2(wst);
     else emit(wst, true, 0u);
@@ -587,7 +590,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void p
   }
   stm.mark(8);
   if constexpr (STAMPS) {
-    stm.acc[13] = __builtin_amdgcn_s_memrealtime() - rt0;
+    stm.acc[14] = __builtin_amdgcn_s_memrealtime() - rt0;
     stm.acc[15] = 1;
     stm.flush();
   }

@@ -26,10 +26,15 @@ for rep in range(3):
     tm = codec.timing_read_all()
 print(cfg, "pack kernel ms (stamps build):", round(tm["pack"][0], 4))
 waves = out[15] or 1  # acc[15] = 1 per (persistent) wave
-print("wave lifetime us:", round(out[13] / waves / 100, 2))
+print("wave lifetime us:", round(out[14] / waves / 100, 2))
 names = ["loads issue", "classes (+load wait)", "look-ahead", "cover/publish exit", "entry wait",
-         "bytes+publish agg", "finish prev (look-back, flush)", "emission", "tail"]
-tot = sum(out[i] for i in range(9))
+         "bytes+publish agg", "finish prev: flush + positions", "emission", "tail",
+         "finish prev: look-back"]
+tot = sum(out[i] for i in range(10))
 print("cycles/wave", round(tot / waves))
 for i, nm in enumerate(names):
     print(f"  {nm:32s} {out[i] / waves:12.0f}  {100 * out[i] / max(tot, 1):5.1f}%")
+ntiles = (int(off[-1].item()) + 1023) // 1024
+print("tiles", ntiles, "look-backs past the group per tile", round(out[10] / ntiles, 3),
+      "group windows per tile", round(out[11] / ntiles, 3),
+      "in-group hop cycles/tile", round(out[12] / ntiles), "group hop cycles/tile", round(out[13] / ntiles))
