@@ -611,10 +611,18 @@ hipError_t launch_pack_tiles3(const PackTileArgs& a, hipStream_t stream) {
   static const unsigned cap_false = resident_blocks((const void*)pack3_kernel<false>, 256, 0);
   static const unsigned cap_true = resident_blocks((const void*)pack3_kernel<true>, 256, 0);
   const unsigned want = (unsigned)((a.ntiles + 3) / 4);
+  // tuning knob: at most CPK_PACK3_BLOCKS workgroups in the grid (fewer waves in flight)
+  static const unsigned knob = getenv("CPK_PACK3_BLOCKS") ? (unsigned)atoi(getenv("CPK_PACK3_BLOCKS"))
+                                                          : 0u;
+  unsigned ct = cap_true, cf = cap_false;
+  if (knob) {
+    ct = knob < ct ? knob : ct;
+    cf = knob < cf ? knob : cf;
+  }
   if (a.stamps)
-    pack3_kernel<true><<<want < cap_true ? want : cap_true, 256, 0, stream>>>(a);
+    pack3_kernel<true><<<want < ct ? want : ct, 256, 0, stream>>>(a);
   else
-    pack3_kernel<false><<<want < cap_false ? want : cap_false, 256, 0, stream>>>(a);
+    pack3_kernel<false><<<want < cf ? want : cf, 256, 0, stream>>>(a);
   return hipGetLastError();
 }
 
