@@ -127,6 +127,7 @@ struct PackScratch {
   uint64_t* hdesc;
   uint32_t* gcnt;
   uint32_t* state;
+  uint32_t* lead;
   uint64_t* bits;
   uint32_t* scan_counter;
   uint64_t* scan_desc;
@@ -148,6 +149,7 @@ PackScratch carve_pack(void* base, uint64_t N, uint64_t ntiles) {
   s.hdesc = c.take<uint64_t>((ntiles + 4095) / 4096);
   s.gcnt = c.take<uint32_t>((ntiles + 63) / 64);
   s.state = c.take<uint32_t>(ntiles);
+  s.lead = c.take<uint32_t>(ntiles);
   s.bits = c.take<uint64_t>((N + 63) / 64);
   s.scan_counter = c.take<uint32_t>(4);
   s.scan_desc = c.take<uint64_t>(cpk::scan_tiles(ntiles + 1));
@@ -213,6 +215,7 @@ cpk_status pack_common(cpk_ctx* ctx, const uint64_t* d_words, uint64_t N, const 
   a.hdesc = s.hdesc;
   a.gcnt = s.gcnt;
   a.state = s.state;
+  a.lead = s.lead;
   a.tile_b = s.tile_b;
   a.tile_bytes = s.tile_bytes;
   a.tile_off = s.tile_off;

@@ -31,6 +31,7 @@ struct PackTileArgs {
   uint64_t* hdesc;             // per 64-group unit look-back descriptors (cpk_pack3.hip)
   uint32_t* gcnt;              // per group arrival tickets
   uint32_t* state;             // ntiles exit budgets (0x80000000 | budget)
+  uint32_t* lead;              // ntiles first sync word of the tile (0x80000000 | word, kT: none)
   // two-pass form: count pass -> (entry budget, bytes) per tile; scan -> output offsets
   uint32_t* tile_b;
   uint64_t* tile_bytes;

@@ -45,14 +45,6 @@ constexpr int kT = 64 * kK;            // words per tile
 // then one trash dword per lane for the stores a lane does not need.
 constexpr int kStgCap = 10 * kT;
 constexpr int kSlotDw = (16 + kStgCap + 48) / 4;  // the staging slot, in dwords
-#ifndef CPK_P3_SEL_AHEAD
-#define CPK_P3_SEL_AHEAD 1
-#endif
-constexpr bool kSelAhead = CPK_P3_SEL_AHEAD != 0;
-#ifndef CPK_P3_EMIT2
-#define CPK_P3_EMIT2 1
-#endif
-constexpr bool kEmit2 = CPK_P3_EMIT2 != 0;
 
 __device__ __forceinline__ uint32_t tag_of(uint32_t lo, uint32_t hi) {
   const uint32_t m7 = 0x7f7f7f7fu;
@@ -193,6 +185,7 @@ __device__ __forceinline__ void flush_slot(const PackTileArgs& a, uint32_t* stg,
 struct Staged3 {
   uint64_t t, agg, tend, pidx, p0;  // p0: lane l's entry of pos[pidx ..] (loaded early)
   uint32_t loff, heads, rh, crf, nzA, nzB;
+  uint32_t patch;  // 0, or 0x80000000 | (word of the open run's head << 16) | its count byte
 };
 
 // Requested positions (message starts) inside the tile: excl + lane offset + the lane's bytes
@@ -245,6 +238,14 @@ __device__ __forceinline__ void finish3(const PackTileArgs& a, uint32_t* wst, co
 #endif
   stm.mark(9);
   publish_incl(a.desc, a.gdesc, s.t, a.ntiles, excl + s.agg);
+  if (s.patch && s.tend < a.nwords) {
+    // the run open at the tile end: count = words to the first sync (<= 256 past the tile end)
+    const uint32_t lead = wait_nonzero32(a.lead + s.t + 1, a.err) & 0x7fffffffu;
+    const uint32_t h = (s.patch >> 16) & 0x7fffu;
+    const uint32_t cnt = min((uint32_t)kT + min(lead, 256u) - h - 1u, 255u);
+    if (lane_id() == 0) ((uint8_t*)wst)[s.patch & 0xffffu] = (uint8_t)cnt;
+    lane_handoff();
+  }
   const bool over = excl + s.agg > a.out_capacity;
   if (over && lane_id() == 0) raise_error(a.err, kErrCapacity);
   if (!over) flush_slot(a, wst, excl, (uint32_t)s.agg);
@@ -266,7 +267,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void p
   const uint64_t nwaves = (uint64_t)gridDim.x * 4;
   const uint64_t N = a.nwords;
   const uint64_t nbitw = (N + 63) >> 6;
-  const uint32_t trash = (uint32_t)kSlotDw + (uint32_t)l;
   Stamps<STAMPS> stm;
   stm.start(a.stamps);
   uint64_t rt0 = 0;
@@ -318,12 +318,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void p
     const uint64_t cb0 = a.chunk_bits[cbi < nbitw ? cbi : nbitw - 1];
     // the word before the tile (lane 0 only; a lane-varying address keeps it in a VGPR)
     const uint64_t pw0 = a.words[l == 0 && tbase > 0 ? tbase - 1 : w0 < N ? w0 : N - 1];
-    // first look-ahead words (see below), loaded with the tile
-    const uint64_t ga = tend + l;
-    const uint64_t xa0 = a.words[ga < N ? ga : N - 1];
-    const uint32_t z0 = opaque_zero();
-    const uint64_t cai = (tend >> 6) + z0;
-    const uint64_t ca0 = a.chunk_bits[cai < nbitw ? cai : nbitw - 1];
     // requested positions of the tile (message starts): the first 64, needed at the end
     typedef const __attribute__((address_space(4))) uint64_t cu64;
     const uint64_t pidx = a.pos ? *((cu64*)a.tile_first + t) : 0;  // scalar load
@@ -332,15 +326,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void p
     const uint64_t p00 = (a.pos ? a.pos : a.words)[pv ? pi : 0];
     const uint64_t cbw = cbi < nbitw ? cb0 : 0;
     const uint64_t pw = tbase > 0 ? pw0 : 0;
-    const uint64_t xa = ga < N ? xa0 : 0;
-    const uint64_t ca = cai < nbitw ? ca0 : 0;
     const uint64_t p0 = pv ? p00 : ~0ull;
     stm.mark(0);
 #if CPK_P3_LOADONLY
     {  // diagnostic only (no output): the kernel's loads alone
       uint32_t x = 0;
       for (int k = 0; k < kK; k++) x ^= xlo[k] ^ xhi[k];
-      x ^= (uint32_t)cbw ^ (uint32_t)pw ^ (uint32_t)xa ^ (uint32_t)ca ^ (uint32_t)p0;
+      x ^= (uint32_t)cbw ^ (uint32_t)pw ^ (uint32_t)p0;
       if (x == 0x9e3779b9u) a.err[0] = x;
       continue;
     }
@@ -380,51 +372,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void p
     const bool lv = kv >= kK;  // the lane's last word is valid
     stm.mark(1);
 
-    // ---- look-ahead: words from tend to the first sync at / after it (<= 256), for the counts
-    //      of runs still open at the tile end ---------------------------------------------------
-    const int last = nvalid - 1;
-    const int ll = last / kK;
-    const bool lastZ = (readlane32(Zm, ll) >> (last % kK)) & 1;
-    const bool lastR = (readlane32(Rm, ll) >> (last % kK)) & 1;
-    int la = 0;
-    if ((lastZ || lastR) && tend < N) {
-      uint64_t czc = lastZ, crc = lastR;
-      la = 256;
-      uint64_t xk[4] = {xa, 0, 0, 0}, ck[4] = {ca, 0, 0, 0};
-      for (int k = 0; k < 4; k++) {
-        const uint64_t g = tend + 64 * k + l;
-        if (k == 1) {
-          // words 64 .. 255 past the tile together: one round trip instead of three
-#pragma unroll
-          for (int j = 1; j < 4; j++) {
-            const uint64_t gj = tend + 64 * j + l;
-            xk[j] = gj < N ? a.words[gj] : 0;
-            ck[j] = ((tend >> 6) + j < nbitw) ? a.chunk_bits[(tend >> 6) + j] : 0;
-          }
-        }
-        const uint64_t xx = xk[k];
-        const uint32_t tg = tag_of((uint32_t)xx, (uint32_t)(xx >> 32));
-        const uint64_t Vg = ballot(g < N);
-        const uint64_t Cg = uniform64(ck[k]);
-        const uint64_t Zg = ballot(xx == 0) & Vg;
-        const uint64_t Rg = ballot(__popc(tg) >= 7) & Vg;
-        const uint64_t Og = Vg & ~Zg & ~Rg;
-        const uint64_t S = Cg | Og | (Zg & ~((Zg << 1) | czc)) | (Rg & ~((Rg << 1) | crc)) | ~Vg;
-        if (S) {
-          la = 64 * k + lowest_bit(S);
-          break;
-        }
-        czc = Zg >> 63;
-        crc = Rg >> 63;
-      }
-    }
     // first sync at / after the next lane's first word (tile-relative)
     const uint64_t hs = ballot(SY != 0);
     const uint32_t fs = SY ? (uint32_t)__builtin_ctz(SY) : 16u;
     const uint64_t above = hs & ~mask_le(l);
     const int ja = above ? lowest_bit(above) : 0;
     const uint32_t fsa = shfl32(fs, ja);
-    const uint32_t nsl = above ? (uint32_t)(kK * ja) + fsa : (uint32_t)(kT + la);
+    // a run still open at the tile end: its count byte is written as if the batch ended here and
+    // patched at the tile's finish from the next tile's first sync (lead[], published below)
+    const uint32_t nsl = above ? (uint32_t)(kK * ja) + fsa : (uint32_t)kT;
+    {
+      const int L0 = hs ? lowest_bit(hs) : 0;
+      const uint32_t lead = hs ? (uint32_t)(kK * L0) + shfl32(fs, L0) : (uint32_t)kT;
+      if (l == 0) store_agent32(a.lead + t, 0x80000000u | lead);
+    }
     stm.mark(2);
 
     // ---- entry budgets and coverage ----------------------------------------------------------
@@ -459,71 +420,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void p
     stm.mark(5);
 
     // ---- emission: the lane's records as a byte stream at slot byte 16 + (loff - base) -------
-    auto emit = [&](uint32_t* stg, bool mine, uint32_t base) {
-      if (!mine) return;
-      const uint32_t s0 = 16u + loff - base;
-      uint32_t pos = s0 >> 2;  // dword the pending bytes start in
-      uint32_t na = s0 & 3u;   // bytes of that dword before the pending ones (0 = none)
-      uint32_t acc = 0;
-      const uint32_t lbase = (uint32_t)(kK * l);
-      // the selector of word k + 1 is read before word k's stores (kSelAhead): the wait for it
-      // then covers only the read, not the stores behind it
-      uint64_t sel_next = kSelAhead ? sel_tab[tags[0] & 0xffu] : 0;
-#pragma unroll
-      for (int k = 0; k < kK; k++) {
-        const uint32_t lo = xlo[k], hi = xhi[k];
-        const uint32_t tg = (tags[k >> 2] >> (8 * (k & 3))) & 0xffu;
-        uint64_t sel;
-        if (kSelAhead) {
-          sel = sel_next;
-          if (k + 1 < kK) sel_next = sel_tab[(tags[(k + 1) >> 2] >> (8 * ((k + 1) & 3))) & 0xffu];
-        } else {
-          sel = sel_tab[tg];
-        }
-        const uint32_t nz = __popc(tg);
-        const bool cvk = (cv.cov >> k) & 1, zhk = (cv.zh >> k) & 1, fhk = (cv.fh >> k) & 1;
-        const bool vk = (V >> k) & 1;
-        // run count: stretch words after this one, <= 255
-        const uint32_t after = SY & (0xfffeu << k);
-        const uint32_t ns = after ? lbase + (uint32_t)__builtin_ctz(after) : nsl;
-        const uint32_t cnt = min(ns - (lbase + (uint32_t)k) - 1u, 255u);
-        const uint32_t c8 = cnt << 8;
-        uint32_t r0 = __builtin_amdgcn_perm(hi, lo, (uint32_t)sel) | tg | (zhk ? c8 : 0u);
-        uint32_t r1 = __builtin_amdgcn_perm(hi, lo, (uint32_t)(sel >> 32));
-        uint32_t r2 = fhk ? ((hi >> 24) | c8) : 0u;
-        uint32_t L = 1u + nz + ((zhk || fhk) ? 1u : 0u);
-        if (cvk) {
-          r0 = lo;
-          r1 = hi;
-          r2 = 0;
-          L = ((Rm >> k) & 1) ? 8u : 0u;
-        }
-        if (!vk) L = 0;
-        // window: the pending bytes, then the record (<= 13 bytes, 4 dwords)
-        const uint32_t sh = 8u * na;
-        const uint64_t q01 = (((uint64_t)r1 << 32) | r0) << sh;
-        const uint64_t q12 = (((uint64_t)r2 << 32) | r1) << sh;
-        const uint32_t d0 = (uint32_t)q01 | acc;
-        const uint32_t d1 = (uint32_t)(q01 >> 32);
-        const uint32_t d2 = (uint32_t)(q12 >> 32);
-        const uint32_t d3 = (uint32_t)(((uint64_t)r2 << sh) >> 32);
-        const uint32_t nb = na + L;
-        const uint32_t q = nb >> 2;  // whole dwords
-        // d0 may hold the previous lane's last bytes: OR it; d1, d2 are the lane's alone
-        atomicOr(q >= 1u ? stg + pos : wst + trash, q >= 1u ? d0 : 0u);
-        *(q >= 2u ? stg + pos + 1u : wst + trash) = d1;
-        *(q >= 3u ? stg + pos + 2u : wst + trash) = d2;
-        acc = q == 0u ? d0 : (q == 1u ? d1 : (q == 2u ? d2 : d3));
-        na = nb & 3u;
-        pos += q;
-        // keep the iterations apart: hoisting the next words' table reads and counts only
-        // buys register pressure (the stores wait on the LDS anyway)
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      if (na) atomicOr(stg + pos, acc);  // the last partial dword (the next lane may share it)
-    };
-
-    // Offset-indexed emission (kEmit2): every record is OR-ed into the slot at its own byte
+    // Offset-indexed emission: every record is OR-ed into the slot at its own byte
     // offset, up to 4 dwords (bytes past a record are zero, so OR-ing a whole window never
     // disturbs a neighbour's bytes, and the slot is zero before a tile is staged) -- no byte carry
     // runs from one record to the next, and the windows' dwords are immediate offsets from one
@@ -572,8 +469,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void p
     // the previous tile: its look-back, stores and positions
     if (p_on) finish3(a, wst, pend, stm);
     stm.mark(6);
-    if (kEmit2) emit2(wst);
-    else emit(wst, true, 0u);
+    emit2(wst);
     stm.mark(7);
     pend.t = t;
     pend.agg = agg;
@@ -586,6 +482,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void p
     pend.crf = crf;
     pend.nzA = nzA;
     pend.nzB = nzB;
+    {
+      // The one head whose run may still be open at the tile end (no sync after it in the tile,
+      // fewer than 255 words left) got a provisional count (as if the batch ended here): its
+      // word and the slot byte of its count go to the finish, which patches the count from the
+      // next tile's lead.
+      const int hsy = hi_bit16(SY);
+      // heads at or after the lane's last sync (a stretch that starts at it has its head there)
+      const uint32_t hd = (cv.zh | cv.fh) & (0xffffu << (hsy < 0 ? 0 : hsy)) & 0xffffu;
+      const int kk = hi_bit16(hd);
+      const uint32_t h = (uint32_t)(kK * l + kk);
+      const bool mine = above == 0 && hd != 0 && h + 256u > (uint32_t)kT;
+      uint32_t patch = 0;
+      if (mine) {
+        const uint32_t k = (uint32_t)kk, mk = (1u << k) - 1u;
+        const uint32_t mA = k >= 8 ? 0xffffffffu : ((1u << (4 * k)) - 1u);
+        const uint32_t mB = k <= 8 ? 0u : ((1u << (4 * (k - 8))) - 1u);
+        auto nib = [](uint32_t x) {
+          const uint32_t y = (x & 0x0f0f0f0fu) + ((x >> 4) & 0x0f0f0f0fu);
+          return (y * 0x01010101u) >> 24;
+        };
+        const uint32_t before = nib(nzA & mA) + nib(nzB & mB) + __popc(heads & mk) +
+                                __popc(rh & mk) + __popc(crf & mk);
+        patch = 0x80000000u | (h << 16) | (16u + loff + before + (((cv.zh >> k) & 1) ? 1u : 9u));
+      }
+      const uint64_t pm = ballot(mine);
+      pend.patch = pm ? readlane32(patch, lowest_bit(pm)) : 0u;
+    }
     p_on = true;
   }
   stm.mark(8);
