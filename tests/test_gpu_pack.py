@@ -102,6 +102,33 @@ def test_long_runs_across_tiles(codec, oracle):
         assert data == b"".join(oracle.pack_chunk(c) for c in cc), shift
 
 
+def test_runs_open_at_tile_end(codec, oracle):
+    """A zero or raw stretch whose last head sits d words before a 1024-word tile end and that
+    runs on e words into the next tile (the count byte the pack kernel patches from the next
+    tile's first sync), ended by an O word, a family change or a chunk start."""
+    F = np.frombuffer(bytes(range(1, 9)), "<u8")[0]
+    O = np.frombuffer(bytes([1, 2, 0, 0, 5, 0, 0, 0]), "<u8")[0]
+    R1 = np.frombuffer(bytes([1, 2, 0, 4, 5, 6, 7, 8]), "<u8")[0]
+    chunks = []
+    for fill in (0, F):
+        for d in (1, 2, 17, 100, 255, 256, 257, 600):
+            for e in (0, 1, 5, 200, 254, 255, 256, 300):
+                for end in ("O", "fam", "chunk"):
+                    head = np.full(1024 - d, O, "<u8")
+                    run = np.full(d + e, fill, "<u8")
+                    if end == "chunk":
+                        chunks += [np.concatenate([head, run]), np.full(1024 - e, O, "<u8")]
+                        continue
+                    stop = R1 if (end == "fam" and fill == 0) else (np.uint64(0) if end == "fam"
+                                                                     else O)
+                    tail = np.full(1024 - e, O, "<u8")
+                    tail[0] = stop
+                    chunks.append(np.concatenate([head, run, tail]))
+    data, coff = gpu_pack_chunks(codec, chunks)
+    for i, c in enumerate(chunks):
+        assert data[coff[i]:coff[i + 1]] == oracle.pack_chunk(c), i
+
+
 @pytest.mark.parametrize("profile", ["mixed", "bytes", "text"])
 def test_message_batches(codec, oracle, profile):
     rng = np.random.default_rng(99 + len(profile))
