@@ -45,6 +45,7 @@ constexpr int kT = 64 * kK;            // words per tile
 // then one trash dword per lane for the stores a lane does not need.
 constexpr int kStgCap = 10 * kT;
 constexpr int kSlotDw = (16 + kStgCap + 48) / 4;  // the staging slot, in dwords
+constexpr int kTrashDw = 64 + 4;                   // trash windows behind the slot
 
 __device__ __forceinline__ uint32_t tag_of(uint32_t lo, uint32_t hi) {
   const uint32_t m7 = 0x7f7f7f7fu;
@@ -255,14 +256,14 @@ __device__ __forceinline__ void finish3(const PackTileArgs& a, uint32_t* wst, co
 template <bool STAMPS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void pack3_kernel(
     PackTileArgs a) {
-  // per wave: the staging slot, then four trash dwords per lane
-  __shared__ __attribute__((aligned(16))) uint32_t stg_all[4][kSlotDw + 256];
+  // per wave: the staging slot, then the trash windows (lane l: dwords l .. l + 3)
+  __shared__ __attribute__((aligned(16))) uint32_t stg_all[4][kSlotDw + kTrashDw];
   __shared__ uint64_t sel_tab[256];
   const int l = lane_id();
   const int wv = (int)uniform32(threadIdx.x >> 6);
   uint32_t* const wst = stg_all[wv];
   sel_tab[threadIdx.x] = make_sel(threadIdx.x);
-  for (int i = l; i < (kSlotDw + 256) / 4; i += 64) ((u32x4*)wst)[i] = (u32x4){0, 0, 0, 0};
+  for (int i = l; i < (kSlotDw + kTrashDw) / 4; i += 64) ((u32x4*)wst)[i] = (u32x4){0, 0, 0, 0};
   __syncthreads();
   const uint64_t nwaves = (uint64_t)gridDim.x * 4;
   const uint64_t N = a.nwords;
@@ -451,9 +452,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void p
           L = ((Rm >> k) & 1) ? 8u : 0u;
         }
         const uint32_t sh = 8u * (o & 3u);
-        // an empty record (covered zero word) ORs into the lane's own trash window: a zero
-        // stretch would otherwise put every lane's atomics on the same slot dwords
-        uint32_t* const w = L ? stg + (o >> 2) : wst + kSlotDw + 4 * l;
+        // an empty record (covered zero word) ORs into the lane's trash window: a zero stretch
+        // would otherwise put every lane's atomics on the same slot dwords.  The windows overlap
+        // (lane l: dwords l .. l + 3, contents never read), so the 32 lanes of a bank group hit
+        // 32 banks; disjoint windows 4 dwords apart made every such OR a 4-way bank conflict.
+        uint32_t* const w = L ? stg + (o >> 2) : wst + kSlotDw + l;
         const uint64_t q01 = (((uint64_t)r1 << 32) | r0) << sh;
         const uint64_t q12 = (((uint64_t)r2 << 32) | r1) << sh;
         const uint32_t w3 = (uint32_t)(((uint64_t)r2 << sh) >> 32);
