@@ -52,6 +52,9 @@ CONFIGS = {
                workload="C5: 32 Mi mixed-size messages (64 B-16 KiB), round-robin, 4 Mi per GPU"),
 }
 DEBUG_ENV = ("CPK_DEBUG_SKIP", "CPK_STAMPS")
+# kernel-selection knobs: a headline number comes from the default kernels unless --ab is given
+KERNEL_ENV = ("CPK_PACK4", "CPK_PACK3", "CPK_PACK_V2", "CPK_PACK3_BLOCKS", "CPK_PACK_STEPS",
+              "CPK_PACK_PF", "CPK_PACK_TWO_PASS")
 
 
 def parse():
@@ -76,6 +79,8 @@ def parse():
                     help="skip the manifest hash check (the device round trip is still checked)")
     ap.add_argument("--host-inclusive", action="store_true",
                     help="also time the H2D/D2H-inclusive path (reported on stderr)")
+    ap.add_argument("--ab", action="store_true",
+                    help="allow non-default kernel-selection knobs (A/B runs; recorded in 'knobs')")
     return ap.parse_args()
 
 
@@ -455,6 +460,12 @@ def main():
     if bad:
         print(json.dumps({"error": f"diagnostic knob(s) set: {bad}; refusing to report a value"}))
         sys.exit(2)
+    knobs = {k: v for k, v in sorted(os.environ.items()) if k.startswith("CPK_")}
+    sel = [k for k in KERNEL_ENV if k in knobs]
+    if sel and not args.ab:
+        print(json.dumps({"error": f"kernel-selection knob(s) set: {sel}; pass --ab for an A/B "
+                                   "run (the headline comes from the default kernels)"}))
+        sys.exit(2)
     import numpy as np
     import torch
 
@@ -530,6 +541,9 @@ def main():
                                      if cb else ""),
             "roofline": s["roofline"],
             "cpu_baseline": cb,
+            "kernels": {"pack": "pack_tile + scan + pack_place (cpk_pack4.hip)"
+                        if os.environ.get("CPK_PACK4", "1") != "0" else "round-2 A/B kernel",
+                        "knobs": knobs},
         }
         if subs:
             result["sub_results"] = []

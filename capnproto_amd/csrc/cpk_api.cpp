@@ -33,6 +33,11 @@ struct cpk_ctx {
   void* pinned = nullptr;
   size_t pinned_size = 0;
   hipEvent_t meta_ev = nullptr;
+  // calls on different streams share the scratch and the device staging: a call on a stream
+  // other than the previous call's waits for everything enqueued on that stream (order_ev)
+  hipStream_t last_stream = nullptr;
+  bool used = false;
+  hipEvent_t order_ev = nullptr;
   // diagnostics: the last pack call's per-tile tables (cpk_debug_pack_tables)
   uint64_t* dbg_tile_bytes = nullptr;
   uint8_t* dbg_step_b = nullptr;
@@ -120,6 +125,27 @@ struct TimedLaunch {
   }
 };
 
+// Orders this call after the context's previous call when they come on different streams: the
+// scratch, the tile tables and stage[] belong to the context, not to a stream.  (Inside a graph
+// capture the previous stream's work is outside the graph: captured sequences use one stream.)
+cpk_status order_streams(cpk_ctx* ctx, hipStream_t s) {
+  if (ctx->used && s != ctx->last_stream) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cs) != hipSuccess) return CPK_ERR_HIP;
+    if (cs == hipStreamCaptureStatusNone) {
+      if (!ctx->order_ev &&
+          hipEventCreateWithFlags(&ctx->order_ev, hipEventDisableTiming) != hipSuccess)
+        return CPK_ERR_HIP;
+      if (hipEventRecord(ctx->order_ev, ctx->last_stream) != hipSuccess ||
+          hipStreamWaitEvent(s, ctx->order_ev, 0) != hipSuccess)
+        return CPK_ERR_HIP;
+    }
+  }
+  ctx->used = true;
+  ctx->last_stream = s;
+  return CPK_OK;
+}
+
 struct PackScratch {
   uint32_t* counter;
   uint64_t* desc;
@@ -137,6 +163,9 @@ struct PackScratch {
   uint64_t* tile_bytes;
   uint64_t* tile_off;
   uint8_t* step_b;
+  uint32_t* thole;
+  uint32_t* tpatch;
+  uint8_t* scr;
   size_t total;
 };
 
@@ -159,6 +188,9 @@ PackScratch carve_pack(void* base, uint64_t N, uint64_t ntiles) {
   s.tile_bytes = c.take<uint64_t>(ntiles);
   s.tile_off = c.take<uint64_t>(ntiles + 1);
   s.step_b = c.take<uint8_t>(16 * ntiles);
+  s.thole = c.take<uint32_t>(ntiles);
+  s.tpatch = c.take<uint32_t>(ntiles);
+  s.scr = cpk::pack_v4() ? c.take<uint8_t>(ntiles * cpk::kPackScratchBytes + 16) : nullptr;
   s.total = c.off;
   return s;
 }
@@ -172,8 +204,11 @@ cpk_status pack_common(cpk_ctx* ctx, const uint64_t* d_words, uint64_t N, const 
                        uint64_t* d_out_off, int32_t* d_status, hipStream_t stream) {
   if (!ctx || (!d_off && n) || (!d_words && N) || (!d_out && cap)) return CPK_ERR_INVALID_ARGUMENT;
   if (hipSetDevice(ctx->device) != hipSuccess) return CPK_ERR_HIP;
-  const bool v3 = cpk::pack_v3();
-  const uint64_t T = v3 ? 1024 : 64ull * (cpk::pack_v2() ? cpk::pack2_steps() : cpk::pack_steps());
+  if (order_streams(ctx, stream) != CPK_OK) return CPK_ERR_HIP;
+  const bool v4 = cpk::pack_v4();
+  const bool v3 = !v4 && cpk::pack_v3();
+  const uint64_t T = v4 ? cpk::kPackTileWords
+                        : v3 ? 1024 : 64ull * (cpk::pack_v2() ? cpk::pack2_steps() : cpk::pack_steps());
   const uint64_t ntiles = (N + T - 1) / T;
   cpk_status st = ensure(&ctx->scratch, &ctx->scratch_size, pack_scratch_bytes(N, ntiles));
   if (st != CPK_OK) return st;
@@ -220,6 +255,9 @@ cpk_status pack_common(cpk_ctx* ctx, const uint64_t* d_words, uint64_t N, const 
   a.tile_bytes = s.tile_bytes;
   a.tile_off = s.tile_off;
   a.step_b = s.step_b;
+  a.scr = s.scr;
+  a.thole = s.thole;
+  a.tpatch = s.tpatch;
   a.err = ctx->err;
   ctx->dbg_tile_bytes = s.tile_bytes;
   ctx->dbg_step_b = s.step_b;
@@ -228,7 +266,14 @@ cpk_status pack_common(cpk_ctx* ctx, const uint64_t* d_words, uint64_t N, const 
   a.stamps = cpk::debug_stamps(0);
   a.debug_skip = cpk::debug_skip();
   TimedLaunch tl(ctx, 0, stream);
-  if (v3) {
+  if (v4) {
+    // tiles -> scratch slots, scan of the tile byte counts, scratch -> output
+    e = cpk::launch_pack_tiles4(a, stream);
+    if (e == hipSuccess)
+      e = cpk::launch_exclusive_scan(s.tile_bytes, ntiles, s.tile_off, s.scan_counter,
+                                     s.scan_desc, ctx->err, stream);
+    if (e == hipSuccess) e = cpk::launch_pack_place(a, stream);
+  } else if (v3) {
     e = cpk::launch_pack_tiles3(a, stream);
   } else if (cpk::pack_v2()) {
     e = cpk::launch_pack_tiles2(a, stream);
@@ -329,6 +374,7 @@ cpk_status unpack_common(cpk_ctx* ctx, uint32_t mode, const uint8_t* d_packed, u
   if (!ctx || (!d_in_off && n) || (!d_packed && P) || (!d_status && n))
     return CPK_ERR_INVALID_ARGUMENT;
   if (hipSetDevice(ctx->device) != hipSuccess) return CPK_ERR_HIP;
+  if (order_streams(ctx, stream) != CPK_OK) return CPK_ERR_HIP;
   const uint64_t B = cpk::kUnpackTileBytes;
   const uint64_t ntiles = (P + B - 1) / B;
   UnpackScratch probe = carve_unpack(nullptr, ntiles, n);
@@ -482,6 +528,7 @@ cpk_status cpk_destroy(cpk_ctx* ctx) {
     if (ctx->stage[i]) (void)hipFree(ctx->stage[i]);
   if (ctx->pinned) (void)hipHostFree(ctx->pinned);
   if (ctx->meta_ev) (void)hipEventDestroy(ctx->meta_ev);
+  if (ctx->order_ev) (void)hipEventDestroy(ctx->order_ev);
   delete ctx;
   return CPK_OK;
 }
@@ -534,6 +581,7 @@ cpk_status cpk_pack_segments(cpk_ctx* ctx, const uint64_t* const* h_seg_ptrs,
   if (nseg > (1u << 20)) return CPK_ERR_INVALID_ARGUMENT;
   if (hipSetDevice(ctx->device) != hipSuccess) return CPK_ERR_HIP;
   hipStream_t s = (hipStream_t)stream;
+  if (order_streams(ctx, s) != CPK_OK) return CPK_ERR_HIP;
   const uint64_t tw = nseg / 2 + 1;
   // meta: seg_ptr[nseg], chunk_off[nseg + 2], table[tw]
   const uint64_t nmeta = nseg + (nseg + 2) + tw;
@@ -656,6 +704,7 @@ cpk_status cpk_split_packed_stream(cpk_ctx* ctx, const uint8_t* d_packed, uint64
   if (hipSetDevice(ctx->device) != hipSuccess) return CPK_ERR_HIP;
   const uint64_t limit = limits ? limits->traversal_limit_words : 8ull * 1024 * 1024;
   hipStream_t s = (hipStream_t)stream;
+  if (order_streams(ctx, s) != CPK_OK) return CPK_ERR_HIP;
   // the record-head map (one u64 per output word) and 8 words of call state: in_off[2],
   // word_off[2], meta[4] (stop byte, stop word, decode status)
   cpk_status st = ensure(&ctx->stage[3], &ctx->stage_size[3], words_capacity * 8 + 128);

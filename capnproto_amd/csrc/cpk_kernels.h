@@ -7,8 +7,9 @@
 
 namespace cpk {
 
-constexpr int kPackSteps = 16;                  // words per pack tile = 64 * kPackSteps
-constexpr uint64_t kPackTileWords = 64 * kPackSteps;
+constexpr int kPackSteps = 16;                  // step-major kernels (A/B): words per tile / 64
+constexpr uint64_t kPackTileWords = 2048;       // words per workgroup tile (cpk_pack4.hip)
+constexpr uint64_t kPackScratchBytes = 10 * kPackTileWords;  // a tile's packed bytes, worst case
 constexpr uint64_t kUnpackTileBytes = 4096;     // packed bytes per unpack tile (>= 2050)
 
 struct PackTileArgs {
@@ -37,6 +38,11 @@ struct PackTileArgs {
   uint64_t* tile_bytes;
   uint64_t* tile_off;
   uint8_t* step_b;             // two-pass kernels (cpk_pack2.hip): budget entering each step
+  // cpk_pack4.hip: per-tile scratch slots (ntiles * kPackScratchBytes + 16), the byte of a
+  // tile's provisional count (~0: none) and the next tile's final value for it (0x100 | v)
+  uint8_t* scr;
+  uint32_t* thole;
+  uint32_t* tpatch;
   uint32_t* err;
   unsigned long long* stamps;  // diagnostic build only (env CPK_STAMPS), else NULL
   uint32_t debug_skip;         // timing ablations only (env CPK_DEBUG_SKIP): 1 = no look-back
@@ -52,6 +58,10 @@ hipError_t launch_pack_tiles2(const PackTileArgs& a, hipStream_t stream);
 // lane-serial kernel (cpk_pack3.hip): 64 lanes x 16 consecutive words per tile
 bool pack_v3();
 hipError_t launch_pack_tiles3(const PackTileArgs& a, hipStream_t stream);
+// workgroup-tile kernel (cpk_pack4.hip, the default): 4 waves x 64 lanes x 8 consecutive words
+bool pack_v4();
+hipError_t launch_pack_tiles4(const PackTileArgs& a, hipStream_t stream);  // tiles -> scratch
+hipError_t launch_pack_place(const PackTileArgs& a, hipStream_t stream);   // scratch -> out
 hipError_t launch_pack_stage(int stage, const PackTileArgs& a, hipStream_t stream);
 // tile_first (first i with pos[i] >= tile start, per tile) as extra blocks of a prologue
 // kernel: one launch fewer per call.  ntiles == 0: no such job.

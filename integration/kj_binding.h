@@ -57,6 +57,42 @@ class KjIn final : public cpk_capnp::BufferedInputStream {
   kj::BufferedInputStream& k_;
 };
 
+// serialize-packed.h:32-62, the stream-level codec (used by the reference's tests and by `capnp
+// convert`'s flat-packed paths, compiler/capnp.c++:1066-1071, :1130-1132): kj streams in and out,
+// the device codec in between.
+namespace _ {
+
+class PackedOutputStream final : public kj::OutputStream {
+ public:
+  explicit PackedOutputStream(kj::BufferedOutputStream& inner) : out_(inner), packed_(out_) {}
+  void write(kj::ArrayPtr<const kj::byte> data) override {
+    packed_.write(data.begin(), data.size());
+  }
+  // kj/io.c++:109-113: one write() -- one chunk -- per piece
+  void write(kj::ArrayPtr<const kj::ArrayPtr<const kj::byte>> pieces) override {
+    for (auto& p : pieces) write(p);
+  }
+
+ private:
+  KjOut out_;
+  cpk_capnp::_::PackedOutputStream packed_;
+};
+
+class PackedInputStream final : public kj::InputStream {
+ public:
+  explicit PackedInputStream(kj::BufferedInputStream& inner) : in_(inner), packed_(in_) {}
+  size_t tryRead(kj::ArrayPtr<kj::byte> buffer, size_t minBytes) override {
+    return packed_.tryRead(buffer.begin(), minBytes, buffer.size());
+  }
+  void skip(size_t bytes) override { packed_.skip(bytes); }
+
+ private:
+  KjIn in_;
+  cpk_capnp::_::PackedInputStream packed_;
+};
+
+}  // namespace _
+
 // capnp::word and cpk_capnp::word are both eight opaque bytes.
 static_assert(sizeof(capnp::word) == sizeof(cpk_capnp::word), "word size");
 

@@ -1,0 +1,261 @@
+// kj_binding_test.c++ -- reference callers run through the binding (integration/kj_binding.h)
+// with the device codec underneath.  Built by oracle/Makefile.ref against the reference's own
+// kj / capnp objects WITHOUT the reference's serialize-packed.o, so every packed or unpacked byte
+// here comes from libcpk_hip.so; run on the GPU box by tests/test_gpu_binding.py.
+//
+//   1. the expectPacksTo loop of serialize-packed-test.c++:90-195 over its KATs (:202-221, kept as
+//      tests/golden/kats.txt): computeUnpackedSizeInWords, PackedOutputStream::write into a
+//      kj::VectorOutputStream, PackedInputStream::read from a kj::ArrayInputStream, reads through
+//      fragmented buffers (preferredReadSize 1, 2, 4, ...), skip(), five back-to-back copies;
+//   2. writePackedMessage / PackedMessageReader over the reference's fixtures (testdata/binary ->
+//      packed, segmented -> segmented-packed), segments compared with capnp::FlatArrayMessageReader;
+//   3. the addressbook flow of samples/addressbook.c++:47-79: writePackedMessageToFd into a pipe,
+//      PackedMessageReader over kj::FdInputStream, getRoot<AnyPointer>() walked to the two people
+//      the sample writes (ids 123 / 456, names, emails, phone counts).
+//
+//   kj_binding_test <tests/golden dir>     -> prints "binding ok: N checks", exit 0
+#include <capnp/any.h>
+#include <capnp/serialize.h>
+#include <kj/io.h>
+#include <unistd.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <fstream>
+#include <iterator>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "kj_binding.h"
+
+namespace {
+
+int checks = 0;
+
+void check(bool ok, const std::string& what) {
+  ++checks;
+  if (!ok) {
+    std::fprintf(stderr, "FAILED: %s\n", what.c_str());
+    std::exit(1);
+  }
+}
+
+std::vector<kj::byte> read_file(const std::string& path) {
+  std::ifstream f(path, std::ios::binary);
+  check(bool(f), "open " + path);
+  return std::vector<kj::byte>(std::istreambuf_iterator<char>(f), {});
+}
+
+std::vector<kj::byte> unhex(const std::string& s) {
+  std::vector<kj::byte> v;
+  if (s == "-") return v;
+  for (size_t i = 0; i + 1 < s.size(); i += 2) v.push_back((kj::byte)std::stoul(s.substr(i, 2), 0, 16));
+  return v;
+}
+
+// A BufferedInputStream over bytes that hands them out at most `preferred` at a time (the
+// fragmented reads of TestPipe, serialize-packed-test.c++:33-88).
+class FragmentedInput final : public kj::BufferedInputStream {
+ public:
+  FragmentedInput(kj::ArrayPtr<const kj::byte> data, size_t preferred)
+      : data_(data), preferred_(preferred) {}
+  kj::ArrayPtr<const kj::byte> tryGetReadBuffer() override {
+    const size_t n = std::min(preferred_, data_.size() - pos_);
+    return data_.slice(pos_, pos_ + n);
+  }
+  size_t tryRead(kj::ArrayPtr<kj::byte> buffer, size_t minBytes) override {
+    size_t n = 0;
+    while (n < minBytes && pos_ < data_.size()) {
+      const size_t k = std::min({preferred_, data_.size() - pos_, buffer.size() - n});
+      memcpy(buffer.begin() + n, data_.begin() + pos_, k);
+      pos_ += k;
+      n += k;
+    }
+    return n;
+  }
+  void skip(size_t bytes) override { pos_ += bytes; }
+  size_t remaining() const { return data_.size() - pos_; }
+
+ private:
+  kj::ArrayPtr<const kj::byte> data_;
+  size_t preferred_;
+  size_t pos_ = 0;
+};
+
+kj::Array<kj::byte> pack_chunks(const std::vector<kj::byte>& unpacked, int copies) {
+  kj::VectorOutputStream out;
+  {
+    cpk_kj::_::PackedOutputStream packed(out);
+    for (int i = 0; i < copies; i++) packed.write(kj::arrayPtr(unpacked.data(), unpacked.size()));
+  }
+  return kj::heapArray(out.getArray());
+}
+
+// serialize-packed-test.c++:90-195 (expectPacksTo) for one KAT
+void expect_packs_to(const std::vector<kj::byte>& unpacked, const std::vector<kj::byte>& packed,
+                     const std::string& name) {
+  const size_t U = unpacked.size();
+  check(cpk_kj::computeUnpackedSizeInWords(kj::arrayPtr(packed.data(), packed.size())) == U / 8,
+        name + ": computeUnpackedSizeInWords");
+  auto got = pack_chunks(unpacked, 1);
+  check(got.size() == packed.size() && memcmp(got.begin(), packed.data(), packed.size()) == 0,
+        name + ": pack");
+  {
+    kj::ArrayInputStream in(kj::arrayPtr(packed.data(), packed.size()));
+    cpk_kj::_::PackedInputStream pin(in);
+    std::vector<kj::byte> back(U);
+    pin.read(kj::arrayPtr(back.data(), U));
+    check(back == unpacked, name + ": unpack");
+    check(in.tryGetReadBuffer().size() == 0, name + ": unpack consumed the input");
+  }
+  for (size_t pref = 1; pref <= 2 * packed.size() + 1; pref *= 2) {
+    FragmentedInput in(kj::arrayPtr(packed.data(), packed.size()), pref);
+    cpk_kj::_::PackedInputStream pin(in);
+    std::vector<kj::byte> back(U);
+    pin.read(kj::arrayPtr(back.data(), U));
+    check(back == unpacked, name + ": fragmented unpack " + std::to_string(pref));
+    check(in.remaining() == 0, name + ": fragmented unpack consumed " + std::to_string(pref));
+  }
+  {
+    kj::ArrayInputStream in(kj::arrayPtr(packed.data(), packed.size()));
+    cpk_kj::_::PackedInputStream pin(in);
+    pin.skip(U);
+    check(in.tryGetReadBuffer().size() == 0, name + ": skip");
+  }
+  {
+    // five back-to-back writes, read back as five words-long reads
+    auto five = pack_chunks(unpacked, 5);
+    std::vector<kj::byte> want;
+    for (int i = 0; i < 5; i++) want.insert(want.end(), packed.begin(), packed.end());
+    check(five.size() == want.size() && memcmp(five.begin(), want.data(), want.size()) == 0,
+          name + ": five copies packed");
+    kj::ArrayInputStream in(kj::arrayPtr(five.begin(), five.size()));
+    cpk_kj::_::PackedInputStream pin(in);
+    for (int i = 0; i < 5; i++) {
+      std::vector<kj::byte> back(U);
+      pin.read(kj::arrayPtr(back.data(), U));
+      check(back == unpacked, name + ": five copies, copy " + std::to_string(i));
+    }
+  }
+}
+
+// segments of an unpacked (framed) message, as the reference reads them
+struct Flat {
+  std::vector<capnp::word> words;
+  kj::Own<capnp::FlatArrayMessageReader> reader;
+  std::vector<kj::ArrayPtr<const capnp::word>> segs;
+  explicit Flat(const std::vector<kj::byte>& bytes) : words(bytes.size() / 8) {
+    memcpy(words.data(), bytes.data(), bytes.size());
+    reader = kj::heap<capnp::FlatArrayMessageReader>(kj::arrayPtr(words.data(), words.size()));
+    for (uint i = 0;; i++) {
+      auto s = reader->getSegment(i);
+      if (s == nullptr) break;
+      segs.push_back(s);
+    }
+  }
+  kj::ArrayPtr<const kj::ArrayPtr<const capnp::word>> pieces() const {
+    return kj::arrayPtr(segs.data(), segs.size());
+  }
+};
+
+void check_same_segments(capnp::MessageReader& r, const Flat& f, const std::string& name) {
+  for (uint i = 0; i < f.segs.size(); i++) {
+    auto s = r.getSegment(i);
+    check(s.size() == f.segs[i].size() &&
+              memcmp(s.begin(), f.segs[i].begin(), s.size() * sizeof(capnp::word)) == 0,
+          name + ": segment " + std::to_string(i));
+  }
+}
+
+void fixture(const std::string& dir, const std::string& src, const std::string& dst) {
+  auto unpacked = read_file(dir + "/" + src);
+  auto packed = read_file(dir + "/" + dst);
+  Flat f(unpacked);
+  kj::VectorOutputStream out;
+  cpk_kj::writePackedMessage(out, f.pieces());
+  auto got = out.getArray();
+  check(got.size() == packed.size() && memcmp(got.begin(), packed.data(), packed.size()) == 0,
+        src + " -> " + dst + ": writePackedMessage");
+  kj::ArrayInputStream in(kj::arrayPtr(packed.data(), packed.size()));
+  {
+    cpk_kj::PackedMessageReader reader(in);
+    check_same_segments(reader, f, dst + ": PackedMessageReader");
+  }
+  check(in.tryGetReadBuffer().size() == 0, dst + ": reader consumed the message");
+}
+
+// samples/addressbook.capnp: AddressBook { people @0 :List(Person) }; Person { id @0 :UInt32,
+// name @1 :Text, email @2 :Text, phones @3 :List(PhoneNumber), employment union }.
+void addressbook(const std::string& dir) {
+  auto unpacked = read_file(dir + "/addressbook.bin");
+  auto packed = read_file(dir + "/addressbook.packed");
+  Flat f(unpacked);
+  int fds[2];
+  check(pipe(fds) == 0, "pipe");
+  cpk_kj::writePackedMessageToFd(fds[1], f.pieces());  // samples/addressbook.c++:75
+  close(fds[1]);
+  std::vector<kj::byte> wire;
+  {
+    kj::byte buf[4096];
+    ssize_t n;
+    while ((n = ::read(fds[0], buf, sizeof buf)) > 0) wire.insert(wire.end(), buf, buf + n);
+    close(fds[0]);
+  }
+  check(wire == packed, "addressbook: writePackedMessageToFd bytes == the sample's");
+  // samples/addressbook.c++:79 (PackedFdMessageReader message(fd)), over a second pipe
+  check(pipe(fds) == 0, "pipe 2");
+  check(::write(fds[1], packed.data(), packed.size()) == (ssize_t)packed.size(), "pipe write");
+  close(fds[1]);
+  kj::FdInputStream fin(fds[0]);
+  kj::BufferedInputStreamWrapper bin(fin);
+  {
+    cpk_kj::PackedMessageReader message(bin);
+    check_same_segments(message, f, "addressbook: PackedMessageReader");
+    auto book = message.getRoot<capnp::AnyPointer>().getAs<capnp::AnyStruct>();
+    auto people = book.getPointerSection()[0].getAs<capnp::AnyList>().as<capnp::List<capnp::AnyStruct>>();
+    check(people.size() == 2, "addressbook: two people");
+    const uint32_t ids[2] = {123, 456};
+    const char* names[2] = {"Alice", "Bob"};
+    const char* emails[2] = {"alice@example.com", "bob@example.com"};
+    const uint phones[2] = {1, 2};
+    for (uint i = 0; i < 2; i++) {
+      auto p = people[i];
+      auto data = p.getDataSection();
+      uint32_t id;
+      memcpy(&id, data.begin(), 4);
+      check(id == ids[i], "addressbook: person id");
+      auto ptrs = p.getPointerSection();
+      check(std::string(ptrs[1].getAs<capnp::Text>().cStr()) == names[i], "addressbook: name");
+      check(std::string(ptrs[2].getAs<capnp::Text>().cStr()) == emails[i], "addressbook: email");
+      check(ptrs[3].getAs<capnp::AnyList>().size() == phones[i], "addressbook: phones");
+    }
+  }
+  close(fds[0]);
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  if (argc < 2) {
+    std::fprintf(stderr, "usage: %s <tests/golden dir>\n", argv[0]);
+    return 2;
+  }
+  const std::string dir = argv[1];
+  std::ifstream kats(dir + "/kats.txt");
+  check(bool(kats), "kats.txt");
+  std::string line;
+  int k = 0;
+  while (std::getline(kats, line)) {
+    std::istringstream ls(line);
+    std::string u, p;
+    if (!(ls >> u >> p)) continue;
+    expect_packs_to(unhex(u), unhex(p), "kat " + std::to_string(k++));
+  }
+  check(k >= 11, "all KATs read");
+  fixture(dir, "binary", "packed");
+  fixture(dir, "segmented", "segmented-packed");
+  addressbook(dir);
+  std::printf("binding ok: %d checks (%d KATs, 2 fixtures, addressbook)\n", checks, k);
+  return 0;
+}

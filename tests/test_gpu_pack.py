@@ -88,7 +88,7 @@ def test_random_chunks(codec, oracle, profile):
 
 
 def test_long_runs_across_tiles(codec, oracle):
-    """Zero / raw / R' stretches much longer than a tile (1024 words) and a chunk boundary
+    """Zero / raw / R' stretches much longer than a tile (2048 words) and a chunk boundary
     inside them; counts must see past the tile end."""
     F = np.frombuffer(bytes(range(1, 9)), "<u8")[0]
     R1 = np.frombuffer(bytes([1, 2, 0, 4, 5, 6, 7, 8]), "<u8")[0]
@@ -96,32 +96,34 @@ def test_long_runs_across_tiles(codec, oracle):
               np.concatenate([np.full(700, R1, "<u8"), np.full(2000, F, "<u8")]),
               np.zeros(1023, "<u8"), np.zeros(1, "<u8"), np.full(1025, F, "<u8"),
               np.concatenate([[F], np.full(4000, R1, "<u8")])]
-    for shift in (0, 1, 255, 511, 1000):  # move the structure against the tile grid
+    for shift in (0, 1, 255, 511, 1000, 2047):  # move the structure against the tile grid
         cc = [np.zeros(shift, "<u8")] + chunks
         data, coff = gpu_pack_chunks(codec, cc)
         assert data == b"".join(oracle.pack_chunk(c) for c in cc), shift
 
 
-def test_runs_open_at_tile_end(codec, oracle):
-    """A zero or raw stretch whose last head sits d words before a 1024-word tile end and that
-    runs on e words into the next tile (the count byte the pack kernel patches from the next
-    tile's first sync), ended by an O word, a family change or a chunk start."""
+@pytest.mark.parametrize("period", [512, 1024, 2048])
+def test_runs_open_at_tile_end(codec, oracle, period):
+    """A zero or raw stretch whose last head sits d words before a boundary at `period` (the
+    pack kernel's wave: 512 words, workgroup tile: 2048) and that runs on e words past it, ended
+    by an O word, a family change or a chunk start.  Across a tile boundary the count byte of
+    the open run is written by the next tile."""
     F = np.frombuffer(bytes(range(1, 9)), "<u8")[0]
     O = np.frombuffer(bytes([1, 2, 0, 0, 5, 0, 0, 0]), "<u8")[0]
     R1 = np.frombuffer(bytes([1, 2, 0, 4, 5, 6, 7, 8]), "<u8")[0]
     chunks = []
     for fill in (0, F):
-        for d in (1, 2, 17, 100, 255, 256, 257, 600):
+        for d in (1, 2, 17, 100, 255, 256, 257, 500):
             for e in (0, 1, 5, 200, 254, 255, 256, 300):
                 for end in ("O", "fam", "chunk"):
-                    head = np.full(1024 - d, O, "<u8")
+                    head = np.full(period - d, O, "<u8")
                     run = np.full(d + e, fill, "<u8")
                     if end == "chunk":
-                        chunks += [np.concatenate([head, run]), np.full(1024 - e, O, "<u8")]
+                        chunks += [np.concatenate([head, run]), np.full(period - e, O, "<u8")]
                         continue
                     stop = R1 if (end == "fam" and fill == 0) else (np.uint64(0) if end == "fam"
                                                                      else O)
-                    tail = np.full(1024 - e, O, "<u8")
+                    tail = np.full(period - e, O, "<u8")
                     tail[0] = stop
                     chunks.append(np.concatenate([head, run, tail]))
     data, coff = gpu_pack_chunks(codec, chunks)

@@ -30,6 +30,18 @@ def _free_port():
     return p
 
 
+def _global_batch():
+    """The global batch: 12 flat messages (table word + one segment) known to every rank."""
+    rng = np.random.default_rng(7)
+    sizes = rng.integers(1, 300, 12)
+    msgs = []
+    for s in sizes:
+        body = rng.integers(0, 2**63, int(s), dtype=np.uint64)
+        body[rng.random(int(s)) < 0.4] = 0
+        msgs.append(np.concatenate([np.array([int(s) << 32], dtype=np.uint64), body]))
+    return msgs
+
+
 def _worker(rank, world, port, q):
     import torch.distributed as dist
 
@@ -39,14 +51,7 @@ def _worker(rank, world, port, q):
         import pyoracle
 
         o = pyoracle.Oracle()
-        rng = np.random.default_rng(7)
-        # the global batch: 12 flat messages (table word + one segment) known to every rank
-        sizes = rng.integers(1, 300, 12)
-        msgs = []
-        for s in sizes:
-            body = rng.integers(0, 2**63, int(s), dtype=np.uint64)
-            body[rng.random(int(s)) < 0.4] = 0
-            msgs.append(np.concatenate([np.array([int(s) << 32], dtype=np.uint64), body]))
+        msgs = _global_batch()
         first, stride, count = shard_messages(rank, world, len(msgs), "round_robin")
         mine = [msgs[first + stride * i] for i in range(count)]
         off = np.cumsum([0] + [len(m) for m in mine]).astype(np.uint64)
@@ -83,9 +88,18 @@ def test_gloo_world2_shards_and_reduction():
         assert red["ok_all"]
     assert out[0][1]["unpacked_all"] == out[1][1]["unpacked_all"] > 0
     # global placement from the all-gathered per-rank totals: rank 1 starts where rank 0 ends,
-    # and the concatenation is the whole batch's packed stream
+    # and the concatenation is the packed stream of the whole batch in shard order (rank 0's
+    # messages, then rank 1's), packed here on one rank
     (b0, t0, p0), (b1, t1, p1) = out[0][4], out[1][4]
     assert b0 == 0 and b1 == len(p0) and t0 == t1 == len(p0) + len(p1)
+    import pyoracle
+
+    msgs = _global_batch()
+    order = out[0][3] + out[1][3]
+    whole = [msgs[i] for i in order]
+    off = np.cumsum([0] + [len(m) for m in whole]).astype(np.uint64)
+    packed, poff, st = pyoracle.Oracle().pack_batch(np.concatenate(whole), off)
+    assert p0 + p1 == bytes(packed[: int(poff[-1])])
 
 
 @pytest.mark.parametrize("world", [1, 2, 3, 8])
