@@ -537,7 +537,9 @@ cpk_status cpk_reserve(cpk_ctx* ctx, uint64_t max_words, uint64_t max_packed_byt
                        uint64_t max_items) {
   if (!ctx) return CPK_ERR_INVALID_ARGUMENT;
   if (hipSetDevice(ctx->device) != hipSuccess) return CPK_ERR_HIP;
-  const uint64_t pt = (max_words + 63) / 64;  // covers every tile size
+  // the tiles of the kernel that will run (the A/B kernels' smallest tile is 64 words)
+  const uint64_t T = cpk::pack_v4() ? cpk::kPackTileWords : 64;
+  const uint64_t pt = (max_words + T - 1) / T;
   size_t need = pack_scratch_bytes(max_words, pt);
   const uint64_t ut = (max_packed_bytes + cpk::kUnpackTileBytes - 1) / cpk::kUnpackTileBytes;
   const size_t un = carve_unpack(nullptr, ut, max_items).total + 64;

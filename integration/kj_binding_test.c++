@@ -186,7 +186,8 @@ void fixture(const std::string& dir, const std::string& src, const std::string& 
 }
 
 // samples/addressbook.capnp: AddressBook { people @0 :List(Person) }; Person { id @0 :UInt32,
-// name @1 :Text, email @2 :Text, phones @3 :List(PhoneNumber), employment union }.
+// name @1 :Text, email @2 :Text, phones @3 :List(PhoneNumber), employment union } -- id in the
+// data section, name / email / phones the first three pointers.
 void addressbook(const std::string& dir) {
   auto unpacked = read_file(dir + "/addressbook.bin");
   auto packed = read_file(dir + "/addressbook.packed");
@@ -226,9 +227,10 @@ void addressbook(const std::string& dir) {
       memcpy(&id, data.begin(), 4);
       check(id == ids[i], "addressbook: person id");
       auto ptrs = p.getPointerSection();
-      check(std::string(ptrs[1].getAs<capnp::Text>().cStr()) == names[i], "addressbook: name");
-      check(std::string(ptrs[2].getAs<capnp::Text>().cStr()) == emails[i], "addressbook: email");
-      check(ptrs[3].getAs<capnp::AnyList>().size() == phones[i], "addressbook: phones");
+      // pointer section: name, email, phones, then the employment union's school (Alice)
+      check(std::string(ptrs[0].getAs<capnp::Text>().cStr()) == names[i], "addressbook: name");
+      check(std::string(ptrs[1].getAs<capnp::Text>().cStr()) == emails[i], "addressbook: email");
+      check(ptrs[2].getAs<capnp::AnyList>().size() == phones[i], "addressbook: phones");
     }
   }
   close(fds[0]);
