@@ -286,8 +286,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void p
   const uint64_t above = hs & ~mask_le(l);
   const int ja = above ? lowest_bit(above) : 0;
   const uint32_t fsa = shfl32(fs, ja);
+  // the tile's exit, with the raw bit (the run open at the tile end is a raw run when the
+  // tile's last word is not zero), published by the last wave as soon as it is known: right here
+  // when the last wave holds a sync point (its exit is then the tile's, whatever the entry)
+  uint32_t t_exit = 0;
+  auto publish_state = [&](uint32_t ex) {
+    const uint32_t lz = readlane32(Zm >> 7, 63) & 1u;
+    t_exit = ex | ((ex != 0 && !lz) ? 0x100u : 0u);
+    if (l == 0) store_agent32(a.state + T, 0x80000000u | t_exit);
+  };
   {
     const uint32_t exit0 = hs != 0 ? wave_exit(0u, hs, nonsimple, c0.b_out, Zm, Fm) : 0u;
+    if (w == kWv - 1 && hs != 0) publish_state(exit0);
     const int L0 = hs ? lowest_bit(hs) : 0;
     const uint32_t fsl = shfl32(fs, L0);
     const uint32_t fsw = hs ? (uint32_t)(kK * L0) + fsl : (uint32_t)kWW;
@@ -319,14 +329,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void p
     if (first_sync || T == 0) return 0u;
     return wait_nonzero32(a.state + T - 1, a.err) & 0x1ffu;
   };
-  // the tile's exit, with the raw bit (the run open at the tile end is a raw run when the
-  // tile's last word is not zero), published by the last wave as soon as it is known
-  uint32_t t_exit = 0;
-  auto publish_state = [&](uint32_t ex) {
-    const uint32_t lz = readlane32(Zm >> 7, 63) & 1u;
-    t_exit = ex | ((ex != 0 && !lz) ? 0x100u : 0u);
-    if (l == 0) store_agent32(a.state + T, 0x80000000u | t_exit);
-  };
+  const bool last_sync = sum_sync(sm[kWv - 1]);  // the exit went out before barrier A
   uint32_t bT = 0, bw = 0;
   bool have_bT = false;
   if (!serial) {
@@ -336,7 +339,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void p
 #pragma unroll
     for (int v = 0; v < kWv; v++)
       if (sum_sync(sm[v])) js = v;
-    if (js >= 0 && w == kWv - 1) publish_state(sum_exit(sm[js]));
+    if (js >= 0 && !last_sync && w == kWv - 1) publish_state(sum_exit(sm[js]));
     // this wave's entry: the nearest lower wave with a sync point, else the tile's entry
     int jb = -1;
 #pragma unroll
@@ -365,7 +368,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void p
         const uint32_t ex =
             hs != 0 ? sum_exit(sm[v]) : wave_exit(bw, hs, nonsimple, c0.b_out, Zm, Fm);
         if (l == 0) s_sexit[v] = ex;
-        if (v == kWv - 1) publish_state(ex);
+        if (v == kWv - 1 && !last_sync) publish_state(ex);
       }
       __syncthreads();
     }
@@ -518,20 +521,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void p
 }
 
 // ---------------------------------------------------------------------------------------------
-// 2. Placement: one workgroup per tile moves the tile's bytes from its scratch slot to their
-//    final place (out + tile_off[T], from the scan of the tile byte counts), writing the final
-//    count byte of a run the next tile closed, and turns the tile's requested positions into
-//    output offsets.
+// 2. Placement: one wave per tile moves the tile's bytes from its scratch slot to their final
+//    place (out + tile_off[T], from the scan of the tile byte counts), writing the final count
+//    byte of a run the next tile closed, and turns the tile's requested positions into output
+//    offsets.  (A tile's bytes are a few KiB at most: a whole workgroup per tile spent more on
+//    its own start than on the copy.)
 __global__ __launch_bounds__(256) void pack_place_kernel(PackTileArgs a) {
-  const int tid = (int)threadIdx.x;
-  const uint64_t T = blockIdx.x;
+  const int l = lane_id();
+  const uint64_t T = (uint64_t)blockIdx.x * 4 + uniform32(threadIdx.x >> 6);
+  if (T >= a.ntiles) return;
   const uint64_t off = a.tile_off[T];
   const uint32_t n = (uint32_t)(a.tile_off[T + 1] - off);
   const uint64_t total = a.tile_off[a.ntiles];
   if (total > a.out_capacity) {
-    if (T == 0 && tid == 0) raise_error(a.err, kErrCapacity);
+    if (T == 0 && l == 0) raise_error(a.err, kErrCapacity);
   } else if (n) {
-    // count byte patched by the next tile (pos, value) -- lane-uniform
+    // count byte patched by the next tile (position, value) -- wave-uniform
     const uint32_t hole = T + 1 < a.ntiles ? a.thole[T] : 0xffffffffu;
     const uint32_t pv = hole != 0xffffffffu ? a.tpatch[T + 1] : 0u;
     const uint8_t* const src = a.scr + T * (uint64_t)kScr;
@@ -544,7 +549,7 @@ __global__ __launch_bounds__(256) void pack_place_kernel(PackTileArgs a) {
       const uint8_t v = src[j];
       return (pv && j == hole) ? (uint8_t)pv : v;
     };
-    if ((uint32_t)tid < head) o0[tid] = byte_at(tid);
+    if ((uint32_t)l < head) o0[l] = byte_at(l);
     if (A1 > al) {
       const uint32_t body = (uint32_t)((A1 & ~15ull) - A0);
       const uint32_t nblk = (body - head) >> 4;
@@ -553,7 +558,7 @@ __global__ __launch_bounds__(256) void pack_place_kernel(PackTileArgs a) {
       const uint32_t rr = head & 3u;
       const uint32_t* const s32 = (const uint32_t*)src;
       u32x4* const ob = (u32x4*)(o0 + head);
-      for (uint32_t i = tid; i < nblk; i += 256) {
+      for (uint32_t i = l; i < nblk; i += 64) {
         const uint32_t d = (head >> 2) + 4 * i;
         const uint32_t v0 = s32[d], v1 = s32[d + 1], v2 = s32[d + 2], v3 = s32[d + 3],
                        v4 = s32[d + 4];
@@ -573,22 +578,20 @@ __global__ __launch_bounds__(256) void pack_place_kernel(PackTileArgs a) {
         }
         ob[i] = v;
       }
-      if (body + (uint32_t)tid < n) o0[body + tid] = byte_at(body + tid);
+      if (body + (uint32_t)l < n) o0[body + l] = byte_at(body + l);
     }
   }
-  // requested positions: tile-relative offsets (pack_tile) + the tile's output offset
+  // requested positions: tile-relative offsets (pack_tile) + the tile's output offset;
+  // positions at or past the batch end (the last tile's share) take the total
   if (a.pos) {
     const uint64_t i0 = a.tile_first[T];
     const uint64_t i1 = T + 1 < a.ntiles ? a.tile_first[T + 1] : a.npos + 1;
-    const uint64_t tend = (T + 1) * kTW;
-    for (uint64_t i = i0 + tid; i < i1; i += 256) {
-      // positions at or past the batch end (the last tile's share) take the total
+    for (uint64_t i = i0 + l; i < i1; i += 64) {
       if (T + 1 == a.ntiles && a.pos[i] >= a.nwords) a.pos_out[i] = total;
       else a.pos_out[i] += off;
     }
-    (void)tend;
   }
-  if (T + 1 == a.ntiles && tid == 0 && a.total_out) *a.total_out = total;
+  if (T + 1 == a.ntiles && l == 0 && a.total_out) *a.total_out = total;
 }
 
 }  // namespace
@@ -608,7 +611,7 @@ hipError_t launch_pack_tiles4(const PackTileArgs& a, hipStream_t stream) {
 
 hipError_t launch_pack_place(const PackTileArgs& a, hipStream_t stream) {
   if (a.ntiles == 0) return hipSuccess;
-  pack_place_kernel<<<(unsigned)a.ntiles, 256, 0, stream>>>(a);
+  pack_place_kernel<<<(unsigned)((a.ntiles + 3) / 4), 256, 0, stream>>>(a);
   return hipGetLastError();
 }
 
