@@ -52,9 +52,10 @@ CONFIGS = {
                workload="C5: 32 Mi mixed-size messages (64 B-16 KiB), round-robin, 4 Mi per GPU"),
 }
 DEBUG_ENV = ("CPK_DEBUG_SKIP", "CPK_STAMPS")
-# kernel-selection knobs: a headline number comes from the default kernels unless --ab is given
-KERNEL_ENV = ("CPK_PACK4", "CPK_PACK3", "CPK_PACK_V2", "CPK_PACK3_BLOCKS", "CPK_PACK_STEPS",
-              "CPK_PACK_PF", "CPK_PACK_TWO_PASS")
+# kernel-selection knobs (env): a headline number comes from the default kernels unless --ab is
+# given.  None is left in the library (round 2's A/B pack kernels are gone); every CPK_* variable
+# that is set is recorded in the result's "kernels.knobs".
+KERNEL_ENV: tuple = ()
 
 
 def parse():
@@ -541,8 +542,9 @@ def main():
                                      if cb else ""),
             "roofline": s["roofline"],
             "cpu_baseline": cb,
-            "kernels": {"pack": "pack_tile + scan + pack_place (cpk_pack4.hip)"
-                        if os.environ.get("CPK_PACK4", "1") != "0" else "round-2 A/B kernel",
+            "kernels": {"pack": "pack_tile + scan + pack_place (capnproto_amd/csrc/cpk_pack.hip)",
+                        "unpack": "header + scan + index + resolve + expand + fallback "
+                                  "(capnproto_amd/csrc/cpk_unpack.hip)",
                         "knobs": knobs},
         }
         if subs:

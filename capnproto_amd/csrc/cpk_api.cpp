@@ -38,11 +38,6 @@ struct cpk_ctx {
   hipStream_t last_stream = nullptr;
   bool used = false;
   hipEvent_t order_ev = nullptr;
-  // diagnostics: the last pack call's per-tile tables (cpk_debug_pack_tables)
-  uint64_t* dbg_tile_bytes = nullptr;
-  uint8_t* dbg_step_b = nullptr;
-  uint32_t* dbg_tile_b = nullptr;
-  uint64_t dbg_ntiles = 0;
 };
 
 namespace cpk {
@@ -147,50 +142,37 @@ cpk_status order_streams(cpk_ctx* ctx, hipStream_t s) {
 }
 
 struct PackScratch {
-  uint32_t* counter;
-  uint64_t* desc;
-  uint64_t* gdesc;
-  uint64_t* hdesc;
-  uint32_t* gcnt;
   uint32_t* state;
-  uint32_t* lead;
   uint64_t* bits;
   uint32_t* scan_counter;
   uint64_t* scan_desc;
   size_t zero_bytes;
   uint64_t* tile_first;
-  uint32_t* tile_b;
   uint64_t* tile_bytes;
   uint64_t* tile_off;
-  uint8_t* step_b;
   uint32_t* thole;
   uint32_t* tpatch;
   uint8_t* scr;
   size_t total;
 };
 
+// Pack scratch: the zeroed part (exit budgets polled by the next tile, the chunk-start bitmap
+// OR-ed by the framing kernel, the scan's descriptors), then per tile the first requested
+// position, byte count, offset, count-byte patch, and the tile's slot for its packed bytes.
 PackScratch carve_pack(void* base, uint64_t N, uint64_t ntiles) {
   Carve c(base);
   PackScratch s;
-  s.counter = c.take<uint32_t>(4);
-  s.desc = c.take<uint64_t>(ntiles);
-  s.gdesc = c.take<uint64_t>((ntiles + 63) / 64);
-  s.hdesc = c.take<uint64_t>((ntiles + 4095) / 4096);
-  s.gcnt = c.take<uint32_t>((ntiles + 63) / 64);
   s.state = c.take<uint32_t>(ntiles);
-  s.lead = c.take<uint32_t>(ntiles);
   s.bits = c.take<uint64_t>((N + 63) / 64);
   s.scan_counter = c.take<uint32_t>(4);
   s.scan_desc = c.take<uint64_t>(cpk::scan_tiles(ntiles + 1));
   s.zero_bytes = c.off;
   s.tile_first = c.take<uint64_t>(ntiles);
-  s.tile_b = c.take<uint32_t>(ntiles);
   s.tile_bytes = c.take<uint64_t>(ntiles);
   s.tile_off = c.take<uint64_t>(ntiles + 1);
-  s.step_b = c.take<uint8_t>(16 * ntiles);
   s.thole = c.take<uint32_t>(ntiles);
   s.tpatch = c.take<uint32_t>(ntiles);
-  s.scr = cpk::pack_v4() ? c.take<uint8_t>(ntiles * cpk::kPackScratchBytes + 16) : nullptr;
+  s.scr = c.take<uint8_t>(ntiles * cpk::kPackScratchBytes + 16);
   s.total = c.off;
   return s;
 }
@@ -205,10 +187,7 @@ cpk_status pack_common(cpk_ctx* ctx, const uint64_t* d_words, uint64_t N, const 
   if (!ctx || (!d_off && n) || (!d_words && N) || (!d_out && cap)) return CPK_ERR_INVALID_ARGUMENT;
   if (hipSetDevice(ctx->device) != hipSuccess) return CPK_ERR_HIP;
   if (order_streams(ctx, stream) != CPK_OK) return CPK_ERR_HIP;
-  const bool v4 = cpk::pack_v4();
-  const bool v3 = !v4 && cpk::pack_v3();
-  const uint64_t T = v4 ? cpk::kPackTileWords
-                        : v3 ? 1024 : 64ull * (cpk::pack_v2() ? cpk::pack2_steps() : cpk::pack_steps());
+  const uint64_t T = cpk::kPackTileWords;
   const uint64_t ntiles = (N + T - 1) / T;
   cpk_status st = ensure(&ctx->scratch, &ctx->scratch_size, pack_scratch_bytes(N, ntiles));
   if (st != CPK_OK) return st;
@@ -244,55 +223,20 @@ cpk_status pack_common(cpk_ctx* ctx, const uint64_t* d_words, uint64_t N, const 
   a.tile_first = s.tile_first;
   a.pos_out = d_out_off;
   a.total_out = nullptr;
-  a.tile_counter = s.counter;
-  a.desc = s.desc;
-  a.gdesc = s.gdesc;
-  a.hdesc = s.hdesc;
-  a.gcnt = s.gcnt;
   a.state = s.state;
-  a.lead = s.lead;
-  a.tile_b = s.tile_b;
   a.tile_bytes = s.tile_bytes;
   a.tile_off = s.tile_off;
-  a.step_b = s.step_b;
   a.scr = s.scr;
   a.thole = s.thole;
   a.tpatch = s.tpatch;
   a.err = ctx->err;
-  ctx->dbg_tile_bytes = s.tile_bytes;
-  ctx->dbg_step_b = s.step_b;
-  ctx->dbg_tile_b = s.tile_b;
-  ctx->dbg_ntiles = ntiles;
-  a.stamps = cpk::debug_stamps(0);
-  a.debug_skip = cpk::debug_skip();
   TimedLaunch tl(ctx, 0, stream);
-  if (v4) {
-    // tiles -> scratch slots, scan of the tile byte counts, scratch -> output
-    e = cpk::launch_pack_tiles4(a, stream);
-    if (e == hipSuccess)
-      e = cpk::launch_exclusive_scan(s.tile_bytes, ntiles, s.tile_off, s.scan_counter,
-                                     s.scan_desc, ctx->err, stream);
-    if (e == hipSuccess) e = cpk::launch_pack_place(a, stream);
-  } else if (v3) {
-    e = cpk::launch_pack_tiles3(a, stream);
-  } else if (cpk::pack_v2()) {
-    e = cpk::launch_pack_tiles2(a, stream);
-  } else if (cpk::pack_fused() || a.stamps) {  // (stamps: single-pass kernel only)
-    e = cpk::launch_pack_tiles(a, stream);
-  } else {
-    // count pass -> scan of tile byte counts -> emit pass
-    TimedLaunch tc(ctx, 6, stream);
-    e = cpk::launch_pack_stage(0, a, stream);
-    tc.done();
-    if (e == hipSuccess)
-      e = cpk::launch_exclusive_scan(s.tile_bytes, ntiles, s.tile_off, s.scan_counter,
-                                     s.scan_desc, ctx->err, stream);
-    if (e == hipSuccess) {
-      TimedLaunch te(ctx, 7, stream);
-      e = cpk::launch_pack_stage(1, a, stream);
-      te.done();
-    }
-  }
+  // tiles -> scratch slots, scan of the tile byte counts, scratch -> output
+  e = cpk::launch_pack_tiles(a, stream);
+  if (e == hipSuccess)
+    e = cpk::launch_exclusive_scan(s.tile_bytes, ntiles, s.tile_off, s.scan_counter, s.scan_desc,
+                                   ctx->err, stream);
+  if (e == hipSuccess) e = cpk::launch_pack_place(a, stream);
   tl.done();
   return hip_status(e);
 }
@@ -537,9 +481,7 @@ cpk_status cpk_reserve(cpk_ctx* ctx, uint64_t max_words, uint64_t max_packed_byt
                        uint64_t max_items) {
   if (!ctx) return CPK_ERR_INVALID_ARGUMENT;
   if (hipSetDevice(ctx->device) != hipSuccess) return CPK_ERR_HIP;
-  // the tiles of the kernel that will run (the A/B kernels' smallest tile is 64 words)
-  const uint64_t T = cpk::pack_v4() ? cpk::kPackTileWords : 64;
-  const uint64_t pt = (max_words + T - 1) / T;
+  const uint64_t pt = (max_words + cpk::kPackTileWords - 1) / cpk::kPackTileWords;
   size_t need = pack_scratch_bytes(max_words, pt);
   const uint64_t ut = (max_packed_bytes + cpk::kUnpackTileBytes - 1) / cpk::kUnpackTileBytes;
   const size_t un = carve_unpack(nullptr, ut, max_items).total + 64;
@@ -996,18 +938,6 @@ cpk_status cpk_unpacked_size_host(cpk_ctx* ctx, const uint8_t* h_packed, uint64_
 }
 
 // Diagnostic (not in include/cpk.h): the last pack call's per-tile tables (two-pass kernels).
-extern "C" cpk_status cpk_debug_pack_tables(cpk_ctx* ctx, uint64_t* bytes, uint32_t* tile_b,
-                                            uint8_t* step_b, uint64_t n) {
-  if (!ctx || !ctx->dbg_tile_bytes || n > ctx->dbg_ntiles) return CPK_ERR_INVALID_ARGUMENT;
-  if (hipDeviceSynchronize() != hipSuccess) return CPK_ERR_HIP;
-  if (hipMemcpy(bytes, ctx->dbg_tile_bytes, 8 * n, hipMemcpyDeviceToHost) != hipSuccess ||
-      hipMemcpy(tile_b, ctx->dbg_tile_b, 4 * n, hipMemcpyDeviceToHost) != hipSuccess ||
-      hipMemcpy(step_b, ctx->dbg_step_b, 16 * n, hipMemcpyDeviceToHost) != hipSuccess)
-    return CPK_ERR_HIP;
-  return CPK_OK;
-}
-
-// Diagnostic (not in include/cpk.h): copies and clears the phase-stamp sums (CPK_STAMPS=1).
 extern "C" cpk_status cpk_debug_stamps(int which, uint64_t* out16) {
   unsigned long long* b = cpk::debug_stamps(which);
   if (!b || !out16) return CPK_ERR_INVALID_ARGUMENT;

@@ -7,8 +7,7 @@
 
 namespace cpk {
 
-constexpr int kPackSteps = 16;                  // step-major kernels (A/B): words per tile / 64
-constexpr uint64_t kPackTileWords = 2048;       // words per workgroup tile (cpk_pack4.hip)
+constexpr uint64_t kPackTileWords = 2048;       // words per workgroup tile (cpk_pack.hip)
 constexpr uint64_t kPackScratchBytes = 10 * kPackTileWords;  // a tile's packed bytes, worst case
 constexpr uint64_t kUnpackTileBytes = 4096;     // packed bytes per unpack tile (>= 2050)
 
@@ -25,44 +24,20 @@ struct PackTileArgs {
   const uint64_t* tile_first;  // per tile: first i with pos[i] >= tile start
   uint64_t* pos_out;
   uint64_t* total_out;         // optional: total packed bytes
-  // scratch (zeroed before the launch)
-  uint32_t* tile_counter;
-  uint64_t* desc;              // ntiles look-back descriptors
-  uint64_t* gdesc;             // per 64-tile group look-back descriptors
-  uint64_t* hdesc;             // per 64-group unit look-back descriptors (cpk_pack3.hip)
-  uint32_t* gcnt;              // per group arrival tickets
-  uint32_t* state;             // ntiles exit budgets (0x80000000 | budget)
-  uint32_t* lead;              // ntiles first sync word of the tile (0x80000000 | word, kT: none)
-  // two-pass form: count pass -> (entry budget, bytes) per tile; scan -> output offsets
-  uint32_t* tile_b;
-  uint64_t* tile_bytes;
-  uint64_t* tile_off;
-  uint8_t* step_b;             // two-pass kernels (cpk_pack2.hip): budget entering each step
-  // cpk_pack4.hip: per-tile scratch slots (ntiles * kPackScratchBytes + 16), the byte of a
-  // tile's provisional count (~0: none) and the next tile's final value for it (0x100 | v)
-  uint8_t* scr;
-  uint32_t* thole;
-  uint32_t* tpatch;
+  // scratch
+  uint32_t* state;             // ntiles exit budgets (0x80000000 | raw << 8 | budget), zeroed
+  uint64_t* tile_bytes;        // ntiles packed bytes per tile
+  uint64_t* tile_off;          // ntiles + 1: their exclusive scan
+  uint8_t* scr;                // per-tile slots (ntiles * kPackScratchBytes + 16)
+  uint32_t* thole;             // byte of a tile's provisional count (~0: none)
+  uint32_t* tpatch;            // the next tile's final value for it (0x100 | v; 0: none)
   uint32_t* err;
-  unsigned long long* stamps;  // diagnostic build only (env CPK_STAMPS), else NULL
-  uint32_t debug_skip;         // timing ablations only (env CPK_DEBUG_SKIP): 1 = no look-back
 };
 
-int pack_steps();  // words per pack tile = 64 * pack_steps()
-bool pack_fused();  // single-pass kernel (default) or count + emit (A/B knob CPK_PACK_TWO_PASS=1)
+// tiles -> scratch slots (tile_bytes, thole, tpatch), then (after the scan of tile_bytes into
+// tile_off) scratch -> out
 hipError_t launch_pack_tiles(const PackTileArgs& a, hipStream_t stream);
-// single-sweep pack kernel (cpk_pack2.hip, the default; CPK_PACK_V1=1 selects the kernels above)
-int pack2_steps();  // words per tile = 64 * pack2_steps()
-bool pack_v2();
-hipError_t launch_pack_tiles2(const PackTileArgs& a, hipStream_t stream);
-// lane-serial kernel (cpk_pack3.hip): 64 lanes x 16 consecutive words per tile
-bool pack_v3();
-hipError_t launch_pack_tiles3(const PackTileArgs& a, hipStream_t stream);
-// workgroup-tile kernel (cpk_pack4.hip, the default): 4 waves x 64 lanes x 8 consecutive words
-bool pack_v4();
-hipError_t launch_pack_tiles4(const PackTileArgs& a, hipStream_t stream);  // tiles -> scratch
-hipError_t launch_pack_place(const PackTileArgs& a, hipStream_t stream);   // scratch -> out
-hipError_t launch_pack_stage(int stage, const PackTileArgs& a, hipStream_t stream);
+hipError_t launch_pack_place(const PackTileArgs& a, hipStream_t stream);
 // tile_first (first i with pos[i] >= tile start, per tile) as extra blocks of a prologue
 // kernel: one launch fewer per call.  ntiles == 0: no such job.
 struct TileFirstJob {
@@ -134,7 +109,7 @@ uint32_t debug_skip();
 constexpr int kStampSlots = 16;
 constexpr int kStampRows = 256;
 
-// Diagnostic stamp buffers (env CPK_STAMPS=1): [0] pack, [1] unpack; kStampSlots u64 each.
+// Diagnostic stamp buffers (env CPK_STAMPS=1): [1] unpack counters, [2] index phases.
 unsigned long long* debug_stamps(int which);
 
 hipError_t launch_unpack_header(const uint8_t* packed, const uint64_t* in_off, uint64_t n,

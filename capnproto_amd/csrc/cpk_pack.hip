@@ -1,88 +1,71 @@
-// cpk_pack.hip -- MI355X (gfx950) kernels for Cap'n Proto's packed encoding.
+// cpk_pack.hip -- the pack kernels (gfx950): PackedOutputStream::write (capnproto
+// c++/src/capnp/serialize-packed.c++:307-431) once per chunk, for a whole batch of chunks.
 //
-// Functional spec: PackedOutputStream::write (capnproto c++/src/capnp/serialize-packed.c++:
-// 307-431), applied once per OutputStream::write() piece -- the segment table, then each segment
-// (writeMessage serialize.c++:332-357 -> OutputStream::write(pieces) kj/io.c++:109-113).
+// Layout.  A workgroup tile is 2048 consecutive words: 4 waves x 64 lanes x 8 CONSECUTIVE words,
+// so each lane encodes its own 8-word stretch serially and the cross-lane work is a handful of
+// 8-bit mask operations per lane, one wave prefix sum and one workgroup combine.
 //
-// Data-parallel restatement of the greedy scalar loop.  Every word of a chunk is one of
-//   Z  all-zero            F  no zero byte (tag 0xff)
-//   R  at most one zero byte (includes F)   O  anything else (>= 2 zero bytes, non-zero)
-// A maximal run of same-family words (Z, or R) inside a chunk is a "stretch"; chunk starts,
-// O words and family changes are sync points where the scalar loop's state is reset.
-//   * In a Z stretch the heads sit at 0, 256, 512, ... from the stretch start; a head emits
-//     `00 n` with n = min(255, zeros left in the stretch) (:352-374).
-//   * In an R stretch an F word that is a head opens a raw run covering the next <= 255 words of
-//     the stretch (:376-426); R words that are not covered are ordinary heads.
-//   * Output bytes per word: Z head 2, Z covered 0, F head 10, covered R 8, other heads 1 + nz.
-// Inside one 64-word step a run, once opened, never closes (255 > 63), so a step is resolved by
-// a handful of 64-bit mask operations on the wave's ballots (scalar unit): raw-run coverage of
-// every segment is one carry-propagating add, `((U + G) ^ U) & U` with U = ~sync and G the F
-// words shifted by one.  The only state crossing steps is one byte: the budget of the run that
-// is open at the step's last word.
-//
-// Work decomposition: the batch of words is cut into tiles of 64*S words, one wave per tile,
-// persistent waves over a static strided tile order (pack_tiles_kernel below).
+//   classes   per word: tag byte (SWAR), Z all zero, R <= 1 zero byte, F no zero byte, as 8-bit
+//             lane masks.  Sync points -- chunk starts (serialize.c++:311-357 + kj/io.c++:109-113
+//             make every segment-table and segment write() a chunk), O words (neither Z nor R),
+//             the first word of a Z or R stretch -- reset the encoder.
+//   coverage  from a lane's entry budget b (words the run open before the lane may still cover,
+//             serialize-packed.c++:352-374 zero runs, :376-426 raw runs, both <= 255 words) the
+//             covered words and run heads follow from carry-add mask algebra on 8 bits.  A lane
+//             with a sync point has an exit budget independent of b; a sync-free lane of one
+//             kind (all Z, or all F) maps b -> (b - 8) mod 256, so a sync-free wave of them maps b
+//             to itself (512 = 2 * 256).  Other sync-free stretches compose exactly in a scalar
+//             pass (rare: a >= 8-word stretch of words with one zero byte and no O word).
+//   tiles     ticket order (an atomic counter hands out tiles, so a tile only ever waits on
+//             tiles that running workgroups hold: no deadlock whatever else shares the GPU).  A
+//             tile's exit budget is published in state[] as soon as it is known -- right after
+//             the classes when the tile holds a sync point -- and the output offset comes from a
+//             two-level decoupled look-back over workgroup aggregates, done by wave 0 while waves
+//             1-3 emit their records into the LDS staging slot.
+//   count     the count byte of a run still open at the tile end depends on words of the next
+//             tile.  The tile writes it as if the batch ended there; when the next tile's first
+//             word is not a sync point (so the run may go on), the tile leaves that byte out of
+//             its stores and the NEXT tile -- which waits for this tile's exit budget anyway --
+//             writes it.  No tile ever waits on a later one.
+//   emission  each lane ORs its records into the staging slot at their own byte offsets (up to
+//             4 dwords each; bytes past a record are zero), empty records into a per-lane trash
+//             window; the slot then leaves with 16-byte stores.  A tile whose bytes exceed the
+//             slot (> 9 B/word: pathological one-word chunks or alternating raw/other words) is
+//             staged in several windows.
 #include <stdlib.h>
-
-#include <type_traits>
 
 #include "cpk_device.h"
 #include "cpk_kernels.h"
 
 namespace cpk {
-
 namespace {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-// v_writelane: lane `s` (compile-time) of `dst` takes the wave-uniform value `v`.  Inline asm
-// (this compiler has no writelane builtin) hides the SGPR read from the hazard recognizer, so
-// the value goes through an SALU move first: a writelane reading an SGPR that a VALU (ballot)
-// has just written returned stale data.
-template <int L>
-__device__ __forceinline__ uint32_t setlane(uint32_t dst, uint32_t v) {
-  uint32_t tmp;
-  asm volatile("s_mov_b32 %1, %2\n\ts_nop 0\n\tv_writelane_b32 %0, %1, %3"
-               : "+v"(dst), "=&s"(tmp)
-               : "s"((uint32_t)__builtin_amdgcn_readfirstlane((int)v)), "i"(L));
-  return dst;
-}
+constexpr int kK = 8;                          // words per lane
+constexpr int kWv = 4;                         // waves per workgroup
+constexpr int kWW = 64 * kK;                   // words per wave
+constexpr int kTW = kWv * kWW;                 // words per workgroup tile
+constexpr uint32_t kCap = 9 * kTW;             // staging window (bytes)
+constexpr uint32_t kPadF = 16;                 // front pad: records straddling the window start
+constexpr int kSlotDw = (kPadF + kCap + 64) / 4;
+constexpr int kTrashDw = 64 + 4;               // lane l: dwords l .. l + 3
+constexpr uint64_t kScr = kPackScratchBytes;    // scratch slot per tile (<= 10 B per word)
+static_assert(kScr >= 10 * kTW && kScr % 16 == 0, "a tile's bytes fit its scratch slot");
 
-// Compile-time loop: f(std::integral_constant<int, I>) for I in [B, E).
-template <int B, int E, class F>
-__device__ __forceinline__ void static_for(F&& f) {
-  if constexpr (B < E) {
-    f(std::integral_constant<int, B>{});
-    static_for<B + 1, E>(f);
-  }
-}
+static_assert(kTW == (int)kPackTileWords, "tile size shared with cpk_api.cpp");
 
-// Tag byte of a word (bit i <=> byte i non-zero), SWAR on the two dwords.
 __device__ __forceinline__ uint32_t tag_of(uint32_t lo, uint32_t hi) {
   const uint32_t m7 = 0x7f7f7f7fu;
   const uint32_t a = ((lo & m7) + m7) | lo;  // bit 7 of a byte <=> byte non-zero
   const uint32_t b = ((hi & m7) + m7) | hi;
-  const uint32_t c = ((a >> 7) & 0x01010101u) | ((b >> 3) & 0x10101010u);  // bits 8k, 8k+4
+  const uint32_t c = ((a >> 7) & 0x01010101u) | ((b >> 3) & 0x10101010u);
   const uint32_t d = c | (c >> 14);
   return (d | (d >> 7)) & 0xffu;
 }
 
-// Per-lane select by a wave-uniform 64-bit mask held in SGPRs: one v_cndmask.
-__device__ __forceinline__ uint32_t msel(uint64_t mask, uint32_t if_set, uint32_t if_clear) {
-  uint32_t r;
-  asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(r) : "v"(if_clear), "v"(if_set), "s"(mask));
-  return r;
-}
-
-// Index of the lowest set bit, ~0u for 0 (v_ffbl_b32).
-__device__ __forceinline__ uint32_t ffbl32(uint32_t v) {
-  uint32_t r;
-  asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(v));
-  return r;
-}
-
-// v_perm selectors placing the non-zero bytes of a word with tag `tag` after a zero byte 0:
-// dword 0 = [0, c0, c1, c2], dword 1 = [c3 .. c6] (c7 only exists for tag 0xff).
+// v_perm selectors placing the non-zero bytes of a word with tag `tag` after its tag byte:
+// dword 0 = [tag slot, c0, c1, c2], dword 1 = [c3 .. c6] (c7 only exists for tag 0xff).
 __device__ __forceinline__ uint64_t make_sel(uint32_t tag) {
   uint64_t sel = 0x0c0c0c0c0c0c0c0cull;
   int j = 1;
@@ -95,737 +78,535 @@ __device__ __forceinline__ uint64_t make_sel(uint32_t tag) {
   return sel;
 }
 
-// Head / coverage resolution of one step, entry budget b (words the run open before the step
-// may still cover).  All wave-uniform mask arithmetic.
-struct StepRes {
-  uint64_t covered, runheads;  // covered words; Z heads | F heads
-  uint64_t Zheads, Fheads;
-  int b_out;                   // budget leaving the step
+__device__ __forceinline__ int hi_bit(uint32_t m) { return m ? 31 - __clz(m) : -1; }
+
+struct Cov {
+  uint32_t cov, zh, fh;  // covered words, zero-run heads, raw-run heads
+  uint32_t b_out;        // budget leaving the lane
 };
 
-__device__ __forceinline__ StepRes resolve_step(uint64_t Z, uint64_t F, uint64_t R, uint64_t SY,
-                                                int b, bool last_valid) {
-  const uint64_t LM = ~SY & (SY - 1);                     // lead: words before the first sync
-  const uint64_t BM = b >= 64 ? ~0ull : mask_lt(b);       // words the entering run covers
-  const uint64_t lead_cov = BM & LM;
-  const uint64_t zlead = (BM + 1) & LM & Z;               // Z lead: next head at word b
-  const uint64_t Feff = F & ~lead_cov;
-  const uint64_t G = (Feff << 1) & ~SY;
-  const uint64_t fill = (((~SY + G) ^ ~SY) & ~SY) | G;    // words after an F head, same segment
-  const uint64_t Fheads = Feff & ~fill;
-  const uint64_t Zheads = (Z & SY) | zlead;
-  StepRes r;
-  r.covered = (R & (fill | lead_cov)) | (Z & ~Zheads);
-  r.runheads = Zheads | Fheads;
-  r.Zheads = Zheads;
-  r.Fheads = Fheads;
-  // budget for the next step: the last run head of the last segment, or the entering run when
-  // the whole step is its lead; a last word of class O ends with a sync and a zero budget
-  r.b_out = 0;
+// Coverage of one lane's 8 words for entry budget b.
+//   lead    words before the lane's first sync point continue the stretch entering the lane:
+//           the first b are covered; in a Z stretch word b is the next head.
+//   fill    after a raw-run head (F), the following R words up to the next sync point:
+//           ((NS + G) ^ NS) & NS carries each head's bit through the non-sync run behind it.
+// A run never closes inside 8 words (255 > 7), so one head per stretch and lane at most.
+__device__ __forceinline__ Cov cover8(uint32_t Z, uint32_t F, uint32_t R, uint32_t SY, uint32_t b,
+                                      bool last_valid) {
+  const uint32_t NS = ~SY & 0xffu;
+  const uint32_t LM = NS & (SY - 1u);
+  const uint32_t BM = b >= 8u ? 0xffu : ((1u << b) - 1u);
+  const uint32_t lead_cov = BM & LM;
+  const uint32_t zlead = (BM + 1u) & LM & Z;
+  const uint32_t Feff = F & ~lead_cov;
+  const uint32_t G = (Feff << 1) & NS;
+  const uint32_t fill = ((((NS + G) ^ NS) & NS) | G) & 0xffu;
+  Cov c;
+  c.fh = Feff & ~fill;
+  c.zh = (Z & SY) | zlead;
+  c.cov = (R & (fill | lead_cov)) | (Z & ~c.zh);
+  c.b_out = 0;
   if (last_valid) {
-    const int st = highest_bit(SY);         // -1: no sync
-    const int h = highest_bit(r.runheads);  // -1: no head
-    if (h >= 0 && h >= st) r.b_out = 192 + h;
-    else if (SY == 0 && b > 63) r.b_out = b - 64;
+    const int st = hi_bit(SY);
+    const int h = hi_bit(c.zh | c.fh);
+    if (h >= 0 && h >= st) c.b_out = 248u + (uint32_t)h;
+    else if (SY == 0 && b > 7u) c.b_out = b - 8u;
   }
-  return r;
+  return c;
 }
 
-// Valid-lane mask of step s of a tile with n valid words.
-__device__ __forceinline__ uint64_t valid_mask(int n, int s) {
-  const int k = n - 64 * s;
-  return k >= 64 ? ~0ull : (k <= 0 ? 0ull : mask_lt(k));
+// Exit budget of a sync-free lane (lane masks zl, fl) for entry budget b: one kind of word
+// (all Z, or b covers the lane) -> (b - 8) mod 256; else the first F word at or after b heads a
+// raw run (exit 248 + its position), none -> 0.
+__device__ __forceinline__ uint32_t free_lane_exit(uint32_t b, uint32_t zl, uint32_t fl) {
+  if (zl == 0xffu || b >= 8u) return (b - 8u) & 0xffu;
+  const uint32_t fm = fl >> b;
+  return fm ? 248u + b + (uint32_t)__builtin_ctz(fm) : 0u;
 }
 
-template <int S>
-struct TileLoad {
-  uint64_t x[S];  // word 64*s + lane
-  uint64_t nx;    // word tend + lane (look-ahead)
-  uint64_t cb;    // lanes < S: chunk-start bits of step `lane`; lane S: those of the next step
-  uint64_t pw;    // word before the tile (0 for tile 0)
-};
-
-template <int S>
-__device__ __forceinline__ void load_tile(const PackTileArgs& a, uint64_t t, TileLoad<S>& L) {
-  constexpr int T = 64 * S;
+// Entry budget of every lane given the wave's entry budget bw: lanes with a sync point pass on
+// their own exit (ex); sync-free lanes of one kind take 8 words each.  When a sync-free lane
+// holds other words (`nonsimple`), a scalar pass composes the exact per-lane functions.
+__device__ __forceinline__ uint32_t lane_entries(uint32_t bw, uint64_t hs, uint64_t nonsimple,
+                                                 uint32_t ex, uint32_t Z, uint32_t F) {
   const int l = lane_id();
-  const uint64_t N = a.nwords;
-  const uint64_t tbase = t * T;
-  const uint64_t tend = tbase + T < N ? tbase + T : N;
-#pragma unroll
-  for (int s = 0; s < S; s++) {
-    const uint64_t g = tbase + 64 * s + l;
-    L.x[s] = g < N ? a.words[g] : 0;
+  if (nonsimple == 0) {
+    const uint64_t below = hs & mask_lt(l);
+    const int j = highest_bit(below);  // -1: no sync lane below
+    const uint32_t ej = shfl32(ex, j < 0 ? 0 : j);
+    const uint32_t base = j < 0 ? bw : ej;
+    const uint32_t d = (uint32_t)(l - 1 - j);  // sync-free lanes in between
+    return (base - 8u * d) & 0xffu;
   }
-  L.nx = tend + l < N ? a.words[tend + l] : 0;
-  const uint64_t nbitw = (N + 63) >> 6;
-  L.cb = (l <= S && (tbase >> 6) + l < nbitw) ? a.chunk_bits[(tbase >> 6) + l] : 0;
-  L.pw = tbase > 0 ? a.words[tbase - 1] : 0;
+  uint32_t e = 0;
+  uint32_t b = bw;
+#pragma nounroll
+  for (int L = 0; L < 64; L++) {
+    if (l == L) e = b;
+    if ((hs >> L) & 1) b = readlane32(ex, L);
+    else b = free_lane_exit(b, readlane32(Z, L), readlane32(F, L));
+  }
+  return e;
 }
 
-// One wave per tile of 64*S words, persistent waves over a static strided tile order.
-//   pass A   classes + sync masks of every step (wave-uniform SGPR masks), packed tags;
-//            the tile's exit budget is published at once when it does not depend on the entry
-//   entry    the predecessor's exit budget, only when word 0 continues a stretch
-//   pass B   per step: resolve heads / coverage (scalar), record lengths, DPP prefix sum,
-//            v_perm compaction through a 256-entry selector table, records OR-ed into the
-//            wave's LDS staging area at tile-relative byte offsets
-//   look-back  two-level decoupled look-back on the tile's byte count
-//   flush    staged bytes -> global: 16-byte aligned stores (realigned by v_alignbyte), byte
-//            stores for the partial blocks at both ends; the staging area is re-zeroed.
-//
-// MODE kFused: the single-pass kernel above.  The two-pass form splits it at the look-back:
-// MODE kCount (persistent) does pass A and the count pass -- entry budgets still hand over
-// between waves, a one-hop wait only where a tile's first word continues a stretch -- and writes
-// each tile's entry budget and byte count; a scan turns the counts into output offsets; MODE kEmit
-// (one wave per tile, no waits) redoes pass A with the known entry budget, then pass B and the
-// flush at the known offset.
-constexpr int kFused = 0, kCount = 1, kEmit = 2;
+// Exit budget of the wave for entry budget bw (uniform).
+__device__ __forceinline__ uint32_t wave_exit(uint32_t bw, uint64_t hs, uint64_t nonsimple,
+                                              uint32_t ex, uint32_t Z, uint32_t F) {
+  const int j = highest_bit(hs);
+  uint32_t b = j < 0 ? bw : readlane32(ex, j);
+  const uint64_t after = j < 0 ? ~0ull : ~mask_le(j);
+  if ((nonsimple & after) == 0) return (b - 8u * (uint32_t)(63 - j)) & 0xffu;
+#pragma nounroll
+  for (int L = j + 1; L < 64; L++) b = free_lane_exit(b, readlane32(Z, L), readlane32(F, L));
+  return b;
+}
 
-template <int S, bool PF, bool STAMPS, int MODE = kFused>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S <= 8 ? 6 : 3, 8))) void pack_tiles_kernel(
+// Per-wave summary, exchanged through LDS (double-buffered by tile parity), packed in one
+// word: bit 0 the wave holds a sync point (its exit does not depend on its entry), bit 1 no
+// lane needs the scalar composition, bits 2-11 its first sync word (wave-relative; kWW: none),
+// bits 16-23 its exit when it holds a sync point.
+__device__ __forceinline__ uint32_t sum_pack(bool has_sync, bool simple, uint32_t fsw,
+                                             uint32_t exit0) {
+  return (has_sync ? 1u : 0u) | (simple ? 2u : 0u) | (fsw << 2) | (exit0 << 16);
+}
+__device__ __forceinline__ bool sum_sync(uint32_t s) { return s & 1u; }
+__device__ __forceinline__ bool sum_simple(uint32_t s) { return (s >> 1) & 1u; }
+__device__ __forceinline__ uint32_t sum_fsw(uint32_t s) { return (s >> 2) & 0x3ffu; }
+__device__ __forceinline__ uint32_t sum_exit(uint32_t s) { return (s >> 16) & 0xffu; }
+
+// ---------------------------------------------------------------------------------------------
+// 1. Tile kernel: one workgroup per 2048-word tile, in blockIdx order.  The tile's packed bytes
+//    go to its own scratch slot (scr + T * kScr, 16-byte aligned), with its byte count, the
+//    position of its provisional count byte (if the next tile may change it) and, for the
+//    previous tile, the final value of that byte.  The only wait is for the previous tile's
+//    exit budget, and only when this tile's first word goes on with the stretch the previous
+//    tile ended in; the previous tile publishes it right after its classes when it holds a
+//    sync point.  (A tile only waits on a lower one, dispatched before it.)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void pack_tile_kernel(
     PackTileArgs a) {
-  static_assert(S >= 2 && S <= 16 && (S % 2) == 0, "S steps per tile");
-  constexpr int T = 64 * S;
-  // Per-wave staging ring: a tile's records occupy [base, base + 32 + bytes) (16 B pads at both
-  // ends), at most 32 + 640 * S bytes; the ring holds the tile being encoded and the previous
-  // one, whose look-back and flush are deferred until after this tile's emission pass.  The emit
-  // pass flushes each tile at once (one region); the count pass stages nothing.
-  constexpr int kMaxRegion = 32 + 640 * S;
-  constexpr int kStg = MODE == kCount ? 16
-                       : (MODE == kEmit ? ((kMaxRegion + 15) & ~15)
-                                        : (((kMaxRegion * 6 / 5) + 15) & ~15));
-  __shared__ __attribute__((aligned(16))) uint8_t stg_all[4][kStg];
+  __shared__ __attribute__((aligned(16))) uint32_t stg[kSlotDw];
+  __shared__ __attribute__((aligned(16))) uint32_t trash[kWv][kTrashDw];
   __shared__ uint64_t sel_tab[256];
+  __shared__ uint32_t s_sum[kWv];    // wave summaries (sum_pack)
+  __shared__ uint32_t s_bytes[kWv];  // wave byte counts
+  __shared__ uint32_t s_sexit[kWv];  // serial mode: exit of each wave
 
+  const int tid = (int)threadIdx.x;
   const int l = lane_id();
-  const int wv = (int)uniform32(threadIdx.x >> 6);
-  uint8_t* const stg = stg_all[wv];
-  sel_tab[threadIdx.x] = make_sel(threadIdx.x);
-  for (int i = l; i < kStg / 16; i += 64) ((u32x4*)stg)[i] = (u32x4){0, 0, 0, 0};
-  __syncthreads();
-
-  const uint64_t gt_mask = ~mask_le(l);  // lanes above this one
-  const uint32_t gt_lo = (uint32_t)gt_mask, gt_hi = (uint32_t)(gt_mask >> 32);
-  const uint32_t lp1 = (uint32_t)l + 1u;
+  const int w = (int)uniform32(threadIdx.x >> 6);
   const uint64_t N = a.nwords;
   const uint64_t nbitw = (N + 63) >> 6;
-  uint32_t* const state = a.state;
-  const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
-  Stamps<STAMPS> stm;
-  stm.start(a.stamps);
-  uint64_t t = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wv;
-  TileLoad<S> cur;
-  if (t < a.ntiles) load_tile<S>(a, t, cur);
+  const uint64_t T = blockIdx.x;
+  const uint64_t tbase = T * kTW;
+  const uint64_t tend = tbase + kTW < N ? tbase + kTW : N;
+  const uint64_t wbase = tbase + (uint64_t)kWW * w;
+  const int nvw = wbase >= N ? 0 : (int)((N - wbase) < (uint64_t)kWW ? (N - wbase) : kWW);
+  const uint64_t w0 = wbase + (uint64_t)kK * l;  // the lane's first word
 
-  // A tile whose look-back and flush are still to be done.
-  struct Pending {
-    uint64_t t, agg, tend, pidx0, pidx;
-    uint32_t base;
-    bool on;
-  };
-  Pending pend;
-  pend.on = false;
-  auto region = [](uint64_t agg) -> uint32_t { return ((uint32_t)agg + 32u + 15u) & ~15u; };
-  // look-back, inclusive publish, flush of the staged bytes, positions
-  auto finish = [&](const Pending& p) {
-    uint64_t excl = 0;
-    if constexpr (MODE == kEmit) {
-      excl = uniform64(a.tile_off[p.t]);
-    } else if (a.debug_skip & 1) {
-      excl = p.t * 4096;  // timing ablation: no look-back (output meaningless)
-    } else {
-      excl = lookback2(a.desc, a.gdesc, p.t, 0, a.err);
-      publish_incl(a.desc, a.gdesc, p.t, a.ntiles, excl + p.agg);
-    }
-    const uint64_t agg = p.agg;
-    uint8_t* const sb = stg + p.base;
-    const uint32_t* const sb32 = (const uint32_t*)sb;
-    const bool over = excl + agg > a.out_capacity;
-    if (over && l == 0) raise_error(a.err, kErrCapacity);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (!over && agg) {
-      uint8_t* const out = a.out;
-      const uint64_t A0 = (uint64_t)(uintptr_t)out + excl;
-      const uint64_t A1 = A0 + agg;
-      const uint64_t al = (A0 + 15) & ~15ull;
-      const uint64_t hl = al < A1 ? al : A1;
-      if (A0 + l < hl) *(uint8_t*)(uintptr_t)(A0 + l) = sb[16 + l];
-      if (A1 > al) {
-        const uint64_t top = A1 & ~15ull;
-        const uint32_t nb = (uint32_t)((top - al) >> 4);
-        const uint32_t so0 = 16u + (uint32_t)(al - A0);
-        const uint32_t rr = so0 & 3u;
-        for (uint32_t i = l; i < nb; i += 64) {
-          const uint32_t d = (so0 >> 2) + 4 * i;
-          const uint32_t v0 = sb32[d], v1 = sb32[d + 1], v2 = sb32[d + 2], v3 = sb32[d + 3],
-                         v4 = sb32[d + 4];
-          u32x4 v;
-          v.x = __builtin_amdgcn_alignbyte(v1, v0, rr);
-          v.y = __builtin_amdgcn_alignbyte(v2, v1, rr);
-          v.z = __builtin_amdgcn_alignbyte(v3, v2, rr);
-          v.w = __builtin_amdgcn_alignbyte(v4, v3, rr);
-          *(u32x4*)(uintptr_t)(al + 16ull * i) = v;
-        }
-        if (top + l < A1) *(uint8_t*)(uintptr_t)(top + l) = sb[16 + (uint32_t)(top - A0) + l];
-      }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    const uint32_t nz16 = (uint32_t)((agg + 15) >> 4) + 1;
-    for (uint32_t i = l; i < nz16; i += 64) ((u32x4*)(sb + 16))[i] = (u32x4){0, 0, 0, 0};
-    // positions: add the tile's global offset (own stores, read back past L1)
-    if (a.pos) {
-      if constexpr (MODE != kEmit) {  // emit mode wrote absolute positions in pass B
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        for (uint64_t i = p.pidx0 + l; i < p.pidx; i += 64)
-          a.pos_out[i] = load_agent(a.pos_out + i) + excl;
-      }
-      if (p.tend == N) {
-        const uint64_t tot = excl + agg;
-        for (uint64_t i = p.pidx + l; i <= a.npos; i += 64) a.pos_out[i] = tot;
-      }
-    }
-    if (p.tend == N && l == 0 && a.total_out) *a.total_out = excl + agg;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  };
-
-  for (; t < a.ntiles; t += nwaves) {
-    TileLoad<S> nxt;
-    auto tile = [&](auto full_c) {
-    constexpr bool FULL = decltype(full_c)::value;
-    stm.restart();
-    const uint64_t tbase = t * T;
-    const uint64_t tend = tbase + T < N ? tbase + T : N;
-    const int nvalid = FULL ? T : (int)(tend - tbase);
-    const int last = nvalid - 1;
-    uint64_t zc0 = 0, rc0 = 0;  // class of the word before the tile
-    if (tbase > 0) {
-      const uint64_t pw = uniform64(cur.pw);
-      zc0 = pw == 0;
-      rc0 = __popc(tag_of((uint32_t)pw, (uint32_t)(pw >> 32))) >= 7;
-    }
-
-    // ---- pass A --------------------------------------------------------------------------
-    // per step: tags and the Z / R / F ballots, parked in VGPR lanes (lane s = step s); the sync
-    // masks and state-independent byte counts of all steps are then formed at once in lanes
-    uint32_t vSYlo = 0, vSYhi = 0, vFlo = 0, vFhi = 0, vZlo = 0, vZhi = 0, vRlo = 0, vRhi = 0;
-    uint32_t vNsa = 0, vBase = 0, vOb = 0;
-    uint32_t tagpk[S / 2];
-    static_for<0, S>([&](auto sc) {
-      constexpr int s = decltype(sc)::value;
-      const uint64_t x = cur.x[s];
-      if (s % 2 == 0) tagpk[s >> 1] = 0;
-      const uint64_t Z = ballot(x == 0);  // words past the batch end load as 0: masked below
-      vZlo = setlane<s>(vZlo, (uint32_t)Z);
-      vZhi = setlane<s>(vZhi, (uint32_t)(Z >> 32));
-      if (Z != ~0ull) {  // an all-zero step has tag 0, no R / F word and no O bytes
-        const uint32_t tag = tag_of((uint32_t)x, (uint32_t)(x >> 32));
-        tagpk[s >> 1] |= tag << (16 * (s & 1));
-        asm volatile("" : "+v"(tagpk[s >> 1]));  // keep the packed form (VGPR pressure)
-        const uint64_t R = ballot(__popc(tag) >= 7);
-        const uint64_t Fs = ballot(tag == 0xff);
-        vFlo = setlane<s>(vFlo, (uint32_t)Fs);
-        vFhi = setlane<s>(vFhi, (uint32_t)(Fs >> 32));
-        vRlo = setlane<s>(vRlo, (uint32_t)R);
-        vRhi = setlane<s>(vRhi, (uint32_t)(R >> 32));
-        // sum of nz over the O words of the step (their bytes are 1 + nz)
-        const uint32_t nz = __popc(tag);
-        const uint32_t ob = (x != 0 && nz < 7) ? nz : 0;
-        vOb = setlane<s>(vOb, (uint32_t)(__popcll(ballot(ob & 1)) +
-                                         2 * __popcll(ballot(ob & 2)) +
-                                         4 * __popcll(ballot(ob & 4))));
-      }
-    });
-    bool lastZ, lastR;
-    int first_sync = T, sg = -1;
-    {
-      const int kv = nvalid - 64 * l;
-      const uint64_t V = FULL ? ~0ull : (kv >= 64 ? ~0ull : (kv <= 0 ? 0ull : mask_lt(kv)));
-      const uint64_t Z = (((uint64_t)vZhi << 32) | vZlo) & V;
-      const uint64_t R = (((uint64_t)vRhi << 32) | vRlo) & V;
-      const uint64_t F = (((uint64_t)vFhi << 32) | vFlo) & V;
-      // class of the word before the step: the previous lane's last word (tile: word tbase-1)
-      uint32_t zc = dpp_src<0x111, 0xf>((uint32_t)(Z >> 32)) >> 31;
-      uint32_t rc = dpp_src<0x111, 0xf>((uint32_t)(R >> 32)) >> 31;
-      if (l == 0) {
-        zc = (uint32_t)zc0;
-        rc = (uint32_t)rc0;
-      }
-      const uint64_t C = cur.cb;  // lane s: chunk-start bits of step s
-      const uint64_t O = V & ~Z & ~R;
-      const uint64_t SY =
-          C | O | (Z & ~((Z << 1) | zc)) | (R & ~((R << 1) | rc)) | ~V;
-      vSYlo = (uint32_t)SY;
-      vSYhi = (uint32_t)(SY >> 32);
-      vZlo = (uint32_t)Z;
-      vZhi = (uint32_t)(Z >> 32);
-      vRlo = (uint32_t)R;
-      vRhi = (uint32_t)(R >> 32);
-      vFlo = (uint32_t)F;
-      vFhi = (uint32_t)(F >> 32);
-      // state-independent bytes of the step: 1 + nz per O word, 8 per R word
-      vBase = (uint32_t)(__popcll(O) + 8 * __popcll(R)) + vOb;
-      const uint64_t m = l < S ? (SY & V) : 0ull;
-      const uint64_t bm = ballot(m != 0);
-      if (bm) {
-        const int fl = lowest_bit(bm), hl = highest_bit(bm);
-        first_sync = 64 * fl + lowest_bit(readlane64(m, fl));
-        sg = 64 * hl + highest_bit(readlane64(m, hl));
-      }
-      const int ls = last >> 6;
-      lastZ = (readlane64(Z, ls) >> (last & 63)) & 1;
-      lastR = (readlane64(R, ls) >> (last & 63)) & 1;
-    }
-    stm.mark(0);
-    // count pass: pass A was the last use of the words, the next tile's can be on their way
-    if constexpr (MODE == kCount) {
-      if (t + nwaves < a.ntiles) load_tile<S>(a, t + nwaves, cur);
-    }
-
-    // ---- look-ahead: distance from tend to the first sync at / after it (<= 256) ------------
-    int la = 0;
-    if (MODE != kCount && (lastZ || lastR) && tend < N) {
-      uint64_t czc = lastZ, crc = lastR;
-      la = 256;
-      uint64_t xk[4] = {cur.nx, 0, 0, 0}, ck[4] = {readlane64(cur.cb, S), 0, 0, 0};
-      for (int k = 0; k < 4; k++) {
-        const uint64_t g = tend + 64 * k + l;
-        if (k == 1) {
-          // words 64 .. 255 past the tile together: one round trip instead of three
+  // ---- loads: all issued before any is waited for --------------------------------------
+  // (vector loads retire in order; the compiler waits for all of them right behind a load whose
+  // value it moves to an SGPR or at the join behind a load under a branch, so uniform values
+  // come through scalar loads and lane-varying guards are clamped addresses)
+  uint32_t xlo[kK], xhi[kK];
+  if (nvw == kWW) {
+    const u32x4* src = (const u32x4*)(a.words + w0);
 #pragma unroll
-          for (int j = 1; j < 4; j++) {
-            const uint64_t gj = tend + 64 * j + l;
-            xk[j] = gj < N ? a.words[gj] : 0;
-            ck[j] = ((tend >> 6) + j < nbitw) ? a.chunk_bits[(tend >> 6) + j] : 0;
-          }
-        }
-        const uint64_t xx = xk[k];
-        const uint32_t tg = tag_of((uint32_t)xx, (uint32_t)(xx >> 32));
-        const uint64_t V = ballot(g < N);
-        const uint64_t C = ck[k];
-        const uint64_t Z = ballot(xx == 0) & V;
-        const uint64_t R = ballot(__popc(tg) >= 7) & V;
-        const uint64_t O = V & ~Z & ~R;
-        const uint64_t SY = C | O | (Z & ~((Z << 1) | czc)) | (R & ~((R << 1) | crc)) | ~V;
-        if (SY) {
-          la = 64 * k + lowest_bit(SY);
-          break;
-        }
-        czc = Z >> 63;
-        crc = R >> 63;
-      }
+    for (int i = 0; i < kK / 2; i++) {
+      const u32x4 v = src[i];
+      xlo[2 * i] = v.x;
+      xhi[2 * i] = v.y;
+      xlo[2 * i + 1] = v.z;
+      xhi[2 * i + 1] = v.w;
     }
-    // lane s: distance from step s+1's first word to the first sync at / after it
-    {
-      int v = la;
-      static_for<0, S>([&](auto sc) {
-        constexpr int s = S - 1 - decltype(sc)::value;
-        vNsa = setlane<s>(vNsa, v);
-        const int fs = lowest_bit(readlane64(((uint64_t)vSYhi << 32) | vSYlo, s));
-        v = fs < 64 ? fs : (v + 64 < 256 ? v + 64 : 256);
-      });
-    }
-
-    // ---- exit budget, published early when it does not depend on the entry ----------------
-    if (first_sync < T) {
-      int eb = 0;
-      if (lastZ) {
-        eb = 255 - ((last - sg) & 255);
-      } else if (lastR) {
-        int na = sg, qq = -1;
-#pragma unroll
-        for (int s = 0; s < S; s++) {
-          if (64 * s + 63 >= na && 64 * s <= last) {
-            uint64_t m = readlane64(((uint64_t)vFhi << 32) | vFlo, s);
-            if (na > 64 * s) m &= ~mask_lt(na - 64 * s);
-            if (m) {
-              qq = 64 * s + lowest_bit(m);
-              na = qq + 256;
-            }
-          }
-        }
-        eb = (qq >= 0 && last - qq <= 255) ? 255 - (last - qq) : 0;
-      }
-      if (MODE != kEmit && l == 0) store_agent32(state + t, 0x80000000u | (uint32_t)eb);
-    }
-
-    // prefetch the next tile (lands during pass B and the look-back)
-    if (PF && t + nwaves < a.ntiles) load_tile<S>(a, t + nwaves, nxt);
-    stm.mark(1);
-
-    int b = 0;
-    if constexpr (MODE == kEmit) {
-      b = (int)uniform32(a.tile_b[t]);
-    } else {
-      if (first_sync > 0 && t > 0) b = (int)(wait_nonzero32(state + t - 1, a.err) & 0xffu);
-    }
-    const int b_entry = b;
-    stm.mark(2);
-
-    // ---- count pass: heads / coverage of every step, byte offsets --------------------------
-    //   bytes(step) = sum over O words of (1 + nz) + 8 |R| + 2 |Z heads + F heads|
-    // Lane s resolves step s from the masks parked in its lanes (vector unit, all steps at once);
-    // only the entry budgets run step to step on the scalar unit, and a step's exit budget
-    // depends on its entry budget only when the step has no sync at all.
-    uint32_t vCOVlo, vCOVhi, vZHlo, vZHhi, vFHlo, vFHhi, vSoff;
-    uint32_t agg32;
-    {
-      const uint64_t vZ = ((uint64_t)vZhi << 32) | vZlo;
-      const uint64_t vF = ((uint64_t)vFhi << 32) | vFlo;
-      const uint64_t vR = ((uint64_t)vRhi << 32) | vRlo;
-      const uint64_t vSY = ((uint64_t)vSYhi << 32) | vSYlo;
-      const bool lane_step = l < S && 64 * l < nvalid;
-      const bool lv = 64 * l + 63 < nvalid;  // the step's last word is valid
-      // exit budget of a step with a sync: the same for every entry budget (entry 0 here)
-      const StepRes r0 = resolve_step(vZ, vF, vR, vSY, 0, lv);
-      const uint32_t info = (vSY != 0 ? 0x80000000u : 0u) | (vZ != 0 ? 0x40000000u : 0u) |
-                            (uint32_t)r0.b_out;
-      uint32_t vB = 0;
-      static_for<0, S>([&](auto sc) {
-        constexpr int s = decltype(sc)::value;
-        if (64 * s < nvalid) {
-          vB = setlane<s>(vB, (uint32_t)b);
-          const uint32_t inf = readlane32(info, s);
-          if (inf & 0x80000000u) {
-            b = (int)(inf & 0x3ffu);
-          } else if (b > 63) {
-            b -= 64;  // the entering run covers the whole step
-          } else if (inf & 0x40000000u) {
-            b += 192;  // zero stretch: a head at word b
-          } else {  // word stretch: the first F word at / after b opens a run
-            const uint64_t Fm = readlane64(vF, s) & ~mask_lt(b);
-            b = Fm ? 192 + lowest_bit(Fm) : 0;
-          }
-        }
-      });
-      const StepRes r = resolve_step(vZ, vF, vR, vSY, (int)vB, lv);
-      const int kv = nvalid - 64 * l;
-      const uint64_t V = kv >= 64 ? ~0ull : (kv <= 0 ? 0ull : mask_lt(kv));
-      const uint64_t COV = r.covered | ~V;
-      vCOVlo = (uint32_t)COV;
-      vCOVhi = (uint32_t)(COV >> 32);
-      vZHlo = (uint32_t)r.Zheads;
-      vZHhi = (uint32_t)(r.Zheads >> 32);
-      vFHlo = (uint32_t)r.Fheads;
-      vFHhi = (uint32_t)(r.Fheads >> 32);
-      const uint32_t bytes = lane_step ? vBase + 2u * (uint32_t)__popcll(r.runheads) : 0u;
-      const uint32_t incl = wave_incl_sum32(bytes);
-      vSoff = incl - bytes;
-      agg32 = readlane32(incl, S - 1);
-    }
-    if (MODE != kEmit && first_sync == T && l == 0) store_agent32(state + t, 0x80000000u | (uint32_t)b);
-    const uint64_t agg = agg32;
-    if constexpr (MODE == kCount) {
-      if (l == 0) {
-        a.tile_b[t] = (uint32_t)b_entry;
-        a.tile_bytes[t] = agg;
-      }
-      return;
-    }
-    if (MODE == kFused && !(a.debug_skip & 1))
-      publish_agg(a.desc, a.gdesc, a.gcnt, t, a.ntiles, agg, 0, a.err);
-    (void)b_entry;
-    stm.mark(3);
-
-    // ---- staging region: after the pending tile's, else at 0 (finishing it first if needed) ---
-    const uint32_t need = region(agg);
-    uint32_t base = 0;
-    if (pend.on) {
-      const uint32_t pe = pend.base + region(pend.agg);
-      if (pe + need <= (uint32_t)kStg) {
-        base = pe;
-      } else if (need > pend.base) {
-        finish(pend);
-        pend.on = false;
-      }
-    }
-
-    // ---- pass B ----------------------------------------------------------------------------
-    const uint64_t pidx0 = a.pos ? uniform64(a.tile_first[t]) : 0;
-    // emit mode knows the tile's output offset: positions are written absolute
-    const uint64_t pos_base = MODE == kEmit ? uniform64(a.tile_off[t]) : 0;
-    uint64_t pidx = pidx0;
-    uint32_t prel = ~0u;  // next requested position, tile-relative (~0: none in this tile)
-    if (a.pos && pidx <= a.npos) {
-      const uint64_t pn = uniform64(a.pos[pidx]);
-      if (pn - tbase < (uint64_t)T) prel = (uint32_t)(pn - tbase);
-    }
-#pragma unroll
-    for (int s = 0; s < S; s++) {
-      if (64 * s < nvalid) {
-        const uint64_t x = cur.x[s];
-        const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
-        const uint32_t tag = (tagpk[s >> 1] >> (16 * (s & 1))) & 0xffu;
-        const uint32_t nz = __popc(tag);
-        const uint64_t SY = readlane64(((uint64_t)vSYhi << 32) | vSYlo, s);
-        const uint64_t COV = readlane64(((uint64_t)vCOVhi << 32) | vCOVlo, s);
-        const uint64_t ZH = readlane64(((uint64_t)vZHhi << 32) | vZHlo, s);
-        const uint64_t FH = readlane64(((uint64_t)vFHhi << 32) | vFHlo, s);
-        const uint32_t soff = readlane32(vSoff, s);
-        const uint64_t Zs = ((uint64_t)readlane32(vZhi, s) << 32) | readlane32(vZlo, s);
-        if (Zs == ~0ull && !(prel < 64u * s + 64u)) {
-          // all-zero step: the records are its Z heads, two bytes each ([00, count]); the tag
-          // byte stays zero in the staging area, only a non-zero count is stored
-          uint64_t hm = ZH;
-          uint32_t k = 0;
-          while (hm) {
-            const int h = lowest_bit(hm);
-            hm &= hm - 1;
-            const uint64_t after = SY & ~mask_le(h);
-            const uint32_t ns = after ? (uint32_t)lowest_bit(after) : 64u + readlane32(vNsa, s);
-            const uint32_t cnt = min(ns - (uint32_t)h - 1u, 255u);
-            if (cnt && l == 0) stg[base + 16u + soff + 2 * k + 1] = (uint8_t)cnt;
-            k++;
-          }
-          continue;
-        }
-        // record length: head 1 + nz (+1 count byte for run heads), covered R 8, covered Z 0
-        const uint32_t n1 = nz + 1;
-        const uint32_t len = msel(COV, n1 & 8u, n1 + msel(ZH | FH, 1u, 0u));
-        const uint32_t inc = wave_incl_sum32(len);
-        const uint32_t o = inc - len;
-        // run count: stretch words after this one (<= 255); ffbl of 0 is ~0u
-        const uint32_t f_lo = ffbl32((uint32_t)SY & gt_lo);
-        const uint32_t f_hi = __builtin_elementwise_add_sat(
-            ffbl32((uint32_t)(SY >> 32) & gt_hi), 32u);
-        const uint32_t ns = min(min(f_lo, f_hi), 64u + readlane32(vNsa, s));
-        const uint32_t cnt = min(ns - lp1, 255u);
-        // record bytes: [tag, non-zero bytes..., count] for heads, the raw word when covered
-        const uint64_t sel = sel_tab[tag];
-        const uint32_t c8 = cnt << 8;
-        uint32_t w0 = __builtin_amdgcn_perm(hi, lo, (uint32_t)sel) | tag | msel(ZH, c8, 0u);
-        uint32_t w1 = __builtin_amdgcn_perm(hi, lo, (uint32_t)(sel >> 32));
-        const uint32_t w2 = msel(FH, (hi >> 24) | c8, 0u);
-        w0 = msel(COV, lo, w0);
-        w1 = msel(COV, hi, w1);
-        // OR into the staging area at byte 16 + soff + o: four dwords from (at - 1) & ~3, each
-        // only where the record has bytes (a lane of a covered zero word has none; empty lanes
-        // would all hit the same dword and serialise on it)
-        const uint32_t at = base + 16u + soff + o;
-        const uint32_t rr = (0u - at) & 3u;
-        const uint32_t kk = 4u - rr;     // record start inside the 16-byte window (1..4)
-        const uint32_t ee = kk + len;    // record end inside the window
-        uint32_t* dp = (uint32_t*)(stg + ((at - 1u) & ~3u));
-        if (kk < 4u && len) atomicOr(dp + 0, __builtin_amdgcn_alignbyte(w0, 0u, rr));
-        if (ee > 4u) atomicOr(dp + 1, __builtin_amdgcn_alignbyte(w1, w0, rr));
-        if (ee > 8u) atomicOr(dp + 2, __builtin_amdgcn_alignbyte(w2, w1, rr));
-        if (ee > 12u) atomicOr(dp + 3, __builtin_amdgcn_alignbyte(0u, w2, rr));
-        // requested positions inside this step: tile-relative offsets (excl added later)
-        if (prel < 64u * s + 64u) {
-          const uint64_t g0 = tbase + 64 * s;
-          while (true) {
-            const uint64_t i = pidx + l;
-            const uint64_t p = i <= a.npos ? a.pos[i] : ~0ull;
-            const bool in = p < g0 + 64;
-            const uint32_t oo = shfl32(o, in ? (int)(p - g0) : 0);
-            if (in) a.pos_out[i] = pos_base + soff + oo;
-            const uint64_t inm = ballot(in);
-            pidx += __popcll(inm);
-            const uint64_t pn = pidx <= a.npos ? uniform64(a.pos[pidx]) : ~0ull;
-            prel = pn - tbase < (uint64_t)T ? (uint32_t)(pn - tbase) : ~0u;
-            if (inm != ~0ull) break;
-          }
-        }
-      }
-    }
-    stm.mark(4);
-
-    // ---- the next tile's words into the registers pass B no longer needs: issued before the
-    //      previous tile's flush stores, so waiting for them never waits for those stores
-    if (!PF && t + nwaves < a.ntiles) load_tile<S>(a, t + nwaves, cur);
-
-    // ---- finish the previous tile (its look-back had this tile's passes to resolve) --------
-    if (pend.on) finish(pend);
-    if constexpr (MODE == kEmit) {  // no look-back to wait for: flush at once
-      Pending now;
-      now.t = t;
-      now.agg = agg;
-      now.tend = tend;
-      now.pidx0 = pidx0;
-      now.pidx = pidx;
-      now.base = base;
-      now.on = true;
-      finish(now);
-      return;
-    }
-    pend.t = t;
-    pend.agg = agg;
-    pend.tend = tend;
-    pend.pidx0 = pidx0;
-    pend.pidx = pidx;
-    pend.base = base;
-    pend.on = true;
-    stm.mark(5);
-    };
-    // one instantiation of the tile body (the partial last tile's masks cost a few VALU per
-    // step): a second, full-tile copy doubles the kernel's code for no measurable gain
-    tile(std::false_type{});
-    if (PF) cur = nxt;
-  }  // tile loop
-  if (pend.on) finish(pend);
-  stm.flush();
-}
-
-// Chunk-start bitmap + per-message framing status for a batch of flat messages.
-// Message i = words[off[i], off[i+1]): segment table (serializeSegmentTable serialize.c++:
-// 311-330) then segments; chunk starts = message start, table end, each segment start.
-__global__ void message_bits_kernel(const uint64_t* __restrict__ words,
-                                    const uint64_t* __restrict__ off, uint64_t n,
-                                    unsigned long long* __restrict__ bits,
-                                    int32_t* __restrict__ status, TileFirstJob tf,
-                                    uint32_t tf_block) {
-  if (run_tile_first(tf, tf_block)) return;
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint64_t w0 = off[i], w1 = off[i + 1];
-  int32_t st = 0;
-  if (w1 <= w0) {
-    if (status) status[i] = 11;  // CPK_ERR_EMPTY_MESSAGE
-    return;
-  }
-  atomicOr(bits + (w0 >> 6), 1ull << (w0 & 63));
-  const uint64_t nw = w1 - w0;
-  const uint32_t* t32 = (const uint32_t*)(words + w0);
-  const uint64_t nseg = (uint64_t)t32[0] + 1;
-  const uint64_t tw = nseg / 2 + 1;
-  bool ok = tw <= nw;
-  if (ok) {
-    uint64_t total = tw;
-    for (uint64_t s = 0; s < nseg && total <= nw; s++) total += t32[s + 1];
-    ok = total == nw;
-  }
-  if (!ok) {
-    st = 6;  // CPK_ERR_BAD_FRAMING: packed as one chunk
   } else {
-    uint64_t p = w0 + tw;
-    if (p < w1) atomicOr(bits + (p >> 6), 1ull << (p & 63));
-    for (uint64_t s = 0; s + 1 < nseg; s++) {
-      p += t32[s + 1];
-      if (p < w1) atomicOr(bits + (p >> 6), 1ull << (p & 63));
+#pragma unroll
+    for (int k = 0; k < kK; k++) {
+      const uint64_t x = w0 + k < N ? a.words[w0 + k] : 0;
+      xlo[k] = (uint32_t)x;
+      xhi[k] = (uint32_t)(x >> 32);
     }
   }
-  if (status) status[i] = st;
+  const uint64_t cbi = (wbase >> 6) + (uint64_t)(l >> 3);
+  const uint64_t cb0 = a.chunk_bits[cbi < nbitw ? cbi : nbitw - 1];
+  // lane 0: the word before the wave; the other lanes: the word after the tile (its class
+  // decides whether this tile's open run may go on in the next tile)
+  const uint64_t xi = l == 0 ? (wbase > 0 ? wbase - 1 : 0) : (tend < N ? tend : N - 1);
+  const uint64_t xw0 = a.words[xi < N ? xi : N - 1];
+  const uint64_t nbi = (tend >> 6) + (uint64_t)opaque_zero();
+  const uint64_t nb0 = a.chunk_bits[nbi < nbitw ? nbi : nbitw - 1];
+  typedef const __attribute__((address_space(4))) uint64_t cu64;
+  const uint64_t pidx = a.pos ? *((cu64*)a.tile_first + T) : 0;  // scalar load
+  const uint64_t pi = pidx + l;
+  const bool pv = a.pos && pi <= a.npos;
+  const uint64_t p00 = (a.pos ? a.pos : a.words)[pv ? pi : 0];
+  sel_tab[tid] = make_sel((uint32_t)tid);
+  for (int i = tid; i < kSlotDw / 4; i += 64 * kWv) ((u32x4*)stg)[i] = (u32x4){0, 0, 0, 0};
+  const uint64_t cbw = cbi < nbitw ? cb0 : 0;
+  const uint64_t xw = (wbase > 0 || l != 0) ? xw0 : 0;
+  const uint64_t p0 = pv ? p00 : ~0ull;
+
+  // ---- classes -------------------------------------------------------------------------
+  uint32_t Zm = 0, Rm = 0, Fm = 0, nzA = 0;
+  uint32_t tags[kK / 4] = {0, 0};
+#pragma unroll
+  for (int k = 0; k < kK; k++) {
+    const uint32_t tg = tag_of(xlo[k], xhi[k]);
+    const uint32_t nz = __popc(tg);
+    tags[k >> 2] |= tg << (8 * (k & 3));
+    Zm |= (tg == 0 ? 1u : 0u) << k;
+    Rm |= (nz >= 7 ? 1u : 0u) << k;
+    Fm |= (tg == 0xffu ? 1u : 0u) << k;
+    nzA |= nz << (4 * k);
+  }
+  const int kv = nvw - kK * l;
+  const uint32_t V = kv >= kK ? 0xffu : (kv <= 0 ? 0u : ((1u << kv) - 1u));
+  Zm &= V;
+  Rm &= V;
+  Fm &= V;
+  // class of the word before the lane: the previous lane's last word (lane 0: word wbase - 1)
+  uint32_t zc = shfl32(Zm >> 7, l > 0 ? l - 1 : 0) & 1u;
+  uint32_t rc = shfl32(Rm >> 7, l > 0 ? l - 1 : 0) & 1u;
+  const uint32_t xtag = tag_of((uint32_t)xw, (uint32_t)(xw >> 32));
+  if (l == 0) {
+    zc = (wbase > 0 && xw == 0) ? 1u : 0u;
+    rc = (wbase > 0 && __popc(xtag) >= 7) ? 1u : 0u;
+  }
+  const uint32_t C = (uint32_t)(cbw >> (8 * (l & 7))) & 0xffu;
+  const uint32_t O = V & ~Zm & ~Rm;
+  const uint32_t SY =
+      (C | O | (Zm & ~((Zm << 1) | zc)) | (Rm & ~((Rm << 1) | rc)) | ~V) & 0xffu;
+  const bool lv = kv >= kK;
+
+  const uint64_t hs = ballot(SY != 0);
+  const bool simple = SY != 0 || Zm == 0xffu || Fm == 0xffu;
+  const uint64_t nonsimple = ballot(!simple && kv > 0);
+  const Cov c0 = cover8(Zm, Fm, Rm, SY, 0u, lv);  // exits of the lanes with a sync point
+  const uint32_t fs = SY ? (uint32_t)__builtin_ctz(SY) : 8u;
+  // first sync after the lane, wave-relative
+  const uint64_t above = hs & ~mask_le(l);
+  const int ja = above ? lowest_bit(above) : 0;
+  const uint32_t fsa = shfl32(fs, ja);
+  // the tile's exit, with the raw bit (the run open at the tile end is a raw run when the
+  // tile's last word is not zero), published by the last wave as soon as it is known: right here
+  // when the last wave holds a sync point (its exit is then the tile's, whatever the entry)
+  uint32_t t_exit = 0;
+  auto publish_state = [&](uint32_t ex) {
+    const uint32_t lz = readlane32(Zm >> 7, 63) & 1u;
+    t_exit = ex | ((ex != 0 && !lz) ? 0x100u : 0u);
+    if (l == 0) store_agent32(a.state + T, 0x80000000u | t_exit);
+  };
+  {
+    const uint32_t exit0 = hs != 0 ? wave_exit(0u, hs, nonsimple, c0.b_out, Zm, Fm) : 0u;
+    if (w == kWv - 1 && hs != 0) publish_state(exit0);
+    const int L0 = hs ? lowest_bit(hs) : 0;
+    const uint32_t fsl = shfl32(fs, L0);
+    const uint32_t fsw = hs ? (uint32_t)(kK * L0) + fsl : (uint32_t)kWW;
+    if (l == 0) s_sum[w] = sum_pack(hs != 0, nonsimple == 0, fsw, exit0);
+  }
+  // the word after the tile: a sync point there closes this tile's open run at its end
+  bool next_sync = true;
+  if (w == kWv - 1) {
+    const uint32_t ntag = tag_of((uint32_t)xw0, (uint32_t)(xw0 >> 32));
+    const uint32_t nnz = __popc(ntag);
+    const bool nC = (nb0 >> (tend & 63)) & 1;
+    const uint32_t lastZ = readlane32(Zm >> 7, 63) & 1u, lastR = readlane32(Rm >> 7, 63) & 1u;
+    const bool nZ = ntag == 0, nR = nnz >= 7;
+    const bool ns = nC || (!nZ && !nR) || (nZ && !lastZ) || (nR && !lastR);
+    next_sync = tend >= N || readlane32(ns ? 1u : 0u, 63) != 0;
+  }
+  __syncthreads();  // ---- A: wave summaries ---------------------------------------------
+
+  uint32_t sm[kWv];
+#pragma unroll
+  for (int v = 0; v < kWv; v++) sm[v] = uniform32(s_sum[v]);
+  bool serial = false;
+#pragma unroll
+  for (int v = 0; v < kWv; v++) serial |= !sum_sync(sm[v]) && !sum_simple(sm[v]);
+  const bool first_sync = sum_fsw(sm[0]) == 0;
+  // the tile's entry budget (| 0x100: the run is a raw run), waited for only when the tile's
+  // first word goes on with the stretch the previous tile ended in
+  auto tile_entry = [&]() -> uint32_t {
+    if (first_sync || T == 0) return 0u;
+    return wait_nonzero32(a.state + T - 1, a.err) & 0x1ffu;
+  };
+  const bool last_sync = sum_sync(sm[kWv - 1]);  // the exit went out before barrier A
+  uint32_t bT = 0, bw = 0;
+  bool have_bT = false;
+  if (!serial) {
+    // the last wave with a sync point fixes the exit; the one-kind sync-free waves behind it map
+    // budgets to themselves (512 words = 2 runs of 256)
+    int js = -1;
+#pragma unroll
+    for (int v = 0; v < kWv; v++)
+      if (sum_sync(sm[v])) js = v;
+    if (js >= 0 && !last_sync && w == kWv - 1) publish_state(sum_exit(sm[js]));
+    // this wave's entry: the nearest lower wave with a sync point, else the tile's entry
+    int jb = -1;
+#pragma unroll
+    for (int v = 0; v < kWv; v++)
+      if (v < w && sum_sync(sm[v])) jb = v;
+    if (jb >= 0) {
+      bw = sum_exit(sm[jb]);
+    } else {
+      bT = tile_entry();
+      have_bT = true;
+      bw = bT & 0xffu;
+    }
+    if (js < 0 && w == kWv - 1) publish_state(bw);
+  } else {
+    // rare: a sync-free wave that needs the scalar composition -- the waves in order
+#pragma nounroll
+    for (int v = 0; v < kWv; v++) {
+      if (w == v) {
+        if (v == 0) {
+          bT = tile_entry();
+          have_bT = true;
+          bw = bT & 0xffu;
+        } else {
+          bw = uniform32(s_sexit[v - 1]);
+        }
+        const uint32_t ex =
+            hs != 0 ? sum_exit(sm[v]) : wave_exit(bw, hs, nonsimple, c0.b_out, Zm, Fm);
+        if (l == 0) s_sexit[v] = ex;
+        if (v == kWv - 1 && !last_sync) publish_state(ex);
+      }
+      __syncthreads();
+    }
+  }
+  // wave 0 finishes the previous tile's open run: it needs the entry
+  if (w == 0 && !have_bT) bT = tile_entry();
+
+  // ---- coverage, bytes, offsets ----------------------------------------------------------
+  const uint32_t ent = lane_entries(bw, hs, nonsimple, c0.b_out, Zm, Fm);
+  const Cov cv = cover8(Zm, Fm, Rm, SY, ent, lv);
+  const uint32_t heads = V & ~cv.cov;
+  const uint32_t rh = cv.zh | cv.fh;
+  const uint32_t crf = cv.cov & Rm & ~Fm;
+  const uint32_t nzsum = (((nzA & 0x0f0f0f0fu) + ((nzA >> 4) & 0x0f0f0f0fu)) * 0x01010101u) >> 24;
+  const uint32_t bytes = nzsum + __popc(heads) + __popc(rh) + __popc(crf);
+  const uint32_t incl = wave_incl_sum32(bytes);
+  const uint32_t loff = incl - bytes;
+  if (l == 63) s_bytes[w] = incl;
+  __syncthreads();  // ---- B: wave byte counts -------------------------------------------
+
+  uint32_t woff = 0, agg = 0, s0 = (uint32_t)kTW;
+#pragma unroll
+  for (int v = 0; v < kWv; v++) {
+    const uint32_t bv = uniform32(s_bytes[v]);
+    if (v < w) woff += bv;
+    agg += bv;
+    const uint32_t fv = sum_fsw(sm[v]);
+    if (fv < (uint32_t)kWW && (uint32_t)(kWW * v) + fv < s0) s0 = (uint32_t)(kWW * v) + fv;
+  }
+  // next sync point after this lane's last word, tile-relative (the tile end when none)
+  uint32_t nsl = (uint32_t)kTW;
+  if (above) {
+    nsl = (uint32_t)(kWW * w + kK * ja) + fsa;
+  } else {
+#pragma unroll
+    for (int v = kWv - 1; v >= 0; v--)
+      if (v > w && sum_fsw(sm[v]) < (uint32_t)kWW) nsl = (uint32_t)(kWW * v) + sum_fsw(sm[v]);
+  }
+  if (l == 0) {
+    if (w == kWv - 1) {
+      a.tile_bytes[T] = agg;
+      // The run open at the tile end, when the word after the tile goes on with its stretch:
+      // its count byte (written here as if the batch ended at the tile end) is final only
+      // once the next tile has seen where the run stops.
+      const uint32_t b = t_exit & 0xffu;
+      a.thole[T] = (b != 0 && !next_sync) ? agg - 1u - ((t_exit & 0x100u) ? 8u * (255u - b) : 0u)
+                                           : 0xffffffffu;
+    }
+    if (w == 0) {
+      // the previous tile's open run ends in this tile: its count byte
+      const uint32_t b = bT & 0xffu;
+      a.tpatch[T] = b != 0 ? 0x100u | (255u - b + (s0 < b ? s0 : b)) : 0u;
+    }
+  }
+
+  // ---- requested positions (message starts) in this wave: bytes before them in the tile ---
+  if (a.pos) {
+    const uint64_t wend = wbase + kWW < tend ? wbase + kWW : tend;
+    uint64_t idx = pidx;
+    for (bool first = true;; first = false) {
+      const uint64_t i = idx + l;
+      const uint64_t p = first ? p0 : (i <= a.npos ? a.pos[i] : ~0ull);
+      const bool in_t = p >= tbase && p < tend;
+      const bool in_w = p >= wbase && p < wend;
+      const uint32_t rel = in_w ? (uint32_t)(p - wbase) : 0u;
+      const int L = (int)(rel >> 3);
+      const uint32_t k = rel & 7u;
+      const uint32_t oL = shfl32(loff, L), hL = shfl32(heads, L), rL = shfl32(rh, L);
+      const uint32_t cL = shfl32(crf, L), aL = shfl32(nzA, L);
+      const uint32_t mk = (1u << k) - 1u;
+      const uint32_t an = aL & ((1u << (4 * k)) - 1u);
+      const uint32_t nb = (((an & 0x0f0f0f0fu) + ((an >> 4) & 0x0f0f0f0fu)) * 0x01010101u) >> 24;
+      const uint32_t before = nb + __popc(hL & mk) + __popc(rL & mk) + __popc(cL & mk);
+      if (in_w) a.pos_out[i] = woff + oL + before;  // tile-relative; placed by pack_place
+      const uint64_t inm = ballot(in_t);
+      idx += __popcll(inm);
+      if (inm != ~0ull) break;
+    }
+  }
+
+  // ---- emission: records OR-ed into the staging slot at their own byte offsets ------------
+  const uint32_t nwin = agg <= kCap ? 1u : (agg + kCap - 1) / kCap;
+  uint32_t* const wtr = trash[w] + l;
+  u32x4* const dst = (u32x4*)(a.scr + T * (uint64_t)kScr);
+  for (uint32_t win = 0; win < nwin; win++) {
+    const uint32_t wlo = win * kCap;
+    const uint32_t whi = wlo + kCap;
+    const bool windowed = nwin > 1;
+    // the words pass through an opaque move per window, so nothing of the record bodies is
+    // hoisted out of this (almost always single-trip) loop: 8 words' worth of records held live
+    // at once cost the kernel its occupancy
+#pragma unroll
+    for (int k = 0; k < kK; k++) asm volatile("" : "+v"(xlo[k]), "+v"(xhi[k]));
+    uint32_t ecov = cv.cov, ezh = cv.zh, efh = cv.fh, eSY = SY, eR = Rm, enz = nzA, ensl = nsl;
+    uint32_t et0 = tags[0], et1 = tags[1];
+    asm volatile("" : "+v"(ecov), "+v"(ezh), "+v"(efh), "+v"(eSY), "+v"(eR), "+v"(enz));
+    asm volatile("" : "+v"(ensl), "+v"(et0), "+v"(et1));
+    const uint32_t etags[2] = {et0, et1};
+    uint32_t o = woff + loff;  // tile byte offset of the lane's next record
+    const uint32_t lbase = (uint32_t)(kWW * w + kK * l);
+    uint64_t sel_next = sel_tab[etags[0] & 0xffu];
+#pragma unroll
+    for (int k = 0; k < kK; k++) {
+      const uint32_t lo = xlo[k], hi = xhi[k];
+      const uint32_t tg = (etags[k >> 2] >> (8 * (k & 3))) & 0xffu;
+      const uint64_t sel = sel_next;
+      if (k + 1 < kK) sel_next = sel_tab[(etags[(k + 1) >> 2] >> (8 * ((k + 1) & 3))) & 0xffu];
+      const uint32_t nz = (enz >> (4 * k)) & 15u;
+      const bool cvk = (ecov >> k) & 1, zhk = (ezh >> k) & 1, fhk = (efh >> k) & 1;
+      const uint32_t aft = eSY & (0xfeu << k);
+      const uint32_t ns = aft ? lbase + (uint32_t)__builtin_ctz(aft) : ensl;
+      const uint32_t c8 = min(ns - (lbase + (uint32_t)k) - 1u, 255u) << 8;
+      uint32_t r0 = __builtin_amdgcn_perm(hi, lo, (uint32_t)sel) | tg | (zhk ? c8 : 0u);
+      uint32_t r1 = __builtin_amdgcn_perm(hi, lo, (uint32_t)(sel >> 32));
+      uint32_t r2 = fhk ? ((hi >> 24) | c8) : 0u;
+      uint32_t L = 1u + nz + ((zhk || fhk) ? 1u : 0u);
+      if (cvk) {
+        r0 = lo;
+        r1 = hi;
+        r2 = 0;
+        L = ((eR >> k) & 1) ? 8u : 0u;
+      }
+      bool put = L != 0;
+      if (windowed) put = put && o < whi && o + L > wlo;
+      const uint32_t so = kPadF + o - wlo;  // slot byte (in range whenever put)
+      const uint32_t sh = 8u * (so & 3u);
+      // an empty record ORs into the lane's trash window (overlapping windows: the 32 lanes of a
+      // bank group hit 32 banks)
+      uint32_t* const wp = put ? stg + (so >> 2) : wtr;
+      const uint64_t q01 = (((uint64_t)r1 << 32) | r0) << sh;
+      const uint64_t q12 = (((uint64_t)r2 << 32) | r1) << sh;
+      const uint32_t w3 = (uint32_t)(((uint64_t)r2 << sh) >> 32);
+      atomicOr(wp, (uint32_t)q01);
+      atomicOr(wp + 1, (uint32_t)(q01 >> 32));
+      atomicOr(wp + 2, (uint32_t)(q12 >> 32));
+      if (ballot(w3 != 0)) atomicOr(wp + 3, w3);
+      o += L;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();  // ---- C: staged ------------------------------------------------------
+    // the window's bytes to the tile's scratch slot: aligned 16-byte copies
+    const uint32_t n16 = ((whi < agg ? whi : agg) - wlo + 15u) >> 4;
+    for (uint32_t i = tid; i < n16; i += 64 * kWv) dst[(wlo >> 4) + i] = ((const u32x4*)stg)[1 + i];
+    if (windowed) {
+      __syncthreads();
+      for (int i = tid; i < kSlotDw / 4; i += 64 * kWv) ((u32x4*)stg)[i] = (u32x4){0, 0, 0, 0};
+      __syncthreads();
+    }
+  }
 }
 
-__global__ void chunk_bits_kernel(const uint64_t* __restrict__ off, uint64_t n, uint64_t N,
-                                  unsigned long long* __restrict__ bits, TileFirstJob tf,
-                                  uint32_t tf_block) {
-  if (run_tile_first(tf, tf_block)) return;
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i == 0 && N > 0) atomicOr(bits, 1ull);  // word 0 always starts a chunk
-  if (i >= n) return;
-  const uint64_t p = off[i];
-  if (p < N && off[i + 1] > p) atomicOr(bits + (p >> 6), 1ull << (p & 63));
+// ---------------------------------------------------------------------------------------------
+// 2. Placement: one wave per tile moves the tile's bytes from its scratch slot to their final
+//    place (out + tile_off[T], from the scan of the tile byte counts), writing the final count
+//    byte of a run the next tile closed, and turns the tile's requested positions into output
+//    offsets.  (A tile's bytes are a few KiB at most: a whole workgroup per tile spent more on
+//    its own start than on the copy.)
+__global__ __launch_bounds__(256) void pack_place_kernel(PackTileArgs a) {
+  const int l = lane_id();
+  const uint64_t T = (uint64_t)blockIdx.x * 4 + uniform32(threadIdx.x >> 6);
+  if (T >= a.ntiles) return;
+  const uint64_t off = a.tile_off[T];
+  const uint32_t n = (uint32_t)(a.tile_off[T + 1] - off);
+  const uint64_t total = a.tile_off[a.ntiles];
+  if (total > a.out_capacity) {
+    if (T == 0 && l == 0) raise_error(a.err, kErrCapacity);
+  } else if (n) {
+    // count byte patched by the next tile (position, value) -- wave-uniform
+    const uint32_t hole = T + 1 < a.ntiles ? a.thole[T] : 0xffffffffu;
+    const uint32_t pv = hole != 0xffffffffu ? a.tpatch[T + 1] : 0u;
+    const uint8_t* const src = a.scr + T * (uint64_t)kScr;
+    uint8_t* const o0 = a.out + off;
+    const uint64_t A0 = (uint64_t)(uintptr_t)o0;
+    const uint64_t A1 = A0 + n;
+    const uint64_t al = (A0 + 15) & ~15ull;
+    const uint32_t head = (uint32_t)((al < A1 ? al : A1) - A0);  // bytes before 16-byte alignment
+    auto byte_at = [&](uint32_t j) -> uint8_t {
+      const uint8_t v = src[j];
+      return (pv && j == hole) ? (uint8_t)pv : v;
+    };
+    if ((uint32_t)l < head) o0[l] = byte_at(l);
+    if (A1 > al) {
+      const uint32_t body = (uint32_t)((A1 & ~15ull) - A0);
+      const uint32_t nblk = (body - head) >> 4;
+      // output block i = source bytes [head + 16i, head + 16i + 16): source dwords from
+      // (head >> 2) + 4i, shifted by head & 3 bytes
+      const uint32_t rr = head & 3u;
+      const uint32_t* const s32 = (const uint32_t*)src;
+      u32x4* const ob = (u32x4*)(o0 + head);
+      for (uint32_t i = l; i < nblk; i += 64) {
+        const uint32_t d = (head >> 2) + 4 * i;
+        const uint32_t v0 = s32[d], v1 = s32[d + 1], v2 = s32[d + 2], v3 = s32[d + 3],
+                       v4 = s32[d + 4];
+        u32x4 v;
+        v.x = __builtin_amdgcn_alignbyte(v1, v0, rr);
+        v.y = __builtin_amdgcn_alignbyte(v2, v1, rr);
+        v.z = __builtin_amdgcn_alignbyte(v3, v2, rr);
+        v.w = __builtin_amdgcn_alignbyte(v4, v3, rr);
+        const uint32_t b0 = head + 16 * i;
+        if (pv && hole >= b0 && hole < b0 + 16) {
+          const uint32_t q = hole - b0, sh = 8 * (q & 3), m = ~(0xffu << sh),
+                         x = (pv & 0xffu) << sh;
+          if (q < 4) v.x = (v.x & m) | x;
+          else if (q < 8) v.y = (v.y & m) | x;
+          else if (q < 12) v.z = (v.z & m) | x;
+          else v.w = (v.w & m) | x;
+        }
+        ob[i] = v;
+      }
+      if (body + (uint32_t)l < n) o0[body + l] = byte_at(body + l);
+    }
+  }
+  // requested positions: tile-relative offsets (pack_tile) + the tile's output offset;
+  // positions at or past the batch end (the last tile's share) take the total
+  if (a.pos) {
+    const uint64_t i0 = a.tile_first[T];
+    const uint64_t i1 = T + 1 < a.ntiles ? a.tile_first[T + 1] : a.npos + 1;
+    for (uint64_t i = i0 + l; i < i1; i += 64) {
+      if (T + 1 == a.ntiles && a.pos[i] >= a.nwords) a.pos_out[i] = total;
+      else a.pos_out[i] += off;
+    }
+  }
+  if (T + 1 == a.ntiles && l == 0 && a.total_out) *a.total_out = total;
 }
-
-// tile_first[t] = first index i in [0, npos] with pos[i] >= t*T (binary search).
 
 }  // namespace
 
-// ---------------------------------------------------------------------------------------------
-int pack_steps() {
-  static int steps = [] {
-    const char* e = getenv("CPK_PACK_STEPS");  // tuning knob: 4, 8 or 16 (default)
-    const int v = e ? atoi(e) : kPackSteps;
-    return (v == 8 || v == 16 || v == 4) ? v : kPackSteps;
-  }();
-  return steps;
-}
-
-template <int S, bool PF>
-hipError_t launch_pack_s(const PackTileArgs& a, hipStream_t stream) {
-  // persistent grid: every block resident (the stamp build has its own register footprint)
-  static const unsigned cap =
-      resident_blocks((const void*)pack_tiles_kernel<S, PF, false>, 256, 0);
-  static const unsigned cap_st =
-      resident_blocks((const void*)pack_tiles_kernel<S, PF, true>, 256, 0, 128);
-  const uint64_t want = (a.ntiles + 3) / 4;
-  const unsigned c = a.stamps ? cap_st : cap;
-  const unsigned blocks = (unsigned)(want < c ? want : c);
-  if (a.stamps)
-    hipLaunchKernelGGL((pack_tiles_kernel<S, PF, true>), dim3(blocks), dim3(256), 0, stream, a);
-  else
-    hipLaunchKernelGGL((pack_tiles_kernel<S, PF, false>), dim3(blocks), dim3(256), 0, stream, a);
-  return hipGetLastError();
-}
-
-// Prefetch of the next tile's words into registers during the current tile: on by default at
-// 16 steps per tile, where LDS (the staging ring) and not registers bounds occupancy at 3 waves
-// per SIMD; off at 8 steps, where the registers would cost occupancy.  Env CPK_PACK_PF=0/1.
-static bool pack_prefetch() {
-  static const bool on = [] {
-    const char* e = getenv("CPK_PACK_PF");
-    return e ? atoi(e) != 0 : pack_steps() == 16;
-  }();
-  return on;
-}
-
-// Two-pass form (default).  stage 0: count pass, persistent grid (its waves hand entry budgets
-// over); stage 1: emit pass, one wave per tile.  The caller scans tile_bytes into tile_off in
-// between.
-template <int S>
-hipError_t launch_pack_stage_s(int stage, const PackTileArgs& a, hipStream_t stream) {
-  if (stage == 0) {
-    static const unsigned cap =
-        resident_blocks((const void*)pack_tiles_kernel<S, false, false, kCount>, 256, 0);
-    const uint64_t want = (a.ntiles + 3) / 4;
-    const unsigned blocks = (unsigned)(want < cap ? want : cap);
-    hipLaunchKernelGGL((pack_tiles_kernel<S, false, false, kCount>), dim3(blocks), dim3(256), 0,
-                       stream, a);
-  } else {
-    hipLaunchKernelGGL((pack_tiles_kernel<S, false, false, kEmit>),
-                       dim3((unsigned)((a.ntiles + 3) / 4)), dim3(256), 0, stream, a);
-  }
-  return hipGetLastError();
-}
-
-hipError_t launch_pack_stage(int stage, const PackTileArgs& a, hipStream_t stream) {
-  if (a.ntiles == 0) return hipSuccess;
-  switch (pack_steps()) {
-    case 4: return launch_pack_stage_s<4>(stage, a, stream);
-    case 8: return launch_pack_stage_s<8>(stage, a, stream);
-    default: return launch_pack_stage_s<16>(stage, a, stream);
-  }
-}
-
-bool pack_fused() {
-  static const bool on = [] {
-    // A/B knob: CPK_PACK_TWO_PASS=1 selects count + scan + emit (measured slower on C2/C4/C5
-    // than the single-pass kernel once the emission's LDS atomics were predicated)
-    const char* e = getenv("CPK_PACK_TWO_PASS");
-    return !(e && atoi(e) != 0);
-  }();
-  return on;
-}
-
 hipError_t launch_pack_tiles(const PackTileArgs& a, hipStream_t stream) {
   if (a.ntiles == 0) return hipSuccess;
-  const bool pf = pack_prefetch();
-  switch (pack_steps()) {
-    case 4: return pf ? launch_pack_s<4, true>(a, stream) : launch_pack_s<4, false>(a, stream);
-    case 8: return pf ? launch_pack_s<8, true>(a, stream) : launch_pack_s<8, false>(a, stream);
-    default: return pf ? launch_pack_s<16, true>(a, stream) : launch_pack_s<16, false>(a, stream);
-  }
-}
-
-hipError_t launch_message_bits(const uint64_t* words, const uint64_t* off, uint64_t n,
-                               uint64_t* bits, int32_t* status, const TileFirstJob& tf,
-                               hipStream_t stream) {
-  const unsigned nb = (unsigned)((n + 255) / 256);
-  if (nb + tile_first_blocks(tf) == 0) return hipSuccess;
-  hipLaunchKernelGGL(message_bits_kernel, dim3(nb + tile_first_blocks(tf)), dim3(256), 0, stream,
-                     words, off, n, (unsigned long long*)bits, status, tf, nb);
+  if (a.ntiles >= (1ull << 31)) return hipErrorInvalidValue;
+  pack_tile_kernel<<<(unsigned)a.ntiles, 256, 0, stream>>>(a);
   return hipGetLastError();
 }
 
-hipError_t launch_chunk_bits(const uint64_t* off, uint64_t n, uint64_t N, uint64_t* bits,
-                             const TileFirstJob& tf, hipStream_t stream) {
-  const unsigned nb = (n == 0 && N == 0) ? 0u : (unsigned)((n + 256) / 256);
-  if (nb + tile_first_blocks(tf) == 0) return hipSuccess;
-  hipLaunchKernelGGL(chunk_bits_kernel, dim3(nb + tile_first_blocks(tf)), dim3(256), 0, stream,
-                     off, n, N, (unsigned long long*)bits, tf, nb);
+hipError_t launch_pack_place(const PackTileArgs& a, hipStream_t stream) {
+  if (a.ntiles == 0) return hipSuccess;
+  pack_place_kernel<<<(unsigned)((a.ntiles + 3) / 4), 256, 0, stream>>>(a);
   return hipGetLastError();
 }
-
 
 }  // namespace cpk

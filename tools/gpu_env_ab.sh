@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B of environment knobs on the GPU box: for each ENVS entry ("base" or "K=V,K2=V2"), short
 # bench runs of the configs in CFGS (default c2 c4) printing per-kernel times.
-#   gpurun -- 'ENVS="base CPK_PACK4_PERSIST=1" bash tools/gpu_env_ab.sh TAG'
+#   gpurun -- 'ENVS="base CPK_DEBUG_SKIP=1" bash tools/gpu_env_ab.sh TAG'
 set -o pipefail
 TAG=${1:-ab}
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"

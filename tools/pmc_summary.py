@@ -20,8 +20,10 @@ KERNELS = {"pack_tiles_kernel": "pack_tiles", "index_kernel": "unpack_index",
 
 
 def short(name):
-    if "pack3_kernel" in name:
-        return "pack3"
+    if "pack_tile_kernel" in name:
+        return "pack_tile"
+    if "pack_place_kernel" in name:
+        return "pack_place"
     if "pack_tiles_kernel" in name:  # template <S, PF, STAMPS, MODE>: 1 count, 2 emit
         mode = name.split("pack_tiles_kernel<")[1].split(">")[0].split(",")[-1].strip()
         return {"1": "pack_count", "2": "pack_emit"}.get(mode, "pack")
