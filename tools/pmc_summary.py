@@ -14,9 +14,11 @@ import sys
 from collections import defaultdict
 
 out_dir, tag, cfg = sys.argv[1], sys.argv[2], sys.argv[3]
-KERNELS = {"pack_tiles_kernel": "pack_tiles", "index_kernel": "unpack_index",
-           "resolve1_kernel": "unpack_resolve1", "resolve2_kernel": "unpack_resolve2",
-           "expand_kernel": "unpack_expand", "fallback_kernel": "unpack_fallback"}
+KERNELS = {"index_kernel": "unpack_index", "resolve1_kernel": "unpack_resolve1",
+           "resolve2_kernel": "unpack_resolve2", "expand_kernel": "unpack_expand",
+           "fallback_kernel": "unpack_fallback", "header_kernel": "unpack_header",
+           "message_bits_kernel": "pack_framing", "chunk_bits_kernel": "pack_framing",
+           "scan_kernel": "scan", "fill_kernel": "fill"}
 
 
 def short(name):
@@ -24,9 +26,6 @@ def short(name):
         return "pack_tile"
     if "pack_place_kernel" in name:
         return "pack_place"
-    if "pack_tiles_kernel" in name:  # template <S, PF, STAMPS, MODE>: 1 count, 2 emit
-        mode = name.split("pack_tiles_kernel<")[1].split(">")[0].split(",")[-1].strip()
-        return {"1": "pack_count", "2": "pack_emit"}.get(mode, "pack")
     for k, v in KERNELS.items():
         if k in name:
             return v
@@ -66,4 +65,16 @@ for k in sorted(vals):
         traffic[k] = {"read_bytes": round(rd), "write_bytes": round(wr), "bytes": round(rd + wr),
                       "note": "rocprofv3 FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE, per launch"}
         print(f"   HBM traffic per launch: read {rd / 1e6:.1f} MB  write {wr / 1e6:.1f} MB")
+# the pack "launch" the bench times is tile + scan + place; per-step HBM bytes of every kernel
+pk = [k for k in ("pack_tile", "pack_place") if k in traffic]
+if pk:
+    traffic["pack"] = {f: sum(traffic[k][f] for k in pk) for f in ("read_bytes", "write_bytes",
+                                                                   "bytes")}
+    traffic["pack"]["note"] = "pack_tile + pack_place (the bench's pack timer), per launch"
+traffic["step_total_bytes"] = sum(v["bytes"] for k, v in traffic.items()
+                                  if isinstance(v, dict) and k != "pack")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402  (kernel_source_hash: pins the file to the kernels it measured)
+
+traffic["kernel_src_sha256"] = bench.kernel_source_hash()
 json.dump(traffic, open(os.path.join(out_dir, f"{tag}_traffic_{cfg}.json"), "w"), indent=1)
