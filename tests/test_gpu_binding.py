@@ -32,3 +32,28 @@ def test_reference_callers_through_binding():
                        text=True, timeout=120)
     assert r.returncode == 0, r.stderr[-3000:]
     assert "binding ok" in r.stdout and "addressbook" in r.stdout
+
+
+ABIN = os.path.join(ROOT, "oracle", "_ref", "kj_async_binding_test")
+
+
+@pytest.mark.skipif(not os.path.exists(ABIN), reason="oracle/_ref/kj_async_binding_test not built")
+def test_async_message_stream_through_binding():
+    # capnp::MessageStream (serialize-async.h:42-108) with packed framing on the reference's kj
+    # event loop: cpk_kj::PackedMessageStream over an OS socket pair and an in-memory kj pipe,
+    # wire bytes == the reference's packed fixtures (integration/kj_async_binding_test.c++)
+    import re
+
+    nm = subprocess.run(["nm", "-C", ABIN], capture_output=True, text=True).stdout
+    assert not re.search(r"\s(capnp::_::PackedOutputStream|capnp::_::PackedInputStream|"
+                         r"capnp::writePackedMessage|capnp::PackedMessageReader)", nm)
+    assert re.search(r"\sU cpk_read_packed_message_host", nm)
+    assert re.search(r"\sU cpk_pack_messages_host", nm)
+    try:
+        r = subprocess.run([ABIN, os.path.join(ROOT, "tests", "golden")], capture_output=True,
+                           text=True, timeout=60)
+    except subprocess.TimeoutExpired as e:  # name the step that did not finish
+        err = e.stderr.decode() if isinstance(e.stderr, bytes) else (e.stderr or "")
+        pytest.fail("kj_async_binding_test timed out after:\n" + err[-2000:])
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "async binding ok" in r.stdout
