@@ -396,13 +396,11 @@ def summarize(res, world, copy_gbps):
     # write U); SURVEY.md 8(d)
     rt = 2.0 * (U + P) / t_step / 1e9
     rd = (U + P) / t_step / 1e9
-    algo = {"pack": U + P, "unpack_index": P, "unpack_expand": U + P}
-    if kms.get("pack_count", 0) > 0:  # two-pass pack (A/B knob)
-        algo = {"pack_count": U, "pack_emit": U + P, "unpack_index": P, "unpack_expand": U + P}
+    algo = {"pack": U + P, "unpack_tiles": U + P}
     kern = {k: {"ms": round(kms[k], 4),
                 "GBps": round(algo[k] / (kms[k] * 1e-3) / 1e9, 1) if kms[k] > 0 else None,
                 "algorithmic_bytes": int(algo[k])} for k in algo}
-    for k in ("unpack_resolve", "unpack_fallback"):
+    for k in ("unpack_fallback",):
         kern.setdefault(k, {"ms": round(kms[k], 4)})
     dom = max(algo, key=lambda k: kms[k])
     dom_ach = algo[dom] / (kms[dom] * 1e-3) / 1e9 if kms[dom] > 0 else 0.0

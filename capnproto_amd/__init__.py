@@ -284,8 +284,7 @@ class Codec:
                                              C.byref(ul)), "cpk_timing_read")
         return pm.value, pl.value, um.value, ul.value
 
-    TIMERS = ("pack", "unpack", "unpack_index", "unpack_resolve", "unpack_expand",
-              "unpack_fallback", "pack_count", "pack_emit")
+    TIMERS = ("pack", "unpack", "unpack_tiles", "unpack_fallback", "t4", "t5", "t6", "t7")
 
     def timing_read_all(self):
         """{timer name: (summed ms, launches)} since the last read (include/cpk.h timers)."""

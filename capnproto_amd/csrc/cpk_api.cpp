@@ -22,9 +22,8 @@ struct cpk_ctx {
   // device staging for the *_host entry points
   void* stage[4] = {nullptr, nullptr, nullptr, nullptr};
   size_t stage_size[4] = {0, 0, 0, 0};
-  // measurement hooks: [0] pack tile kernels (count .. emit), [1] unpack (index .. fallback),
-  // [2 + stage] each unpack stage kernel (index, resolve, expand, fallback), [6] pack count,
-  // [7] pack emit
+  // measurement hooks: [0] pack (tile, scan, placement), [1] unpack (tiles .. fallback),
+  // [2 + stage] each unpack stage kernel (tiles, fallback)
   bool timing = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[CPK_TIMERS];
   std::vector<hipEvent_t> pool;
@@ -246,35 +245,19 @@ struct UnpackScratch {
   uint32_t* fail_count;
   uint32_t* scan_counter;
   uint64_t* scan_desc;
-  size_t zero_bytes;
   uint64_t* desc;
-  uint64_t* gdesc;
+  uint32_t* x0p;
+  size_t zero_bytes;
   uint64_t* tile_first;
   uint64_t* tile_firstpos;
   uint64_t* flat;
   int32_t* hdr_status;
   uint32_t* fail_list;
-  uint64_t* tm;
-  uint32_t* t_wex;
-  uint32_t* t_x0;
-  uint32_t* t_fms;
-  uint32_t* t_wpre;
-  uint32_t* t_wpost;
-  uint32_t* t_flags;
-  uint32_t* t_ent;
-  int32_t* t_delta;
-  uint32_t* t_xe;
-  uint32_t* t_umask;
-  uint32_t* r1_x;
-  uint32_t* r1_w;
-  uint64_t* g_notok;
-  uint64_t* g_start;
   size_t total;
 };
 
-// Unpack scratch: per message ~40 B, per 4 KiB tile ~870 B (chain-0 masks 512 B, sub-tile word
-// prefixes 256 B, merge table 64 B, descriptors).  Only the fallback list state and the scan
-// descriptors need zeroing; every tile table is fully written before it is read.
+// Unpack scratch: per message ~40 B, per 4 KiB tile 28 B (descriptor, chain-0 exit, first
+// message).  The fallback list state, the scan descriptors and the tile descriptors are zeroed.
 UnpackScratch carve_unpack(void* base, uint64_t ntiles, uint64_t n) {
   Carve c(base);
   UnpackScratch s;
@@ -282,29 +265,14 @@ UnpackScratch carve_unpack(void* base, uint64_t ntiles, uint64_t n) {
   s.fail_count = c.take<uint32_t>(4);
   s.scan_counter = c.take<uint32_t>(4);
   s.scan_desc = c.take<uint64_t>(cpk::scan_tiles(n + 1));
-  s.zero_bytes = c.off;
   s.desc = c.take<uint64_t>(ntiles);
-  s.gdesc = c.take<uint64_t>((ntiles + 63) / 64);
+  s.x0p = c.take<uint32_t>(ntiles);
+  s.zero_bytes = c.off;
   s.tile_first = c.take<uint64_t>(ntiles);
   s.tile_firstpos = c.take<uint64_t>(ntiles);
   s.flat = c.take<uint64_t>(n + 1);
   s.hdr_status = c.take<int32_t>(n);
   s.fail_list = c.take<uint32_t>(n);
-  s.tm = c.take<uint64_t>(64 * ntiles);
-  s.t_wex = c.take<uint32_t>(64 * ntiles);
-  s.t_x0 = c.take<uint32_t>(ntiles);
-  s.t_fms = c.take<uint32_t>(ntiles);
-  s.t_wpre = c.take<uint32_t>(ntiles);
-  s.t_wpost = c.take<uint32_t>(ntiles);
-  s.t_flags = c.take<uint32_t>(ntiles);
-  s.t_ent = c.take<uint32_t>(ntiles);
-  s.t_delta = c.take<int32_t>(16 * ntiles);
-  s.t_xe = c.take<uint32_t>(16 * ntiles);
-  s.t_umask = c.take<uint32_t>(ntiles);
-  s.r1_x = c.take<uint32_t>(ntiles);
-  s.r1_w = c.take<uint32_t>(ntiles);
-  s.g_notok = c.take<uint64_t>((ntiles + 63) / 64);
-  s.g_start = c.take<uint64_t>((ntiles + 63) / 64);
   s.total = c.off;
   return s;
 }
@@ -368,35 +336,16 @@ cpk_status unpack_common(cpk_ctx* ctx, uint32_t mode, const uint8_t* d_packed, u
   a.rec_pos = d_rec_pos;
   a.mode = mode;
   a.ntiles = ntiles;
-  a.tile_counter = nullptr;
   a.desc = s.desc;
-  a.gdesc = s.gdesc;
-  a.gcnt = nullptr;
-  a.state = nullptr;
+  a.x0p = s.x0p;
   a.fail_flag = s.fail_flag;
   a.fail_list = s.fail_list;
   a.fail_count = s.fail_count;
   a.err = ctx->err;
   a.stamps = cpk::debug_stamps(1);  // diagnostic counters (CPK_STAMPS=1), else NULL
-  a.stamps2 = cpk::debug_stamps(2);  // diagnostic phase cycles of index_kernel
   a.debug_skip = cpk::debug_skip();
-  a.tm = s.tm;
-  a.t_wex = s.t_wex;
-  a.t_x0 = s.t_x0;
-  a.t_fms = s.t_fms;
-  a.t_wpre = s.t_wpre;
-  a.t_wpost = s.t_wpost;
-  a.t_flags = s.t_flags;
-  a.t_delta = s.t_delta;
-  a.t_xe = s.t_xe;
-  a.t_umask = s.t_umask;
-  a.r1_x = s.r1_x;
-  a.r1_w = s.r1_w;
-  a.g_notok = s.g_notok;
-  a.g_start = s.g_start;
-  a.t_ent = s.t_ent;
   TimedLaunch tl(ctx, 1, stream);
-  for (int stage = cpk::kUnpackIndex; stage <= cpk::kUnpackFallback; stage++) {
+  for (int stage = cpk::kUnpackTiles; stage <= cpk::kUnpackFallback; stage++) {
     TimedLaunch tk(ctx, 2 + stage, stream);
     e = cpk::launch_unpack_stage(stage, a, stream);
     tk.done();
@@ -949,6 +898,15 @@ extern "C" cpk_status cpk_debug_stamps(int which, uint64_t* out16) {
   for (int i = 0; i < 16; i++) out16[i] = 0;
   for (size_t r = 0; r < rows.size(); r++) out16[r % cpk::kStampSlots] += rows[r];
   if (hipMemset(b, 0, rows.size() * 8) != hipSuccess) return CPK_ERR_HIP;
+  return CPK_OK;
+}
+
+// Diagnostic (not in include/cpk.h): raw copy of a stamp buffer.
+extern "C" cpk_status cpk_debug_dump(int which, uint64_t* out, uint64_t n) {
+  unsigned long long* b = cpk::debug_stamps(which);
+  if (!b || !out || n > (uint64_t)cpk::kStampSlots * cpk::kStampRows) return CPK_ERR_INVALID_ARGUMENT;
+  if (hipDeviceSynchronize() != hipSuccess) return CPK_ERR_HIP;
+  if (hipMemcpy(out, b, n * 8, hipMemcpyDeviceToHost) != hipSuccess) return CPK_ERR_HIP;
   return CPK_OK;
 }
 

@@ -68,39 +68,19 @@ struct UnpackArgs {
   uint64_t* rec_pos;            // optional: packed byte of the record whose head is word i
   uint32_t mode;                // 0 messages, 1 exact-size chunks (flat-packed), 2 size only
   uint64_t ntiles;
-  uint32_t* tile_counter;
-  uint64_t* desc;
-  uint64_t* gdesc;
-  uint32_t* gcnt;
-  uint32_t* state;
+  uint64_t* desc;               // ntiles tile descriptors (cpk_unpack.hip), zeroed
+  uint32_t* x0p;                // ntiles chain-0 exits (0x80000000 | exit), zeroed
   uint32_t* fail_flag;          // per message
   uint32_t* fail_list;
   uint32_t* fail_count;
   uint32_t* err;
   unsigned long long* stamps;   // diagnostic build only (env CPK_STAMPS), else NULL
-  unsigned long long* stamps2;  // diagnostic: per-phase cycles of index_kernel
-  uint32_t debug_skip;
-  // tile tables: index_kernel -> resolve_kernel -> expand_kernel (cpk_unpack.hip)
-  uint64_t* tm;                 // ntiles*64 chain-0 record-start masks (bit = byte of a sub-tile)
-  uint32_t* t_wex;              // ntiles*64 chain-0 words before each 64-byte sub-tile
-  uint32_t* t_x0;               // chain-0 exit (tile-relative; >= 1<<24: past the batch end)
-  uint32_t* t_fms;              // first message start (tile-relative; tile size if none)
-  uint32_t* t_wpre;             // chain-0 words before t_fms
-  uint32_t* t_wpost;            // words from the last message start on
-  uint32_t* t_flags;
-  int32_t* t_delta;             // ntiles*16: entry e's words minus chain 0's (no merge: its words)
-  uint32_t* t_xe;               // ntiles*16: exit of entry e's chain when it does not merge
-  uint32_t* t_umask;            // bit e: entry e's chain does not merge into chain 0
-  uint32_t* r1_x;               // resolve pass 1: exit under the optimistic entry
-  uint32_t* r1_w;               // resolve pass 1: words before the first message start
-  uint64_t* g_notok;            // per 64 tiles: optimistic entry did not merge
-  uint64_t* g_start;            // per 64 tiles: tile holds a message start
-  uint32_t* t_ent;              // true entry (tile-relative)
+  uint32_t debug_skip;          // diagnostic (env CPK_DEBUG_SKIP): 16 no record batches, 32 no lists
   const uint64_t* tile_firstpos;  // in_off[tile_first[t]]: the first message start >= tile start
 };
 
 // Unpack stages (launch_unpack_stage), in launch order.
-constexpr int kUnpackIndex = 0, kUnpackResolve = 1, kUnpackExpand = 2, kUnpackFallback = 3;
+constexpr int kUnpackTiles = 0, kUnpackFallback = 1;
 
 uint32_t debug_skip();
 
@@ -109,7 +89,7 @@ uint32_t debug_skip();
 constexpr int kStampSlots = 16;
 constexpr int kStampRows = 256;
 
-// Diagnostic stamp buffers (env CPK_STAMPS=1): [1] unpack counters, [2] index phases.
+// Diagnostic stamp buffers (env CPK_STAMPS=1): [1] unpack counters.
 unsigned long long* debug_stamps(int which);
 
 hipError_t launch_unpack_header(const uint8_t* packed, const uint64_t* in_off, uint64_t n,

@@ -7,31 +7,21 @@
 // byte (plus 8*count raw bytes for 0xff); a run may not overshoot the words being read.
 //
 // Record starts form a chain (next = p + record length) that restarts at every message start.
-// The batch of packed bytes is cut into 4 KiB tiles.  No kernel waits on another workgroup:
-// every hand-off is a kernel boundary.
-//   1. header_kernel    one thread per message: decodes the first word and the rest of the
-//                       segment table with the reference's checks; yields the flat size.
-//   2. scan             message word offsets (cpk_scan.hip).
-//   3. index_kernel     one wave per tile.  Resolves "chain 0", the chain entered at the tile's
-//                       first byte: each lane walks its 64-byte sub-tile speculatively (message
-//                       clips kept out of the step), then a fixed point settles every lane's true
-//                       entry.  Stores chain 0's record-start masks (512 B per tile), its exit, word
-//                       counts, and a merge table: for entries 1..9 the word difference to chain 0
-//                       where their chain meets it, or their own exit and words when it never does.
-//   4. resolve1_kernel  one thread per tile: optimistic entry = the predecessor's chain-0 exit;
-//                       table lookup (or a walk through global memory for an entry past a raw
-//                       run); marks the tiles whose entry does not merge, per 64-tile group.
-//      resolve2_kernel  an optimistic entry is wrong only after such a tile with no message start
-//                       in between: those stretches are replayed from their first tile; writes
-//                       segmented tile word values and 64-tile group aggregates.
-//   5. expand_kernel    one wave per tile.  Word offset by a look-back over the (final) tile
-//                       values (both hops' loads in one round trip), chain 0 patched for the true
-//                       entry, then records are expanded one lane per record, 64 consecutive
-//                       records at a time (record list per quarter tile, built four lanes per
-//                       sub-tile; coalesced stores); zero and raw runs are written by the wave.
-//   6. fallback_kernel  messages flagged by an unsettled fixed point or a capped walk, decoded
-//                       serially (one wave per message).  None of the benchmark configurations
-//                       needs it; the error tests do.
+// The batch of packed bytes is cut into 4 KiB tiles, one wave each; P is read once.
+//   1. header_kernel        one thread per message: decodes the first word and the rest of the
+//                           segment table with the reference's checks; yields the flat size.
+//   2. scan                 message word offsets (cpk_scan.hip).
+//   3. unpack_tiles_kernel  per tile: "chain 0", the chain entered at the tile's first byte, from
+//                           speculative walks of the 64-byte sub-tiles and a lane fixed point;
+//                           its exit is published at once.  The tile's optimistic entry is where
+//                           the predecessor's chain 0 leads; its chain from there (traced until
+//                           it meets chain 0) gives an aggregate that a look-back over the
+//                           predecessors confirms or corrects (a tile holding a message start is
+//                           inclusive at once).  Then the records are expanded one lane per
+//                           record, 64 consecutive records at a time (coalesced stores), zero and
+//                           raw runs written by the wave.
+//   4. fallback_kernel      messages flagged by an unsettled fixed point, decoded serially (one
+//                           wave per message).  None of the benchmark configurations needs it.
 #include <limits.h>
 
 #include "cpk_device.h"
@@ -44,14 +34,7 @@ namespace {
 constexpr int kB = (int)kUnpackTileBytes;  // 4096
 constexpr int kPad = 16;
 constexpr int kDead = 1 << 24;  // chain ran into the end of the batch
-constexpr uint64_t kSegBit = 1ull << 61;
-constexpr int kTab = 16;                    // merge-table slots per tile
-constexpr int kTabWalk = 10;                // entries 1..9 are walked (a record that is not a
-                                            // raw run ends at most 9 bytes into the next tile)
-constexpr int kMergeCap = 48;               // merge-walk records before the jump walk
-constexpr uint32_t kTileUnsettled = 1;      // lane fixed point hit its iteration cap
-constexpr uint32_t kTileHasStart = 2;       // a message starts inside the tile
-constexpr int kWalkCap = 4096;              // records a resolve thread walks before giving up
+constexpr int kMergeCap = 48;               // entry-walk records before the jump walk
 
 // status codes (include/cpk.h)
 constexpr int32_t kOK = 0, kEOF = 1, kOvershoot = 2, kTooMany = 3, kTooLarge = 4, kInvalid = 5;
@@ -144,18 +127,9 @@ __device__ __forceinline__ int rec_len(uint32_t tag, uint32_t cnt) {
   return 1 + __popc(tag) + ((tag == 0 || tag == 0xff) ? 1 : 0) + (tag == 0xff ? 8 * (int)cnt : 0);
 }
 
-// Index staging layout: sub-tile l (tile bytes [64l, 64l + 64)) is row l of kRow bytes, its 64
-// bytes followed by a copy of the next 12, so every byte a walk step reads (p, p + 1, p + 9)
-// lies in p's row.  Rows start 19 dwords apart: lanes walking their own sub-tiles in step hit 32
-// distinct banks (at a 64-byte stride every lane's row began on bank 0 or 16: 16-way conflicts).
-#ifndef CPK_INDEX_ROW
-#define CPK_INDEX_ROW 64
-#endif
-constexpr int kRow = CPK_INDEX_ROW;  // 64: plain layout (A/B builds only)
-constexpr int kRowBytes = 64 * kRow + 16;
-__device__ __forceinline__ const uint8_t* ix(const uint8_t* d, int p) {
-  return d + p + (kRow - 64) * (p >> 6);
-}
+// Staged tile bytes: tile byte p at d[p], zero past the batch end, kPad bytes past the tile, so
+// every byte a walk step reads (p, p + 1, p + 9) is in LDS.
+__device__ __forceinline__ const uint8_t* ix(const uint8_t* d, int p) { return d + p; }
 
 // Record length at tile position p given the staged rows (no clipping).
 __device__ __forceinline__ int record_len(const uint8_t* d, int p) {
@@ -498,18 +472,10 @@ __device__ __forceinline__ void run_jobs(const UnpackArgs& a, const RunJob& job,
 }
 
 // Diagnostic counters (env CPK_STAMPS=1 only; a.stamps is NULL otherwise).
-enum : int { kDbgUnsettled = 0, kDbgTableMiss, kDbgWalkFail, kDbgWalks, kDbgFlagged,
-             kDbgUmaskTiles, kDbgMergeSteps, kDbgSettleIters, kDbgWalkSteps, kDbgWalkStepsMax,
-             kDbgMerge64, kDbgMerge256, kDbgMerge1k, kDbgSettle8, kDbgSettle24 };
+enum : int { kDbgFlagged = 4 };
 __device__ __forceinline__ void dbg_count(const UnpackArgs& a, int slot) {
   if (a.stamps) atomicAdd(a.stamps + kStampSlots * (blockIdx.x & (kStampRows - 1)) + slot, 1ull);
 }
-__device__ __forceinline__ void dbg_add(const UnpackArgs& a, int slot, uint64_t v) {
-  if (a.stamps && lane_id() == 0)
-    atomicAdd(a.stamps + kStampSlots * (blockIdx.x & (kStampRows - 1)) + slot,
-              (unsigned long long)v);
-}
-
 __device__ __forceinline__ void flag_message(const UnpackArgs& a, uint64_t m) {
   if (atomicExch(a.fail_flag + m, 1u) == 0) {
     const uint32_t i = atomicAdd(a.fail_count, 1u);
@@ -608,33 +574,6 @@ __device__ __forceinline__ void stage_load(const UnpackArgs& a, uint64_t A, Stag
   }
 }
 
-// The same bytes into the index rows (kRow layout): dword stores (rows are 4-byte aligned),
-// and the lane holding the first 16 bytes of row r + 1 also writes their first 12 as row r's tail.
-__device__ __forceinline__ void stage_store_rows(const Staged& sg, uint8_t* d) {
-  const int l = lane_id();
-#pragma unroll
-  for (int k = 0; k < kStageVecs; k++) {
-    const int o = 16 * (64 * k + l);
-    if (o < kB + kPad) {
-      const int row = o >> 6, c = o & 63;
-      if (row < 64) {
-        uint32_t* q = (uint32_t*)(d + kRow * row + c);
-        q[0] = sg.v[k].x;
-        q[1] = sg.v[k].y;
-        q[2] = sg.v[k].z;
-        q[3] = sg.v[k].w;
-      }
-      if (c == 0 && row > 0) {
-        uint32_t* q = (uint32_t*)(d + kRow * (row - 1) + 64);
-        q[0] = sg.v[k].x;
-        q[1] = sg.v[k].y;
-        q[2] = sg.v[k].z;
-      }
-    }
-  }
-  lane_handoff();  // other lanes read these bytes next
-}
-
 __device__ __forceinline__ void stage_tile(const UnpackArgs& a, uint64_t A, uint8_t* d) {
   Staged sg;
   stage_load(a, A, sg);
@@ -724,346 +663,221 @@ __device__ __forceinline__ uint64_t make_dep(uint32_t tag) {
   return sel;
 }
 
-// 3. Index: one wave per tile, chain 0 + merge table (see the file comment).  Two waves per
-// workgroup: 10.5 KiB of LDS each, 15 workgroups (30 waves) per CU.
-#ifndef CPK_INDEX_WAVES
-#define CPK_INDEX_WAVES 2
-#endif
-constexpr int kIndexWaves = CPK_INDEX_WAVES;
-template <bool STAMPS>
-__global__ __launch_bounds__(64 * kIndexWaves) void index_kernel(UnpackArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds_data[kIndexWaves][kRowBytes];
-  __shared__ uint64_t lds_ms[kIndexWaves][64];  // message starts, then chain-0 masks
-  const int l = lane_id();
-  const int wv = (int)uniform32(threadIdx.x >> 6);
-  const uint64_t t = (uint64_t)blockIdx.x * kIndexWaves + wv;
-  if (t >= a.ntiles) return;
-  Stamps<STAMPS> stm;
-  stm.start(a.stamps2);
-  uint64_t rt0 = 0;
-  if constexpr (STAMPS) rt0 = __builtin_amdgcn_s_memrealtime();
-  uint8_t* d = lds_data[wv];
-  uint64_t* lds_tm = lds_ms[wv];
-  const uint64_t P = a.nbytes;
-  const uint64_t A = t * kB;
+// ---------------------------------------------------------------------------------------------
+// 3. The tile kernel: one wave per 4 KiB packed tile, four waves per workgroup, tiles in
+//    workgroup order (a tile only ever waits on lower tiles, which are running or done).
+//
+// Tile descriptors (desc[t], zero until published).  A tile's exit is the first position of its
+// chain at or past the tile end; its words are those of its records (message starts excepted,
+// below).  States:
+//   AGG   the tile's exit and words for its optimistic entry -- the one the predecessor's chain 0
+//         leads to (x0p[t - 1], published as soon as the predecessor has settled chain 0);
+//   INCL  its true exit and the inclusive words of the message at the tile end.
+// The ok bit says the exit is the tile's chain-0 exit: then the next tile's optimistic entry is
+// its true one, provided this tile's own entry was.  A tile holding a message start publishes
+// INCL at once: its exit and the words after its last start do not depend on its entry.
+constexpr uint64_t kOkBit = 1ull << 61;
+constexpr int kExitShift = 48;                       // bits 48-60: exit - kB
+constexpr uint64_t kWordsMask = (1ull << kExitShift) - 1;
+constexpr uint32_t kExitDead = 0x1fff;               // the chain ran past the batch end
 
-  // this tile's and the next tile's first message (and where it starts), with the tile's bytes:
-  // a tile holding at most one message start (the batch end counts) needs no message window
-  const bool lastt = t + 1 >= a.ntiles;
-  const uint64_t mf0 = a.tile_first[t], mf1 = lastt ? a.nmsgs + 1 : a.tile_first[t + 1];
-  const uint64_t fp0 = a.tile_firstpos[t], fp1 = lastt ? ~0ull : a.tile_firstpos[t + 1];
-  Staged stg;
-  stage_load(a, A, stg);
-  const uint64_t mfirst = uniform64(mf0);
-  const uint64_t nstarts = uniform64(mf1) - mfirst;
-  stm.mark(0);
-  if constexpr (kRow == 64) stage_store(stg, d);
-  else stage_store_rows(stg, d);
-  stm.mark(1);
-  int nms_tile_after;
-  uint64_t msw;
-  if (nstarts <= 1) {
-    const uint64_t f0 = uniform64(fp0), f1 = uniform64(fp1);
-    const uint64_t after = nstarts ? f1 : f0;  // first start at or after the tile end
-    nms_tile_after = (int)((after < P ? after : P) - A);
-    msw = (nstarts && (f0 - A) >> 6 == (uint64_t)l) ? 1ull << ((f0 - A) & 63) : 0ull;
-  } else {
-    (void)tile_msg_starts(a, A, mfirst, lds_ms[wv], &nms_tile_after, nullptr);
-    msw = lds_ms[wv][l];
-  }
-  const SubTile st = make_subtile(A, P, msw, nms_tile_after);
-  stm.mark(2);
-
-  // ---- chain 0: speculative walks, then the lane fixed point for entry 0 --------------------
-  uint64_t chain = 0, runm = 0;
-  int sx = kDead;
-  if (!(a.debug_skip & 4) && st.s < st.pend) sx = walk(d, st, st.s, 0, &chain, &runm);
-  stm.mark(3);
-  int e = st.s;
-  uint64_t tm = 0;
-  int out = 0;
-  int siters = 0;
-  const bool settled =
-      (a.debug_skip & 4) ? true : settle(d, st, chain, sx, 0, e, tm, out, runm, &siters);
-  stm.mark(4);
-  if (a.stamps) {
-    const uint32_t nrec = __popcll(chain);
-    dbg_add(a, kDbgSettleIters, (uint64_t)siters);
-    if (siters > 8) dbg_add(a, kDbgSettle8, 1);
-    if (siters > 24) dbg_add(a, kDbgSettle24, 1);
-    dbg_add(a, kDbgWalkSteps, readlane32(wave_incl_sum32(nrec), 63));
-    dbg_add(a, kDbgWalkStepsMax, readlane32(wave_incl_max32(nrec), 63));
-  }
-  const uint32_t x0 = readlane32((uint32_t)out, 63);
-
-  // first message start (the batch end counts), tile-relative; kB if none
-  const uint64_t msl = ballot(st.msw != 0);
-  const int fl = lowest_bit(msl);
-  const int fms = msl ? 64 * fl + lowest_bit(readlane64(st.msw, fl)) : kB;
-
-  // ---- words of chain 0: per lane, before fms, after the lane's last message start ----------
-  const uint64_t pre_m = fms <= st.s ? 0ull : (fms >= st.s + 64 ? ~0ull : mask_lt(fms - st.s));
-  uint32_t w_all = __popcll(tm), w_pre = __popcll(tm & pre_m), w_post = 0;
-  const uint64_t msin = tm & st.msw;
-  const int lastms = highest_bit(msin);
-  const bool has_ms = lastms >= 0;
-  if (has_ms) w_post = __popcll(tm & ~mask_lt(lastms));
-  const uint64_t rruns = tm & runm;
-  {
-    uint64_t rr = rruns;
-    while (rr) {
-      const int b = lowest_bit(rr);
-      rr &= rr - 1;
-      const uint8_t* q = ix(d, st.s + b);
-      const uint32_t c = q[1 + __popc(q[0])];
-      w_all += c;
-      if ((pre_m >> b) & 1) w_pre += c;
-      if (has_ms && b >= lastms) w_post += c;
-    }
-  }
-  const uint32_t Wex = wave_incl_sum32(w_all) - w_all;
-  const uint32_t wpre0 = readlane32(wave_incl_sum32(w_pre), 63);
-  const uint64_t hm = ballot(has_ms);
-  const bool tile_has_start = hm != 0;
-  const int lm = highest_bit(hm);
-  const uint32_t contrib = (!tile_has_start || l > lm) ? w_all : (l == lm ? w_post : 0u);
-  const uint32_t wpost = readlane32(wave_incl_sum32(contrib), 63);
-  a.tm[t * 64 + l] = tm;
-  a.t_wex[t * 64 + l] = Wex;
-  lds_tm[l] = tm;
-  lane_handoff();
-  stm.mark(5);
-
-  // ---- merge table: lane e (1..15) walks the chain entered at byte e until it meets chain 0;
-  //      a chain that never does (parity-locked or raw-run data) is walked to the tile end
-  int m = 0, p = l;
-  uint32_t ww = 0;
-  bool merged = true;
-  int msteps = 0;
-  bool open = false;  // still walking after kMergeCap records
-  if (!(a.debug_skip & 8) && l >= 1 && l < kTabWalk) {
-    open = true;
-    for (int k = 0; k < kMergeCap; k++) {
-      msteps = k;
-      if (p >= fms) {
-        if (fms < kB) m = fms;           // every chain restarts at the first message start
-        else if (p == (int)x0) m = kB;   // left the tile at chain 0's exit
-        else merged = false;
-        open = false;
-        break;
-      }
-      // the four reads of a step are independent: one LDS round trip per record
-      const uint64_t mk = lds_tm[p >> 6];
-      const uint8_t* q = ix(d, p);
-      const uint32_t tag = q[0], c1 = q[1], c9 = q[9];
-      asm volatile("" ::"v"(tag), "v"(c1), "v"(c9));  // keep the reads ahead of the branch
-      if ((mk >> (p & 63)) & 1) {
-        m = p;
-        open = false;
-        break;
-      }
-      const uint32_t cnt = tag == 0 ? c1 : (tag == 0xff ? c9 : 0u);
-      ww += 1 + cnt;
-      p += rec_len(tag, cnt);
-    }
-  }
-  if (ballot(open)) {
-    // Rare: chains that run on beside chain 0 for hundreds of records (interleaved chains that
-    // meet late or never).  Walked record by record such a chain costs one LDS round trip per
-    // record across the tile, and that one wave set the kernel's tail.  Every lane now also
-    // walks a second chain B of its sub-tile -- from its first byte chain 0 does not start a
-    // record at, until it meets chain 0 -- and a walk that lands on B jumps straight to B's end
-    // (B's exit, or the chain-0 record where B meets it), adding B's records and run counts.
-    const uint64_t vm = st.vend <= st.s ? 0ull : (st.vend >= st.s + 64 ? ~0ull
-                                                                     : mask_lt(st.vend - st.s));
-    const uint64_t notA = ~tm & vm;
-    uint64_t chB = 0, rB = 0;
-    int xB = kDead;
-    if (notA) xB = walk(d, st, st.s + lowest_bit(notA), tm, &chB, &rB);
-    rB &= chB;
-    for (int k = kMergeCap; k < 2 * kB && ballot(open); k++) {
-      // every lane takes part in the shuffles (an inactive source lane would read as 0)
-      const int j = open ? (p >> 6 < 63 ? p >> 6 : 63) : l;
-      const uint64_t Bj = shfl64(chB, j), rBj = shfl64(rB, j);
-      const int xBj = (int)shfl32((uint32_t)xB, j);
-      if (open) {
-        msteps = k;
-        if (p >= fms) {
-          if (fms < kB) m = fms;
-          else if (p == (int)x0) m = kB;
-          else merged = false;
-          open = false;
-        } else {
-          const uint64_t mk = lds_tm[p >> 6];
-          const uint8_t* q = ix(d, p);
-          const uint32_t tag = q[0], c1 = q[1], c9 = q[9];
-          const int b = p & 63;
-          if ((mk >> b) & 1) {
-            m = p;
-            open = false;
-          } else if ((Bj >> b) & 1) {
-            const uint64_t on = ~mask_lt(b);
-            ww += __popcll(Bj & on);
-            uint64_t rr = rBj & on;
-            while (rr) {
-              const uint8_t* r = ix(d, 64 * j + lowest_bit(rr));
-              rr &= rr - 1;
-              ww += r[1 + __popc(r[0])];
-            }
-            p = xBj;  // kDead: B ran into the batch end (as chain 0 then did: x0 == kDead)
-          } else {
-            const uint32_t cnt = tag == 0 ? c1 : (tag == 0xff ? c9 : 0u);
-            ww += 1 + cnt;
-            p += rec_len(tag, cnt);
-          }
-        }
-      }
-    }
-  }
-  // chain-0 words before the merge point (all lanes take part in the shuffles)
-  const int L = (m >> 6) < 63 ? (m >> 6) : 63;
-  const uint64_t tmL = shfl64(tm, L);
-  const uint64_t rrL = shfl64(rruns, L);
-  const uint32_t WexL = shfl32(Wex, L);
-  int32_t delta = 0;
-  if (l >= 1 && l < kTab) {
-    if (!merged) {
-      delta = (int32_t)ww;  // words of the chain's records in the tile
-      a.t_xe[t * kTab + l] = (uint32_t)p;
-    } else {
-      uint32_t w0;
-      if (m >= kB) {
-        w0 = wpre0;  // no message start in the tile: wpre0 counts every record
-      } else {
-        const int b = m & 63;
-        w0 = WexL + __popcll(tmL & mask_lt(b));
-        uint64_t r2 = rrL & mask_lt(b);
-        while (r2) {
-          const int bb = lowest_bit(r2);
-          r2 &= r2 - 1;
-          const uint8_t* q = ix(d, 64 * (m >> 6) + bb);
-          w0 += q[1 + __popc(q[0])];
-        }
-      }
-      delta = (int32_t)(ww - w0);
-    }
-  }
-  stm.mark(6);
-  const uint32_t umask = (uint32_t)ballot(l >= 1 && l < kTab && !merged);
-  if (a.stamps) {
-    const uint32_t mx = readlane32(wave_incl_max32((uint32_t)msteps), 63);
-    dbg_add(a, kDbgMergeSteps, mx);
-    if (mx > 64) dbg_add(a, kDbgMerge64, 1);
-    if (mx > 256) dbg_add(a, kDbgMerge256, 1);
-    if (mx > 1024) dbg_add(a, kDbgMerge1k, 1);
-    if (umask) dbg_add(a, kDbgUmaskTiles, 1);
-  }
-  if (l < kTab) a.t_delta[t * kTab + l] = delta;
-  if (l == 0) {
-    a.t_x0[t] = x0;
-    a.t_fms[t] = (uint32_t)fms;
-    a.t_wpre[t] = wpre0;
-    a.t_wpost[t] = wpost;
-    a.t_umask[t] = umask;
-    a.t_flags[t] = (settled ? 0u : kTileUnsettled) | (tile_has_start ? kTileHasStart : 0u);
-  }
-  stm.mark(7);
-  if constexpr (STAMPS) {
-    stm.acc[13] = __builtin_amdgcn_s_memrealtime() - rt0;  // 100 MHz: calibrates the phases
-    stm.acc[14] = 1;
-    stm.acc[15] = 1;
-    stm.flush();
-  }
+__device__ __forceinline__ uint64_t make_desc(uint64_t state, uint32_t exit, uint32_t x0,
+                                              uint64_t words) {
+  const uint32_t e = exit >= (uint32_t)kDead ? kExitDead : exit - (uint32_t)kB;
+  return state | (exit == x0 ? kOkBit : 0ull) | ((uint64_t)e << kExitShift) | (words & kWordsMask);
+}
+__device__ __forceinline__ uint32_t desc_exit(uint64_t d) {
+  const uint32_t e = (uint32_t)(d >> kExitShift) & 0x1fffu;
+  return e == kExitDead ? (uint32_t)kDead : e + (uint32_t)kB;
 }
 
-// Walks the chain entered at tile-relative byte E of tile t through global memory until it meets
-// a chain-0 record start or the first message start (merged: the tile's exit is chain 0's), or
-// leaves the tile (its own exit).  *wpre = words of its records before the first message start.
-// False when the walk cap is hit.
-__device__ bool walk_global(const UnpackArgs& a, uint64_t t, uint32_t E, uint32_t fms,
-                            uint32_t x0, uint32_t wpre0, uint32_t* wpre, uint32_t* exit,
-                            bool* merged) {
-  const uint8_t* b = a.packed;
-  const uint64_t P = a.nbytes;
-  const uint64_t A = t * kB;
-  const uint64_t* tmt = a.tm + t * 64;
-  auto byte_at = [&](uint64_t q) -> uint32_t { return q < P ? (uint32_t)b[q] : 0u; };
-  uint32_t p = E, w = 0;
-  *merged = true;
-  *exit = x0;
-  for (int k = 0; k < kWalkCap; k++) {
-    if (p >= fms) {
-      *wpre = w;
-      if (fms >= (uint32_t)kB && p != x0) {
-        *merged = false;
-        *exit = p;
-      }
-      return true;
-    }
-    const uint64_t tmw = tmt[p >> 6];
-    if ((tmw >> (p & 63)) & 1) {
-      // merged at p: chain-0 words before p = sub-tile prefix + records of sub-tile p>>6 below p
-      const uint32_t L = p >> 6, bb = p & 63;
-      uint32_t w0 = a.t_wex[t * 64 + L] + (uint32_t)__popcll(tmw & mask_lt((int)bb));
-      uint64_t r = tmw & mask_lt((int)bb);
-      while (r) {
-        const int j = lowest_bit(r);
-        r &= r - 1;
-        const uint64_t q = A + 64 * L + j;
-        const uint32_t tag = byte_at(q);
-        if (tag == 0) w0 += byte_at(q + 1);
-        else if (tag == 0xff) w0 += byte_at(q + 9);
-      }
-      *wpre = w + (wpre0 - w0);
-      return true;
-    }
-    const uint64_t q = A + p;
-    const uint32_t tag = byte_at(q);
-    const uint32_t cnt = tag == 0 ? byte_at(q + 1) : (tag == 0xff ? byte_at(q + 9) : 0u);
-    w += 1 + cnt;
-    p += (uint32_t)rec_len(tag, cnt);
-  }
-  return false;
-}
-
-// Tile t's entry given the exit of its predecessor (tile-relative to the predecessor).
-__device__ __forceinline__ uint32_t entry_from_exit(const UnpackArgs& a, uint64_t t, uint32_t xp) {
+// Entry of a tile from its predecessor's exit (predecessor-relative), clipped at the tile's first
+// message start (every chain restarts there).
+__device__ __forceinline__ uint32_t entry_from_exit(uint32_t xp, uint32_t fms) {
   const uint32_t E = xp >= (uint32_t)kDead ? (uint32_t)kB : xp - (uint32_t)kB;
-  const uint32_t fms = a.t_fms[t];
   return E < fms ? E : fms;
 }
 
-// Tile t entered at E: its exit, words before its first message start, and whether the entry's
-// chain merged into chain 0 (merge table for E < 16, a global walk beyond).  False: walk cap.
-__device__ bool classify(const UnpackArgs& a, uint64_t t, uint32_t E, uint32_t* exit,
-                         uint32_t* wpre, bool* merged) {
-  const uint32_t fms = a.t_fms[t], wpre0 = a.t_wpre[t], x0 = a.t_x0[t];
-  *merged = true;
-  *exit = x0;
-  if (E == 0) {
-    *wpre = wpre0;
-    return true;
+// Words of the records in mask m of the sub-tile at s (a run record adds its count).
+__device__ __forceinline__ uint32_t mask_words(const uint8_t* d, int s, uint64_t m, uint64_t runs) {
+  uint32_t w = __popcll(m);
+  uint64_t r = m & runs;
+  while (r) {
+    const int b = lowest_bit(r);
+    r &= r - 1;
+    const uint8_t* q = d + s + b;
+    w += q[1 + __popc(q[0])];
   }
-  if (E >= fms) {
-    *wpre = 0;
-    return true;
-  }
-  if (E < (uint32_t)kTabWalk) {
-    const int32_t dl = a.t_delta[t * kTab + E];
-    if ((a.t_umask[t] >> E) & 1) {
-      *merged = false;
-      *exit = a.t_xe[t * kTab + E];
-      *wpre = (uint32_t)dl;
-      dbg_count(a, kDbgTableMiss);
-    } else {
-      *wpre = wpre0 + (uint32_t)dl;
+  return w;
+}
+
+// The chain entered at tile byte E (0 < E < fms) replaces chain 0's record starts before the
+// point where it meets chain 0.  Lane 0 walks it record by record (one LDS round trip per
+// record) for up to kMergeCap records; a chain still running beside chain 0 then (interleaved
+// chains that meet late, or never) is continued by all lanes in step, jumping along each
+// sub-tile's second chain B (from its first byte chain 0 does not start a record at).  Returns
+// the lane's true record-start mask; *exit is chain 0's exit when the chains meet (or the walk
+// reaches the first message start, where every chain restarts), else where the entry's chain
+// leaves the tile.  *runs gains the run records of the walked starts.
+__device__ uint64_t enter_chain(const uint8_t* d, uint64_t* aux, const SubTile& st, uint64_t tm0,
+                                int E, int fms, uint32_t x0, uint32_t* exit, uint64_t* runs) {
+  const int l = lane_id();
+  uint64_t* const fix = aux + 64;
+  aux[l] = tm0;
+  fix[l] = 0;
+  lane_handoff();
+  int p = E, cur = E >> 6, steps = 0;
+  uint64_t fm = 0;
+  bool done = true;
+  if (l == 0) {
+    // the reads of a step are independent (one LDS round trip per record); the walked starts of
+    // a sub-tile collect in a register until the walk leaves it
+    while (p < fms && p < kB && steps < kMergeCap) {
+      const uint64_t mk = aux[p >> 6];
+      const uint32_t tg = d[p], c9 = d[p + 9];
+      asm volatile("" ::"v"(tg), "v"(c9));
+      if ((mk >> (p & 63)) & 1) break;
+      if ((p >> 6) != cur) {
+        fix[cur] = fm;
+        fm = 0;
+        cur = p >> 6;
+      }
+      fm |= 1ull << (p & 63);
+      p += rec_len(tg, c9);
+      steps++;
     }
-    return true;
+    done = steps < kMergeCap;
   }
-  dbg_count(a, kDbgWalks);
-  const bool ok = walk_global(a, t, E, fms, x0, wpre0, wpre, exit, merged);
-  if (!ok) dbg_count(a, kDbgWalkFail);
-  return ok;
+  if (!readlane32(done, 0)) {
+    p = (int)readlane32((uint32_t)p, 0);
+    cur = (int)readlane32((uint32_t)cur, 0);
+    fm = readlane64(fm, 0);
+    const uint64_t vm = st.vend <= st.s ? 0ull : (st.vend >= st.s + 64 ? ~0ull
+                                                                     : mask_lt(st.vend - st.s));
+    const uint64_t notA = ~tm0 & vm;
+    uint64_t chB = 0;
+    int xB = kDead;
+    // (B's records are clipped at the first message start after the tile, as chain 0's are)
+    if (notA) xB = walk(d, st, st.s + lowest_bit(notA), tm0, &chB);
+    for (int k = 0; k < 2 * kB && p < fms && p < kB; k++) {
+      const int j = p >> 6, b = p & 63;
+      if ((readlane64(tm0, j) >> b) & 1) break;
+      if (j != cur) {
+        if (l == 0) fix[cur] = fm;
+        fm = 0;
+        cur = j;
+      }
+      const uint64_t Bj = readlane64(chB, j);
+      if ((Bj >> b) & 1) {
+        fm |= Bj & ~mask_lt(b);
+        p = (int)readlane32((uint32_t)xB, j);
+      } else {
+        fm |= 1ull << b;
+        p += rec_len(d[p], d[p + 9]);
+      }
+    }
+  }
+  if (l == 0) fix[cur] = fm;
+  p = (int)readlane32((uint32_t)p, 0);
+  lane_handoff();
+  const int m = p < fms ? p : fms;  // chain 0 holds from here on
+  const int s = 64 * l;
+  const uint64_t below = m <= s ? 0ull : (m >= s + 64 ? ~0ull : mask_lt(m - s));
+  const uint64_t fl = fix[l];
+  lane_handoff();
+  // run records among the walked starts
+  uint64_t fr = fl & ~*runs, rr = 0;
+  while (fr) {
+    const int b = lowest_bit(fr);
+    fr &= fr - 1;
+    const uint32_t tg = d[s + b];
+    if (tg == 0 || tg == 0xff) rr |= 1ull << b;
+  }
+  *runs |= rr;
+  if (p < fms && p < kB) {
+    *exit = x0;  // met chain 0
+  } else if (fms < kB) {
+    *exit = x0;  // restarted at the first message start
+  } else {
+    // left the tile on its own; its last record clipped at the next message start (as walk())
+    const int q = p < st.nms_after ? p : st.nms_after;
+    *exit = q >= st.pend ? (uint32_t)kDead : (uint32_t)q;
+  }
+  return (tm0 & ~below) | fl;
+}
+
+// Entry at or past the first message start: no record before it (the predecessor's last record
+// reaches past it), chain 0 from there on; an entry past the tile (the predecessor's chain ran
+// past the batch end) leaves no record at all.
+__device__ __forceinline__ uint64_t clip_below(uint64_t tm0, uint32_t fms, int s, uint32_t* exit) {
+  if (fms >= (uint32_t)kB) *exit = (uint32_t)kDead;
+  const uint64_t below = fms <= (uint32_t)s ? 0ull
+                                            : (fms >= (uint32_t)s + 64 ? ~0ull : mask_lt(fms - s));
+  return tm0 & ~below;
+}
+
+// Exclusive prefix of tile t -- words of the message at the tile start before this tile -- and
+// (*xprev) the true exit of tile t - 1, from the descriptors of tiles t - 1, t - 2, ...: up to the
+// nearest INCL, every AGG on the way must be right.  Tile j's AGG is right when tile j - 1's
+// exit (as published, and itself right) has the ok bit; the farthest tile without it makes every
+// nearer one wrong, so the wave then waits for the tile right after it to publish INCL (it
+// resolves its own entry the same way) and starts over.  Waits are only ever for lower tiles.
+__device__ uint64_t lookback_tiles(const UnpackArgs& a, uint64_t t, uint32_t* xprev) {
+  const int l = lane_id();
+  int64_t base = (int64_t)t - 1;  // nearest tile of the window
+  uint64_t acc = 0;
+  uint32_t xfirst = (uint32_t)kB;
+  uint32_t spins = 0;
+  for (;;) {
+    const int64_t idx = base - l;
+    // before tile 0: an inclusive zero whose exit enters tile 0 at byte 0
+    const uint64_t dv = idx >= 0 ? load_agent(a.desc + idx) : (kDescIncl | kOkBit);
+    const uint64_t stt = dv & kDescFlags;
+    const uint64_t sb = ballot(stt == kDescIncl);
+    const int k = sb ? lowest_bit(sb) : 64;
+    const uint64_t nb = ballot(stt == 0);
+    const int nl = nb ? lowest_bit(nb) : 64;
+    const uint64_t* wait_on = nullptr;
+    bool want_incl = false;
+    if (nl < k) {
+      wait_on = a.desc + (base - nl);
+    } else {
+      const int kk = k < 64 ? k : 63;
+      const bool first = base == (int64_t)t - 1;
+      const uint64_t fb = ballot(l <= kk && (l >= 1 || !first) && !(dv & kOkBit));
+      if (fb) {
+        wait_on = a.desc + (base - highest_bit(fb) + 1);
+        want_incl = true;
+      } else {
+        if (first) xfirst = desc_exit(readlane64(dv, 0));
+        acc += wave_sum64(l <= kk ? (dv & kWordsMask) : 0ull);
+        if (k < 64) break;
+        base -= 64;
+        continue;
+      }
+    }
+    // one lane polls the blocking descriptor (sleeping between polls), then the window is read
+    // again from the nearest tile
+    if (l == 0) {
+      for (;;) {
+        const uint64_t f = load_agent(wait_on) & kDescFlags;
+        if (want_incl ? f == kDescIncl : f != 0) break;
+        if (++spins >= kSpinLimit) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    spins = uniform32(spins);
+    if (spins >= kSpinLimit) {
+      raise_error(a.err, kErrInternal);
+      break;
+    }
+    if (want_incl) {
+      base = (int64_t)t - 1;
+      acc = 0;
+    }
+  }
+  *xprev = xfirst;
+  return acc;
 }
 
 __device__ __forceinline__ void flag_tile_messages(const UnpackArgs& a, uint64_t t) {
@@ -1073,281 +887,17 @@ __device__ __forceinline__ void flag_tile_messages(const UnpackArgs& a, uint64_t
   for (uint64_t m = mf; m < a.nmsgs && a.in_off[m] < A + kB; m++) flag_message(a, m);
 }
 
-// 4a. Resolve, optimistic pass: one thread per tile.  Entry = the predecessor's chain-0 exit
-// (right whenever the predecessor's own entry merged, or it holds a message start).  Records
-// the tile's exit and words under that entry and, per 64 tiles, bitmaps of the tiles whose entry
-// chain did not merge and of the tiles holding a message start.
-__global__ __launch_bounds__(256) void resolve1_kernel(UnpackArgs a) {
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool valid = t < a.ntiles;
-  bool merged = true, has_start = false;
-  if (valid) {
-    const uint32_t flags = a.t_flags[t];
-    has_start = flags & kTileHasStart;
-    const uint32_t E = t == 0 ? 0u : entry_from_exit(a, t, a.t_x0[t - 1]);
-    uint32_t x = 0, w = 0;
-    if (!classify(a, t, E, &x, &w, &merged)) {
-      flag_tile_messages(a, t);
-      merged = true;
-    }
-    if (flags & kTileUnsettled) {
-      dbg_count(a, kDbgUnsettled);
-      flag_tile_messages(a, t);
-    }
-    a.r1_x[t] = x;
-    a.r1_w[t] = w;
-  }
-  const uint64_t nb = ballot(valid && !merged);
-  const uint64_t mb = ballot(valid && has_start);
-  if (lane_id() == 0 && valid) {
-    a.g_notok[t / kGroup] = nb;
-    a.g_start[t / kGroup] = mb;
-  }
-}
-
-// First not-merged tile in (lo, hi) (tile indices), or hi if none.
-__device__ __forceinline__ uint64_t next_notok(const UnpackArgs& a, uint64_t lo, uint64_t hi) {
-  uint64_t j = lo + 1;
-  while (j < hi) {
-    const uint64_t G = j / kGroup;
-    uint64_t nb = a.g_notok[G] & ~mask_lt((int)(j % kGroup));
-    if (nb) {
-      const uint64_t k = G * kGroup + lowest_bit(nb);
-      return k < hi ? k : hi;
-    }
-    j = (G + 1) * kGroup;
-  }
-  return hi;
-}
-
-// 4b. Resolve, exact pass: one thread per tile.  An optimistic entry is wrong only after a tile
-// whose own entry did not merge, with no message start in between.  Such a stretch is replayed
-// from its first tile (whose entry is right): entries follow the replayed exits until they agree
-// with the optimistic ones again.  Then segmented tile values + 64-tile group aggregates for the
-// word offsets (expand_kernel's look-back).
-__global__ __launch_bounds__(256) void resolve2_kernel(UnpackArgs a) {
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int l = lane_id();
-  const bool valid = t < a.ntiles;
-  uint64_t v = 0;
-  if (valid) {
-    const uint32_t flags = a.t_flags[t];
-    uint32_t E = t == 0 ? 0u : entry_from_exit(a, t, a.t_x0[t - 1]);
-    uint32_t wpre = a.r1_w[t];
-    // the last tile s < t holding a message start, and the first non-merged tile in (s, t)
-    uint64_t k0 = t;
-    if (t > 0) {
-      int64_t G = (int64_t)(t / kGroup);
-      uint64_t lim = mask_lt((int)(t % kGroup));
-      for (int guard = 0; G >= 0 && guard < (1 << 14); guard++, G--) {
-        const uint64_t mb = a.g_start[G] & lim;
-        uint64_t nb = a.g_notok[G] & lim;
-        if (mb) {
-          const int s = highest_bit(mb);
-          nb &= ~mask_le(s);
-          if (nb) k0 = (uint64_t)G * kGroup + lowest_bit(nb);
-          break;
-        }
-        if (nb) k0 = (uint64_t)G * kGroup + lowest_bit(nb);
-        lim = ~0ull;
-      }
-    }
-    bool ok = true;
-    if (k0 < t) {
-      // replay from k0: its entry is right, its exit is the non-merged chain's
-      uint32_t X = a.r1_x[k0];
-      uint64_t j = k0 + 1;
-      int steps = 0;
-      while (j <= t && ok) {
-        const uint32_t Ej = entry_from_exit(a, j, X);
-        const uint32_t Eopt = entry_from_exit(a, j, a.t_x0[j - 1]);
-        if (Ej == Eopt) {
-          // back on the optimistic path: right until the next non-merged tile
-          const uint64_t k = next_notok(a, j - 1, t);
-          if (k >= t) {
-            break;  // E (optimistic) and wpre (pass 1) are this tile's
-          }
-          X = a.r1_x[k];
-          j = k + 1;
-          continue;
-        }
-        bool mg;
-        uint32_t w;
-        if (++steps > 4096 || !classify(a, j, Ej, &X, &w, &mg)) {
-          ok = false;
-          break;
-        }
-        if (j == t) {
-          E = Ej;
-          wpre = w;
-        }
-        j++;
-      }
-      if (!ok) flag_tile_messages(a, t);
-    }
-    a.t_ent[t] = E;
-    v = (flags & kTileHasStart) ? (kSegBit | a.t_wpost[t]) : (uint64_t)wpre;
-    a.desc[t] = kDescAgg | v;
-  }
-  // group aggregate (tiles 64g .. 64g+63 in lane order): words after the last restart
-  const uint64_t segm = ballot(valid && (v & kSegBit));
-  const int ls = highest_bit(segm);
-  const uint64_t c = (valid && l >= ls) ? (v & ~kSegBit) : 0;
-  const uint64_t sum = wave_sum64(c);
-  if (l == 0 && valid) a.gdesc[t / kGroup] = kDescAgg | (segm ? kSegBit : 0) | sum;
-}
-
-// Tile inputs that depend only on the tile index: prefetched one tile ahead by expand_kernel.
-struct ExpandFetch {
-  Staged stg;
-  uint64_t tm;        // chain-0 record-start mask of the lane's sub-tile
-  uint64_t d1, d2;    // look-back values: in-group predecessors, groups before
-  uint64_t mfirst;
-  uint32_t E, fms;
-};
-
-__device__ __forceinline__ void expand_fetch(const UnpackArgs& a, uint64_t t, ExpandFetch& f) {
-  const int l = lane_id();
-  stage_load(a, t * kB, f.stg);
-  f.mfirst = uniform64(a.tile_first[t]);
-  f.tm = a.tm[t * 64 + l];
-  f.E = uniform32(a.t_ent[t]);
-  f.fms = uniform32(a.t_fms[t]);
-  const uint64_t g = t / kGroup;
-  const int j = (int)(t - g * kGroup);
-  // both look-back loads unconditional (clamped addresses): under a branch, the first one got
-  // its wait before the second was issued -- two round trips instead of one
-  const int64_t G = (int64_t)g - 1;
-  const bool u1 = l < j, u2 = G - l >= 0;
-  const uint64_t r1 = a.desc[u1 ? t - 1 - (uint64_t)l : t];
-  const uint64_t r2 = a.gdesc[u2 ? (uint64_t)(G - l) : 0];
-  f.d1 = u1 ? (r1 & kDescValue) : 0;
-  f.d2 = u2 ? (r2 & kDescValue) : 0;
-}
-
-// Exclusive (segmented) word prefix of tile t from the final tile / group values of
-// resolve2_kernel (prefetched by expand_fetch: the in-group predecessors and up to 64 groups
-// before); farther groups are loaded only when none of those holds a message start.
-__device__ __forceinline__ uint64_t lookback_final(const UnpackArgs& a, uint64_t t,
-                                                   uint64_t d1, uint64_t d2) {
-  const int l = lane_id();
-  const uint64_t g = t / kGroup;
-  const int j = (int)(t - g * kGroup);
-  int64_t G = (int64_t)g - 1;
-  uint64_t excl = 0;
-  if (j > 0) {
-    excl = reduce_nearest(d1, j - 1, kSegBit);
-    if (excl & kSegBit) return excl & ~kSegBit;
-  }
-  while (G >= 0) {
-    const uint64_t sb = ballot(G - l >= 0 && (d2 & kSegBit));
-    const int k = sb ? lowest_bit(sb) : 63;
-    excl = seg_combine(reduce_nearest(d2, k, kSegBit), excl, kSegBit);
-    if (sb) break;
-    G -= 64;
-    d2 = G - l >= 0 ? (a.gdesc[G - l] & kDescValue) : 0;
-  }
-  return excl & ~kSegBit;
-}
-
-// One tile of expand_kernel.
-__device__ __forceinline__ void expand_tile(const UnpackArgs& a, uint64_t t, const ExpandFetch& f,
-                                            uint8_t* d, uint64_t* aux,
-                                            const uint64_t* dep_tab, uint32_t lut) {
+// Expansion of a tile's records given its true record-start masks (lane = sub-tile) and excl,
+// the words of the tile's first message before the tile: one lane per record, 64 consecutive
+// records at a time, coalesced stores; zero and raw runs written by the wave.  Records that end
+// or break a message go through handle_record, the reference's checks in the reference's order.
+__device__ __forceinline__ void expand_records(const UnpackArgs& a, uint64_t A, const uint8_t* d,
+                                               uint64_t* aux, const uint64_t* dep_tab,
+                                               uint32_t lut, uint64_t tm, uint64_t excl,
+                                               MsgWin& win, uint64_t mfirst, uint64_t mlast,
+                                               uint64_t msw) {
   const int l = lane_id();
   uint16_t* list = (uint16_t*)aux;
-  const uint64_t A = t * kB;
-  lane_handoff();  // the previous tile's reads of the wave's LDS stay before this tile's writes
-  const uint64_t mfirst = f.mfirst;
-  uint64_t tm = f.tm;
-  const uint32_t E = f.E;
-  const uint32_t fms = f.fms;
-  // words of the message at the tile start before this tile (tile values are final)
-  const uint64_t excl = lookback_final(a, t, f.d1, f.d2);
-  stage_store(f.stg, d);
-  MsgWin win;
-  // message starts: built in aux, then kept in registers (lane = sub-tile), so that aux is free
-  // for the entry patch and the record lists
-  const uint64_t mlast = tile_msg_starts(a, A, mfirst, aux, nullptr, &win);
-  const uint64_t msw = aux[l];
-  lane_handoff();
-
-  // ---- chain 0 -> the true chain: starts before the merge point come from a walk from E ----
-  if (E > 0) {
-    const bool pre_ok = readlane32(win.ok, 0) != 0;  // message holding the tile's first byte
-    int m = (a.debug_skip & 128) ? 0 : (int)fms;  // (diagnostic 128: chain 0 as is)
-    aux[64 + l] = 0;
-    if (pre_ok && E < fms) {
-      aux[l] = tm;
-      lane_handoff();
-      uint64_t* fix = aux + 64;
-      int p = (int)E, cur = (int)E >> 6, steps = 0;
-      uint64_t fm = 0;
-      bool done = true;
-      if (l == 0 && !(a.debug_skip & 128)) {  // (diagnostic: 128 skips the patch walk)
-        // the reads of a step are independent (one LDS round trip per record); the walked
-        // starts of a sub-tile collect in a register until the walk leaves it
-        done = false;
-        while (p < (int)fms && p < kB && steps < kMergeCap) {
-          const uint64_t mk = aux[p >> 6];
-          const uint32_t tg = d[p], c9 = d[p + 9];
-          asm volatile("" ::"v"(tg), "v"(c9));
-          if ((mk >> (p & 63)) & 1) break;
-          if ((p >> 6) != cur) {
-            fix[cur] = fm;
-            fm = 0;
-            cur = p >> 6;
-          }
-          fm |= 1ull << (p & 63);
-          p += rec_len(tg, c9);
-          steps++;
-        }
-        done = steps < kMergeCap;
-      }
-      if (!readlane32(done, 0)) {
-        // rare: the entry's chain runs on beside chain 0 (as in index_kernel's merge table):
-        // continue by jumping along each sub-tile's second chain B, all lanes in step with
-        // lane 0's walk (its position is uniform, so the lookups are readlanes)
-        p = (int)readlane32((uint32_t)p, 0);
-        cur = (int)readlane32((uint32_t)cur, 0);
-        fm = readlane64(fm, 0);
-        const SubTile st = make_subtile(A, a.nbytes, msw, kB + kPad);
-        const uint64_t vm = st.vend <= st.s ? 0ull : (st.vend >= st.s + 64 ? ~0ull
-                                                                         : mask_lt(st.vend - st.s));
-        const uint64_t notA = ~tm & vm;
-        uint64_t chB = 0;
-        int xB = kDead;
-        if (notA) xB = walk(d, st, st.s + lowest_bit(notA), tm, &chB);
-        for (int k = 0; k < 2 * kB && p < (int)fms && p < kB; k++) {
-          const int j = p >> 6, b = p & 63;
-          if ((readlane64(tm, j) >> b) & 1) break;
-          if (j != cur) {
-            if (l == 0) fix[cur] = fm;
-            fm = 0;
-            cur = j;
-          }
-          const uint64_t Bj = readlane64(chB, j);
-          if ((Bj >> b) & 1) {
-            fm |= Bj & ~mask_lt(b);
-            p = (int)readlane32((uint32_t)xB, j);
-          } else {
-            fm |= 1ull << b;
-            p += rec_len(d[p], d[p + 9]);
-          }
-        }
-      }
-      if (l == 0 && !(a.debug_skip & 128)) {
-        fix[cur] = fm;
-        m = p < (int)fms ? p : (int)fms;
-      }
-      m = (int)readlane32((uint32_t)m, 0);
-      lane_handoff();
-    }
-    const int s = 64 * l;
-    const uint64_t below = m <= s ? 0ull : (m >= s + 64 ? ~0ull : mask_lt(m - s));
-    tm = (tm & ~below) | aux[64 + l];
-  }
-
   // Fast expansion when every message touching the tile is in the window, has a valid header,
   // is not left to the fallback, fits the output, and no two messages start at the same byte.
   bool fast = a.mode == 0 && mlast - (mfirst - 1) <= 63 && a.word_off;
@@ -1617,14 +1167,10 @@ __device__ __forceinline__ void expand_tile(const UnpackArgs& a, uint64_t t, con
   }
 }
 
-
-// 5. Expand: one wave per tile (a persistent form with the next tile's inputs prefetched ran
-// slower: the prefetch registers cost occupancy and spills).
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) void expand_kernel(
-    UnpackArgs a) {
+__global__ __launch_bounds__(256) void unpack_tiles_kernel(UnpackArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds_data[4][kB + kPad];
-  // per wave 1 KiB: message starts while they are found, chain-0 masks + walked starts while
-  // the entry is patched, then the record list of a quarter tile (<= 512 records of >= 2 bytes)
+  // per wave 1 KiB: message starts while they are found, then chain 0 and the walked starts
+  // while the entry's chain is traced, then the record list of a quarter tile
   __shared__ uint64_t lds_aux[4][kB / 32];
   __shared__ uint64_t dep_tab[256];
   const int l = lane_id();
@@ -1633,10 +1179,104 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) voi
   __syncthreads();
   const uint64_t t = (uint64_t)blockIdx.x * 4 + wv;
   if (t >= a.ntiles) return;
-  ExpandFetch f;
-  expand_fetch(a, t, f);
-  expand_tile(a, t, f, lds_data[wv], lds_aux[wv], dep_tab,
-              deposit_sel((uint32_t)l & 15));
+  uint8_t* const d = lds_data[wv];
+  uint64_t* const aux = lds_aux[wv];
+  const uint64_t P = a.nbytes;
+  const uint64_t A = t * kB;
+  Staged stg;
+  stage_load(a, A, stg);
+  const uint64_t mfirst = uniform64(a.tile_first[t]);
+  stage_store(stg, d);
+  MsgWin win;
+  int nms_tile_after;
+  const uint64_t mlast = tile_msg_starts(a, A, mfirst, aux, &nms_tile_after, &win);
+  const uint64_t msw = aux[l];
+  lane_handoff();
+  const SubTile st = make_subtile(A, P, msw, nms_tile_after);
+
+  // ---- chain 0 (entered at the tile's first byte): speculative walks, then the lane fixed point
+  uint64_t chain = 0, runm = 0;
+  int sx = kDead;
+  if (st.s < st.pend) sx = walk(d, st, st.s, 0, &chain, &runm);
+  int e = st.s;
+  uint64_t tm0 = 0;
+  int out = 0;
+  const bool settled = settle(d, st, chain, sx, 0, e, tm0, out, runm);
+  const uint32_t x0 = readlane32((uint32_t)out, 63);
+  if (l == 0) store_agent32(a.x0p + t, 0x80000000u | x0);
+  if (!settled) {
+    // rare (fixed point at its iteration cap): the messages touching the tile go to the serial
+    // fallback decoder, and this tile writes none of their words
+    if (l == 0) flag_tile_messages(a, t);
+    win.ok = 0;
+  }
+
+  // first message start (the batch end counts), tile-relative; kB if none
+  const uint64_t msl = ballot(st.msw != 0);
+  const int fl = lowest_bit(msl);
+  const uint32_t fms = msl ? (uint32_t)(64 * fl + lowest_bit(readlane64(st.msw, fl))) : (uint32_t)kB;
+  // a message starting in the tile: exit and words after the last start are entry-independent
+  const uint64_t msin = tm0 & st.msw;
+  const int lastms = highest_bit(msin);
+  const uint64_t hm = ballot(lastms >= 0);
+  const bool has_start = hm != 0;
+  if (has_start) {
+    const int lm = highest_bit(hm);
+    const uint64_t from = l > lm ? ~0ull : (l == lm ? ~mask_lt(lastms) : 0ull);
+    const uint32_t wl = mask_words(d, st.s, tm0 & from, runm);
+    const uint64_t wpost = readlane32(wave_incl_sum32(wl), 63);
+    if (l == 0) store_agent(a.desc + t, make_desc(kDescIncl, x0, x0, wpost));
+  }
+
+  // ---- the tile's entry and the words before it ------------------------------------------
+  uint64_t tm = tm0, excl = 0;
+  if (t == 0 || fms == 0) {
+    if (!has_start) {  // (tile 0 without a message start: bytes before the first message)
+      const uint64_t w = readlane32(wave_incl_sum32(mask_words(d, st.s, tm0, runm)), 63);
+      if (l == 0) store_agent(a.desc + t, make_desc(kDescIncl, x0, x0, w));
+    }
+  } else {
+    // optimistic entry: where the predecessor's chain 0 leads
+    const uint32_t xp = wait_nonzero32(a.x0p + t - 1, a.err) & 0x7fffffffu;
+    const uint32_t Eopt = entry_from_exit(xp, fms);
+    uint32_t xE = x0;
+    uint64_t runs = runm;
+    if (Eopt > 0 && Eopt < fms)
+      tm = enter_chain(d, aux, st, tm0, (int)Eopt, (int)fms, x0, &xE, &runs);
+    else if (Eopt >= fms)
+      tm = clip_below(tm0, fms, st.s, &xE);
+    uint64_t w = 0;
+    if (!has_start) {
+      w = readlane32(wave_incl_sum32(mask_words(d, st.s, tm, runs)), 63);
+      if (l == 0) store_agent(a.desc + t, make_desc(kDescAgg, xE, x0, w));
+    }
+    uint32_t xprev = 0;
+    excl = lookback_tiles(a, t, &xprev);
+    const uint32_t E = entry_from_exit(xprev, fms);
+    if (E != Eopt) {
+      // the predecessor's chain did not lead where its chain 0 does
+      runs = runm;
+      xE = x0;
+      if (E > 0 && E < fms)
+        tm = enter_chain(d, aux, st, tm0, (int)E, (int)fms, x0, &xE, &runs);
+      else if (E >= fms)
+        tm = clip_below(tm0, fms, st.s, &xE);
+      else
+        tm = tm0;
+      if (!has_start) w = readlane32(wave_incl_sum32(mask_words(d, st.s, tm, runs)), 63);
+    }
+    if (!has_start && l == 0) store_agent(a.desc + t, make_desc(kDescIncl, xE, x0, excl + w));
+    if (a.stamps && l == 0 && t < 1024) {  // diagnostic dump (CPK_STAMPS=1)
+      a.stamps[4 * t] = E | ((uint64_t)Eopt << 32);
+      a.stamps[4 * t + 1] = xE | ((uint64_t)x0 << 32);
+      a.stamps[4 * t + 2] = excl;
+      a.stamps[4 * t + 3] = w | ((uint64_t)fms << 32) | ((uint64_t)has_start << 63);
+    }
+  }
+
+  // ---- expansion -------------------------------------------------------------------------
+  expand_records(a, A, d, aux, dep_tab, deposit_sel((uint32_t)l & 15), tm, excl, win, mfirst,
+                 mlast, msw);
 }
 
 // 6. Serial re-decode of flagged messages: one wave per message; lane 0 walks the records of a
@@ -1763,31 +1403,13 @@ hipError_t launch_unpack_header(const uint8_t* packed, const uint64_t* in_off, u
 
 hipError_t launch_unpack_stage(int stage, const UnpackArgs& a, hipStream_t stream) {
   if (a.ntiles == 0) return hipSuccess;
-  const unsigned wave_blocks = (unsigned)((a.ntiles + 3) / 4);
-  const unsigned index_blocks = (unsigned)((a.ntiles + kIndexWaves - 1) / kIndexWaves);
-  switch (stage) {
-    case kUnpackIndex:
-      if (a.stamps2)
-        hipLaunchKernelGGL(index_kernel<true>, dim3(index_blocks), dim3(64 * kIndexWaves), 0,
-                           stream, a);
-      else
-        hipLaunchKernelGGL(index_kernel<false>, dim3(index_blocks), dim3(64 * kIndexWaves), 0,
-                           stream, a);
-      break;
-    case kUnpackResolve:
-      hipLaunchKernelGGL(resolve1_kernel, dim3((unsigned)((a.ntiles + 255) / 256)), dim3(256), 0,
-                         stream, a);
-      hipLaunchKernelGGL(resolve2_kernel, dim3((unsigned)((a.ntiles + 255) / 256)), dim3(256), 0,
-                         stream, a);
-      break;
-    case kUnpackExpand:
-      hipLaunchKernelGGL(expand_kernel, dim3(wave_blocks), dim3(256), 0, stream, a);
-      break;
-    default:
-      // a small grid: it only loops over the (rare) flagged messages, and an empty launch of
-      // thousands of workgroups costs microseconds
-      hipLaunchKernelGGL(fallback_kernel, dim3(128), dim3(64), 0, stream, a);
-      break;
+  if (stage == kUnpackTiles) {
+    hipLaunchKernelGGL(unpack_tiles_kernel, dim3((unsigned)((a.ntiles + 3) / 4)), dim3(256), 0,
+                       stream, a);
+  } else {
+    // a small grid: it only loops over the (rare) flagged messages, and an empty launch of
+    // thousands of workgroups costs microseconds
+    hipLaunchKernelGGL(fallback_kernel, dim3(128), dim3(64), 0, stream, a);
   }
   return hipGetLastError();
 }
