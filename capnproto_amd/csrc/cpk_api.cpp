@@ -19,9 +19,10 @@ struct cpk_ctx {
   void* scratch = nullptr;       // device scratch (descriptors, bitmaps, tile tables)
   size_t scratch_size = 0;
   uint32_t* err = nullptr;       // device error word (first batch-level error)
-  // device staging for the *_host entry points
-  void* stage[4] = {nullptr, nullptr, nullptr, nullptr};
-  size_t stage_size[4] = {0, 0, 0, 0};
+  // device staging: [0..2] the *_host entry points, [3] cpk_pack_segments (segment list, flat
+  // message, chunk offsets), [4] cpk_split_packed_stream (call state, record-head map)
+  void* stage[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+  size_t stage_size[5] = {0, 0, 0, 0, 0};
   // measurement hooks: [0] pack (tile, scan, placement), [1] unpack (tiles .. fallback),
   // [2 + stage] each unpack stage kernel (tiles, fallback)
   bool timing = false;
@@ -417,7 +418,7 @@ cpk_status cpk_destroy(cpk_ctx* ctx) {
       (void)hipEventDestroy(p.second);
     }
   for (hipEvent_t e : ctx->pool) (void)hipEventDestroy(e);
-  for (int i = 0; i < 4; i++)
+  for (int i = 0; i < 5; i++)
     if (ctx->stage[i]) (void)hipFree(ctx->stage[i]);
   if (ctx->pinned) (void)hipHostFree(ctx->pinned);
   if (ctx->meta_ev) (void)hipEventDestroy(ctx->meta_ev);
@@ -600,9 +601,9 @@ cpk_status cpk_split_packed_stream(cpk_ctx* ctx, const uint8_t* d_packed, uint64
   if (order_streams(ctx, s) != CPK_OK) return CPK_ERR_HIP;
   // the record-head map (one u64 per output word) and 8 words of call state: in_off[2],
   // word_off[2], meta[4] (stop byte, stop word, decode status)
-  cpk_status st = ensure(&ctx->stage[3], &ctx->stage_size[3], words_capacity * 8 + 128);
+  cpk_status st = ensure(&ctx->stage[4], &ctx->stage_size[4], words_capacity * 8 + 128);
   if (st != CPK_OK) return st;
-  uint64_t* state = (uint64_t*)ctx->stage[3];
+  uint64_t* state = (uint64_t*)ctx->stage[4];
   uint64_t* rec_pos = state + 8;
   uint64_t* meta = state + 4;
   hipError_t e = cpk::launch_set_u64x4(state, 0, nbytes, 0, words_capacity, s);

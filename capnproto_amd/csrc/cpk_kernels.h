@@ -75,7 +75,8 @@ struct UnpackArgs {
   uint32_t* fail_count;
   uint32_t* err;
   unsigned long long* stamps;   // diagnostic build only (env CPK_STAMPS), else NULL
-  uint32_t debug_skip;          // diagnostic (env CPK_DEBUG_SKIP): 16 no record batches, 32 no lists
+  uint32_t debug_skip;          // diagnostic (env CPK_DEBUG_SKIP): 4 no chain-0 walks, 8 no look-back,
+                                // 16 no record batches, 32 no lists
   const uint64_t* tile_firstpos;  // in_off[tile_first[t]]: the first message start >= tile start
 };
 

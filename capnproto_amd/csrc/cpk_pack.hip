@@ -16,12 +16,12 @@
 //             kind (all Z, or all F) maps b -> (b - 8) mod 256, so a sync-free wave of them maps b
 //             to itself (512 = 2 * 256).  Other sync-free stretches compose exactly in a scalar
 //             pass (rare: a >= 8-word stretch of words with one zero byte and no O word).
-//   tiles     ticket order (an atomic counter hands out tiles, so a tile only ever waits on
-//             tiles that running workgroups hold: no deadlock whatever else shares the GPU).  A
-//             tile's exit budget is published in state[] as soon as it is known -- right after
-//             the classes when the tile holds a sync point -- and the output offset comes from a
-//             two-level decoupled look-back over workgroup aggregates, done by wave 0 while waves
-//             1-3 emit their records into the LDS staging slot.
+//   tiles     one workgroup per tile in blockIdx order: a tile only ever waits for the exit budget
+//             of the tile before it (dispatched earlier, so running or done -- whatever else
+//             shares the GPU).  The exit budget is published in state[] as soon as it is known
+//             (right after the classes when the tile holds a sync point).  A tile's packed bytes
+//             go to its own scratch slot; a scan of the tile byte counts and a placement kernel
+//             move them to their final offsets (no look-back inside the tile kernel).
 //   count     the count byte of a run still open at the tile end depends on words of the next
 //             tile.  The tile writes it as if the batch ended there; when the next tile's first
 //             word is not a sync point (so the run may go on), the tile leaves that byte out of

@@ -1167,7 +1167,11 @@ __device__ __forceinline__ void expand_records(const UnpackArgs& a, uint64_t A, 
   }
 }
 
-__global__ __launch_bounds__(256) void unpack_tiles_kernel(UnpackArgs a) {
+#ifndef CPK_UNPACK_WPE
+#define CPK_UNPACK_WPE 7  // 72 VGPRs: 7 waves per SIMD (LDS allows 7); 6 at the unconstrained 80
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CPK_UNPACK_WPE))) void
+unpack_tiles_kernel(UnpackArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds_data[4][kB + kPad];
   // per wave 1 KiB: message starts while they are found, then chain 0 and the walked starts
   // while the entry's chain is traced, then the record list of a quarter tile
@@ -1197,11 +1201,12 @@ __global__ __launch_bounds__(256) void unpack_tiles_kernel(UnpackArgs a) {
   // ---- chain 0 (entered at the tile's first byte): speculative walks, then the lane fixed point
   uint64_t chain = 0, runm = 0;
   int sx = kDead;
-  if (st.s < st.pend) sx = walk(d, st, st.s, 0, &chain, &runm);
+  if (st.s < st.pend && !(a.debug_skip & 4)) sx = walk(d, st, st.s, 0, &chain, &runm);
   int e = st.s;
   uint64_t tm0 = 0;
-  int out = 0;
-  const bool settled = settle(d, st, chain, sx, 0, e, tm0, out, runm);
+  int out = st.end;
+  const bool settled =
+      (a.debug_skip & 4) ? true : settle(d, st, chain, sx, 0, e, tm0, out, runm);
   const uint32_t x0 = readlane32((uint32_t)out, 63);
   if (l == 0) store_agent32(a.x0p + t, 0x80000000u | x0);
   if (!settled) {
@@ -1250,8 +1255,8 @@ __global__ __launch_bounds__(256) void unpack_tiles_kernel(UnpackArgs a) {
       w = readlane32(wave_incl_sum32(mask_words(d, st.s, tm, runs)), 63);
       if (l == 0) store_agent(a.desc + t, make_desc(kDescAgg, xE, x0, w));
     }
-    uint32_t xprev = 0;
-    excl = lookback_tiles(a, t, &xprev);
+    uint32_t xprev = xp;
+    if (!(a.debug_skip & 8)) excl = lookback_tiles(a, t, &xprev);
     const uint32_t E = entry_from_exit(xprev, fms);
     if (E != Eopt) {
       // the predecessor's chain did not lead where its chain 0 does

@@ -224,3 +224,45 @@ def test_pack_segments_device_list(codec, oracle, profile):
     with pytest.raises(capnproto_amd.CpkError) as e:
         codec.pack_segments([])
     assert e.value.status == capnproto_amd.EMPTY_MESSAGE
+
+
+def test_concurrent_contexts_two_streams(codec):
+    """Two contexts pack and unpack full-size batches at the same time on two streams: the tile
+    kernels only wait on lower tiles of their own launch (dispatched earlier), so neither can
+    stall the other whatever else shares the GPU; statuses and bytes match a sequential run."""
+    import capnproto_amd
+    import torch
+
+    other = capnproto_amd.Codec(0)
+    try:
+        jobs = []
+        for seed, c in ((3, codec), (4, other)):
+            off, total = c.gen_offsets(8192, seed=seed)  # C5-like sizes, ~45 MiB
+            words = c.gen_messages("mixed", off, total, seed=seed)
+            ref, rmoff, rst = c.pack_messages(words, off)
+            c.sync()
+            jobs.append((c, off, total, words, ref, rmoff, rst))
+        streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+        outs = []
+        for (c, off, total, words, *_), s in zip(jobs, streams):
+            with torch.cuda.stream(s):
+                outs.append(c.pack_messages(words, off, stream=s))
+        for (c, *_), s, (packed, moff, st) in zip(jobs, streams, outs):
+            s.synchronize()
+            c.sync(s)
+        backs = []
+        for (c, off, total, words, *_), s, (packed, moff, st) in zip(jobs, streams, outs):
+            with torch.cuda.stream(s):
+                backs.append(c.unpack_messages(packed, moff, total, stream=s))
+        for s in streams:
+            s.synchronize()
+        for (c, off, total, words, ref, rmoff, rst), (packed, moff, st), (back, wo, ust) in zip(
+                jobs, outs, backs):
+            c.sync()
+            P = int(rmoff[-1].item())
+            assert int(moff[-1].item()) == P
+            assert (st == 0).all() and (ust == 0).all()
+            assert torch.equal(packed[:P], ref[:P]) and torch.equal(moff, rmoff)
+            assert torch.equal(back[:total], words[:total]) and torch.equal(wo, off)
+    finally:
+        other.close()

@@ -33,6 +33,6 @@ cat gpurun_out/${TAG}_stamps.log
 fi
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/${TAG}_prof" -o run \
-  -- python3 "$R/bench.py" --sub none --steps 20 --warmup 3 --no-cpu-baseline > "$R/gpurun_out/${TAG}_prof.log" 2>&1 \
+  -- python3 "$R/bench.py" --sub none --steps 20 --warmup 3 --no-cpu-baseline --no-host > "$R/gpurun_out/${TAG}_prof.log" 2>&1 \
   || { echo "rocprof failed"; tail -20 "$R/gpurun_out/${TAG}_prof.log"; exit 1; }
 echo "rocprof done"
