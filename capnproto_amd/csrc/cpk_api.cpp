@@ -294,7 +294,6 @@ cpk_status unpack_common(cpk_ctx* ctx, uint32_t mode, const uint8_t* d_packed, u
   cpk_status st = ensure(&ctx->scratch, &ctx->scratch_size, probe.total + 64);
   if (st != CPK_OK) return st;
   UnpackScratch s = carve_unpack(ctx->scratch, ntiles, n);
-  if (cpk::launch_fill(ctx->scratch, s.zero_bytes, 0, stream) != hipSuccess) return CPK_ERR_HIP;
   const uint64_t* word_off = d_word_off_in;
   hipError_t e = hipSuccess;
   cpk::TileFirstJob tf;  // each tile's first message, in the same launch as the headers
@@ -304,6 +303,8 @@ cpk_status unpack_common(cpk_ctx* ctx, uint32_t mode, const uint8_t* d_packed, u
   tf.T = B;
   tf.out = s.tile_first;
   tf.outpos = s.tile_firstpos;
+  tf.zero = (uint64_t*)ctx->scratch;  // zeroed in the header / init launch
+  tf.zero_words = s.zero_bytes / 8;
   if (mode == 0) {
     if (!d_word_off_out) return CPK_ERR_INVALID_ARGUMENT;
     if (n == 0) return hip_status(cpk::launch_fill(d_word_off_out, 8, 0, stream));

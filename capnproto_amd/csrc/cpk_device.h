@@ -192,8 +192,16 @@ __device__ __forceinline__ uint32_t wait_nonzero32(const uint32_t* p, uint32_t* 
 
 // Blocks past `first_block` of a prologue kernel compute tile_first (TileFirstJob, cpk_kernels.h):
 // binary search of each tile's start in the sorted positions.  True when this block did so.
+constexpr uint64_t kZeroBlockWords = 4096;  // u64 per zeroing block (256 threads x 16)
 __device__ __forceinline__ bool run_tile_first(const TileFirstJob& tf, uint32_t first_block) {
   if (blockIdx.x < first_block) return false;
+  const uint32_t tfb = (uint32_t)((tf.ntiles + 255) / 256);
+  if (blockIdx.x - first_block >= tfb) {
+    const uint64_t z0 = (uint64_t)(blockIdx.x - first_block - tfb) * kZeroBlockWords;
+    for (uint64_t i = z0 + threadIdx.x; i < z0 + kZeroBlockWords && i < tf.zero_words; i += 256)
+      tf.zero[i] = 0;
+    return true;
+  }
   const uint64_t t = (uint64_t)(blockIdx.x - first_block) * blockDim.x + threadIdx.x;
   if (t < tf.ntiles) {
     const uint64_t key = t * tf.T;
@@ -209,7 +217,8 @@ __device__ __forceinline__ bool run_tile_first(const TileFirstJob& tf, uint32_t 
   return true;
 }
 inline unsigned tile_first_blocks(const TileFirstJob& tf) {
-  return (unsigned)((tf.ntiles + 255) / 256);
+  return (unsigned)((tf.ntiles + 255) / 256 +
+                    (tf.zero ? (tf.zero_words + kZeroBlockWords - 1) / kZeroBlockWords : 0));
 }
 
 // Decoupled look-back (exclusive prefix of tile aggregates) for tile `t` by one wave.

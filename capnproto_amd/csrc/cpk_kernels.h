@@ -45,6 +45,10 @@ struct TileFirstJob {
   uint64_t npos, ntiles, T;
   uint64_t* out;
   uint64_t* outpos = nullptr;  // optional: pos[out[t]] (~0 past the end)
+  // optional: zero zero_words u64 at `zero` in further blocks of the same launch (scratch the
+  // kernels after the prologue expect zeroed: one launch fewer)
+  uint64_t* zero = nullptr;
+  uint64_t zero_words = 0;
 };
 hipError_t launch_message_bits(const uint64_t* words, const uint64_t* off, uint64_t n,
                                uint64_t* bits, int32_t* status, const TileFirstJob& tf,

@@ -152,10 +152,15 @@ __device__ __forceinline__ int next_start_after(const SubTile& st, int q) {
   return after ? q + 1 + lowest_bit(after) : st.nms_after;
 }
 
+// Length of the record whose tag is t and whose byte 9 past the tag is c9.  (An LDS table of
+// lengths by tag measured slower: one more dependent LDS round trip per walk step, and its reads
+// collide in banks.)
+__device__ __forceinline__ int step_len(uint32_t t, uint32_t c9) { return rec_len(t, c9); }
+
 // Walks from p (inside the sub-tile) marking record starts until the chain leaves the sub-tile
 // or reaches a position of `stop`.  Record ends are clipped at the next message start nm, which
 // only moves when the chain reaches it (rare), so the step itself carries no message logic.
-// Returns the position reached.
+// Returns the position reached.  (Sub-tiles are 64-byte aligned in the tile: bit p & 63.)
 __device__ __forceinline__ int walk(const uint8_t* d, const SubTile& st, int p, uint64_t stop,
                                     uint64_t* marks, uint64_t* runs = nullptr) {
   uint64_t m = 0, rm = 0;
@@ -163,14 +168,13 @@ __device__ __forceinline__ int walk(const uint8_t* d, const SubTile& st, int p, 
     // no message start in the tile: the only clip is the first start after the sub-tile, where
     // the walk ends anyway (most tiles of large messages)
     while (p < st.vend) {
-      const uint64_t bit = 1ull << (p - st.s);
+      const uint32_t e = d[p], c9 = d[p + 9];
+      const uint64_t bit = 1ull << (p & 63);
       m |= bit;
-      const uint8_t* q = ix(d, p);
-      const uint32_t tag = q[0];
-      if (tag == 0 || tag == 0xff) rm |= bit;
-      const int np = p + rec_len(tag, q[9]);
+      if (e == 0 || e == 0xff) rm |= bit;
+      const int np = p + step_len(e, c9);
       p = np < st.nms_after ? np : st.nms_after;
-      if (p < st.vend && ((stop >> (p - st.s)) & 1)) break;
+      if (p < st.vend && ((stop >> (p & 63)) & 1)) break;
     }
     *marks = m;
     if (runs) *runs = rm;
@@ -178,18 +182,17 @@ __device__ __forceinline__ int walk(const uint8_t* d, const SubTile& st, int p, 
   }
   int nm = next_start_after(st, p);
   while (p < st.vend) {
-    const uint64_t bit = 1ull << (p - st.s);
+    const uint32_t e = d[p], c9 = d[p + 9];
+    const uint64_t bit = 1ull << (p & 63);
     m |= bit;
-    const uint8_t* q = ix(d, p);
-    const uint32_t tag = q[0];
-    if (tag == 0 || tag == 0xff) rm |= bit;
-    int np = p + rec_len(tag, q[9]);
+    if (e == 0 || e == 0xff) rm |= bit;
+    int np = p + step_len(e, c9);
     if (np >= nm) {
       np = nm;
       nm = np < st.end ? next_start_after(st, np) : st.nms_after;
     }
     p = np;
-    if (p < st.vend && ((stop >> (p - st.s)) & 1)) break;
+    if (p < st.vend && ((stop >> (p & 63)) & 1)) break;
   }
   *marks = m;
   if (runs) *runs = rm;
@@ -734,8 +737,8 @@ __device__ uint64_t enter_chain(const uint8_t* d, uint64_t* aux, const SubTile& 
     // a sub-tile collect in a register until the walk leaves it
     while (p < fms && p < kB && steps < kMergeCap) {
       const uint64_t mk = aux[p >> 6];
-      const uint32_t tg = d[p], c9 = d[p + 9];
-      asm volatile("" ::"v"(tg), "v"(c9));
+      const uint32_t le = d[p], c9 = d[p + 9];
+      asm volatile("" ::"v"(le), "v"(c9));
       if ((mk >> (p & 63)) & 1) break;
       if ((p >> 6) != cur) {
         fix[cur] = fm;
@@ -743,7 +746,7 @@ __device__ uint64_t enter_chain(const uint8_t* d, uint64_t* aux, const SubTile& 
         cur = p >> 6;
       }
       fm |= 1ull << (p & 63);
-      p += rec_len(tg, c9);
+      p += step_len(le, c9);
       steps++;
     }
     done = steps < kMergeCap;
@@ -773,7 +776,7 @@ __device__ uint64_t enter_chain(const uint8_t* d, uint64_t* aux, const SubTile& 
         p = (int)readlane32((uint32_t)xB, j);
       } else {
         fm |= 1ull << b;
-        p += rec_len(d[p], d[p + 9]);
+        p += step_len(d[p], d[p + 9]);
       }
     }
   }
@@ -891,11 +894,12 @@ __device__ __forceinline__ void flag_tile_messages(const UnpackArgs& a, uint64_t
 // the words of the tile's first message before the tile: one lane per record, 64 consecutive
 // records at a time, coalesced stores; zero and raw runs written by the wave.  Records that end
 // or break a message go through handle_record, the reference's checks in the reference's order.
+template <bool PLAIN>
 __device__ __forceinline__ void expand_records(const UnpackArgs& a, uint64_t A, const uint8_t* d,
                                                uint64_t* aux, const uint64_t* dep_tab,
                                                uint32_t lut, uint64_t tm, uint64_t excl,
                                                MsgWin& win, uint64_t mfirst, uint64_t mlast,
-                                               uint64_t msw) {
+                                               uint64_t msw, uint64_t w_tile) {
   const int l = lane_id();
   uint16_t* list = (uint16_t*)aux;
   // Fast expansion when every message touching the tile is in the window, has a valid header,
@@ -1025,6 +1029,67 @@ __device__ __forceinline__ void expand_records(const UnpackArgs& a, uint64_t A, 
       sum += readlane32(inc, 63);
     }
     return;
+  }
+  // plain tiles (most tiles of large messages): no message start in the tile, and no record can
+  // reach the end of its message, by words or by bytes (a record reaches at most 2050 bytes past
+  // the tile) -- no per-record message logic at all
+  if constexpr (PLAIN) {
+  const uint64_t cbase0 = readlane64(win.base, 0), ctotal0 = readlane64(win.total, 0);
+  const uint64_t cend0 = readlane64(win.end, 0);
+  if (fast && !a.rec_pos && w_tile != ~0ull && ballot(msw != 0) == 0 && excl + w_tile < ctotal0 &&
+      cend0 > A + kB + 2064 && !(a.debug_skip & 32)) {
+    uint64_t* const wp0 = a.words + cbase0 + excl;
+    uint32_t sum = 0;  // words of the tile's records so far
+    for (int h = 0; h < 4; h++) {
+      const int src = 16 * h + (l >> 2);
+      const uint32_t sh = 16u * ((uint32_t)l & 3);
+      uint32_t bits = (uint32_t)(shfl64(tm, src) >> sh) & 0xffffu;
+      const uint32_t c = __popc(bits);
+      const uint32_t Rin = wave_incl_sum32(c);
+      const uint32_t nh = readlane32(Rin, 63);
+      uint32_t r = Rin - c;
+      const uint32_t pbase = 64u * (uint32_t)src + sh;
+      while (bits) {
+        const uint32_t b = (uint32_t)__builtin_ctz(bits);
+        bits &= bits - 1;
+        list[r++] = (uint16_t)(pbase + b);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      for (uint32_t b0 = 0; b0 < ((a.debug_skip & 16) ? 0u : nh); b0 += 64) {
+        const uint32_t rr = b0 + l;
+        const bool act = rr < nh;
+        const int p = (int)list[rr < nh ? rr : nh - 1];
+        const uint32_t* dw = (const uint32_t*)(d + (p & ~3));
+        const uint32_t sh2 = (uint32_t)p & 3;
+        const uint32_t q0 = dw[0], q1 = dw[1], q2 = dw[2], q3 = dw[3];
+        const uint32_t b0w = __builtin_amdgcn_alignbyte(q1, q0, sh2);  // bytes p .. p+3
+        const uint32_t b1w = __builtin_amdgcn_alignbyte(q2, q1, sh2);  // p+4 .. p+7
+        const uint32_t b2w = __builtin_amdgcn_alignbyte(q3, q2, sh2);  // p+8 .. p+11
+        const uint32_t tag = b0w & 0xff;
+        const uint32_t dlo = __builtin_amdgcn_alignbyte(b1w, b0w, 1);  // data bytes 0..3
+        const uint32_t dhi = __builtin_amdgcn_alignbyte(b2w, b1w, 1);  // data bytes 4..7
+        const bool z = tag == 0, f = tag == 0xff;
+        uint32_t cnt = z ? (b0w >> 8) & 0xff : 0u;
+        cnt = f ? (b2w >> 8) & 0xff : cnt;
+        const uint32_t w = act ? 1 + cnt : 0;
+        const uint32_t inc = wave_incl_sum32(w);
+        const uint32_t o = sum + inc - w;  // words of the tile before the record
+        const uint64_t sel = dep_tab[tag];
+        const uint32_t wlo = __builtin_amdgcn_perm(dhi, dlo, (uint32_t)sel);
+        const uint32_t whi = __builtin_amdgcn_perm(dhi, dlo, (uint32_t)(sel >> 32));
+        if (act) wp0[o] = ((uint64_t)whi << 32) | wlo;
+        RunJob job;
+        job.n = act ? cnt : 0u;
+        job.dst = cbase0 + excl + o + 1;
+        job.raw = f;
+        job.src = A + (uint32_t)p + 10;
+        run_jobs(a, job, d, A, (uint32_t)(kB + kPad));
+        sum += readlane32(inc, 63);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    return;
+  }
   }
   // fast path: record list per quarter tile (lanes 16h .. 16h+15), 64 records per batch
   uint64_t sum = 0;        // words of the tile's records so far
@@ -1170,6 +1235,9 @@ __device__ __forceinline__ void expand_records(const UnpackArgs& a, uint64_t A, 
 #ifndef CPK_UNPACK_WPE
 #define CPK_UNPACK_WPE 7  // 72 VGPRs: 7 waves per SIMD (LDS allows 7); 6 at the unconstrained 80
 #endif
+// PLAIN: the plain-tile expansion is compiled in (launched for batches of large messages only:
+// its code costs the kernel a few percent where few tiles are plain).
+template <bool PLAIN>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CPK_UNPACK_WPE))) void
 unpack_tiles_kernel(UnpackArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds_data[4][kB + kPad];
@@ -1235,6 +1303,7 @@ unpack_tiles_kernel(UnpackArgs a) {
 
   // ---- the tile's entry and the words before it ------------------------------------------
   uint64_t tm = tm0, excl = 0;
+  uint64_t w_tile = ~0ull;  // words of the tile's records (tiles without a message start)
   if (t == 0 || fms == 0) {
     if (!has_start) {  // (tile 0 without a message start: bytes before the first message)
       const uint64_t w = readlane32(wave_incl_sum32(mask_words(d, st.s, tm0, runm)), 63);
@@ -1270,7 +1339,10 @@ unpack_tiles_kernel(UnpackArgs a) {
         tm = tm0;
       if (!has_start) w = readlane32(wave_incl_sum32(mask_words(d, st.s, tm, runs)), 63);
     }
-    if (!has_start && l == 0) store_agent(a.desc + t, make_desc(kDescIncl, xE, x0, excl + w));
+    if (!has_start) {
+      w_tile = w;
+      if (l == 0) store_agent(a.desc + t, make_desc(kDescIncl, xE, x0, excl + w));
+    }
     if (a.stamps && l == 0 && t < 1024) {  // diagnostic dump (CPK_STAMPS=1)
       a.stamps[4 * t] = E | ((uint64_t)Eopt << 32);
       a.stamps[4 * t + 1] = xE | ((uint64_t)x0 << 32);
@@ -1280,8 +1352,8 @@ unpack_tiles_kernel(UnpackArgs a) {
   }
 
   // ---- expansion -------------------------------------------------------------------------
-  expand_records(a, A, d, aux, dep_tab, deposit_sel((uint32_t)l & 15), tm, excl, win, mfirst,
-                 mlast, msw);
+  expand_records<PLAIN>(a, A, d, aux, dep_tab, deposit_sel((uint32_t)l & 15), tm, excl, win, mfirst,
+                 mlast, msw, w_tile);
 }
 
 // 6. Serial re-decode of flagged messages: one wave per message; lane 0 walks the records of a
@@ -1409,8 +1481,14 @@ hipError_t launch_unpack_header(const uint8_t* packed, const uint64_t* in_off, u
 hipError_t launch_unpack_stage(int stage, const UnpackArgs& a, hipStream_t stream) {
   if (a.ntiles == 0) return hipSuccess;
   if (stage == kUnpackTiles) {
-    hipLaunchKernelGGL(unpack_tiles_kernel, dim3((unsigned)((a.ntiles + 3) / 4)), dim3(256), 0,
-                       stream, a);
+    // plain tiles are most tiles when messages span several tiles
+    const bool plain = a.word_off && a.nmsgs && a.nbytes / a.nmsgs >= 4 * (uint64_t)kB;
+    if (plain)
+      hipLaunchKernelGGL(unpack_tiles_kernel<true>, dim3((unsigned)((a.ntiles + 3) / 4)),
+                         dim3(256), 0, stream, a);
+    else
+      hipLaunchKernelGGL(unpack_tiles_kernel<false>, dim3((unsigned)((a.ntiles + 3) / 4)),
+                         dim3(256), 0, stream, a);
   } else {
     // a small grid: it only loops over the (rare) flagged messages, and an empty launch of
     // thousands of workgroups costs microseconds

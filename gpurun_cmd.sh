@@ -1,2 +1,3 @@
 cd $GRAFT_REPO_ROOT
-SKIPS="0 4 8 16 48 60" CFGS="c2 c4" bash tools/gpu_ablate.sh ab1 && TESTS=none VARIANTS="base w7" CFGS="c2 c3 c5" bash tools/gpu_check.sh f6 && CFGS="c2 c4" bash tools/gpu_prof.sh p6 && timeout -k 10 200 python -u -m pytest tests/test_gpu_pack.py -q -x --timeout 120 --timeout-method thread -p no:cacheprovider -k concurrent
+timeout -k 10 400 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/f14_tests.log 2>&1; tail -2 gpurun_out/f14_tests.log; grep -E "^FAILED" gpurun_out/f14_tests.log | head -5
+TESTS=none CFGS="c2 c3 c4 c5" bash tools/gpu_check.sh f14
