@@ -551,7 +551,7 @@ def main():
             "roofline": s["roofline"],
             "cpu_baseline": cb,
             "kernels": {"pack": "pack_tile + scan + pack_place (capnproto_amd/csrc/cpk_pack.hip)",
-                        "unpack": "header + scan + index + resolve + expand + fallback "
+                        "unpack": "header (+ scratch zeroing) + scan + unpack_tiles + fallback "
                                   "(capnproto_amd/csrc/cpk_unpack.hip)",
                         "knobs": knobs},
         }
@@ -563,10 +563,54 @@ def main():
                 result["sub_results"].append(sr)
         if hi is not None:
             result["host_inclusive"] = hi
+        if not args.no_host:
+            result["small_message_latency"] = small_message_latency(codec)
         print(json.dumps(result))
     codec.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def small_message_latency(codec, reps=300):
+    """Per-call latency of the host entry points on one small message -- the addressbook sample
+    (tests/golden/addressbook.bin, 288 B: the reference's samples/addressbook.c++ message), as
+    writePackedMessage / PackedMessageReader over the C++ facade would call them: pinned-less
+    host buffers, upload, the kernels, a sync, download."""
+    import ctypes as C
+    import numpy as np
+    src = os.path.join(ROOT, "tests", "golden", "addressbook.bin")
+    words = np.frombuffer(open(src, "rb").read(), "<u8").copy()
+    n = len(words)
+    off = np.array([0, n], "<u8")
+    cap = 8 * n + n + 16
+    out = np.zeros(cap, np.uint8)
+    oo = np.zeros(2, "<u8")
+    st = np.zeros(1, "<i4")
+    back = np.zeros(n, "<u8")
+    wo = np.zeros(2, "<u8")
+    lib = codec.lib
+    p = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+    t_pack, t_unpack = [], []
+    for i in range(reps + 20):
+        t0 = time.perf_counter()
+        r1 = lib.cpk_pack_messages_host(codec.ctx, p(words), n, p(off), 1, p(out), cap, p(oo), p(st))
+        t1 = time.perf_counter()
+        P = int(oo[1])
+        r2 = lib.cpk_unpack_messages_host(codec.ctx, p(out), P, p(oo), 1, p(back), n, p(wo), p(st),
+                                          None)
+        t2 = time.perf_counter()
+        if r1 or r2:
+            return {"error": [int(r1), int(r2)]}
+        if i >= 20:
+            t_pack.append(t1 - t0)
+            t_unpack.append(t2 - t1)
+    ok = bool((back == words).all())
+    return {"message_bytes": 8 * n, "packed_bytes": P, "round_trip_exact": ok,
+            "pack_us_median": round(1e6 * float(np.median(t_pack)), 1),
+            "unpack_us_median": round(1e6 * float(np.median(t_unpack)), 1),
+            "calls": reps,
+            "path": "cpk_pack_messages_host / cpk_unpack_messages_host (H2D, kernels, sync, D2H) "
+                    "on the addressbook sample"}
 
 
 def host_inclusive_pipelined(codecs, words, off, total, n, moff, steps, chunks=8):

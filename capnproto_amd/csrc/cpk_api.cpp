@@ -283,7 +283,7 @@ cpk_status unpack_common(cpk_ctx* ctx, uint32_t mode, const uint8_t* d_packed, u
                          uint64_t* d_words, uint64_t cap, uint64_t* d_word_off_out,
                          int32_t* d_status, uint64_t* d_size_out, uint64_t limit,
                          hipStream_t stream, uint64_t* d_in_end = nullptr,
-                         uint64_t* d_rec_pos = nullptr) {
+                         uint64_t* d_rec_pos = nullptr, bool store_free = false) {
   if (!ctx || (!d_in_off && n) || (!d_packed && P) || (!d_status && n))
     return CPK_ERR_INVALID_ARGUMENT;
   if (hipSetDevice(ctx->device) != hipSuccess) return CPK_ERR_HIP;
@@ -331,7 +331,8 @@ cpk_status unpack_common(cpk_ctx* ctx, uint32_t mode, const uint8_t* d_packed, u
   a.word_off = mode == 2 ? nullptr : word_off;
   a.hdr_status = mode == 0 ? s.hdr_status : nullptr;
   a.words = d_words;
-  a.words_capacity = d_words ? cap : 0;
+  // a store-free parse (PackedInputStream::skip) decodes against no output at all
+  a.words_capacity = store_free ? ~0ull : (d_words ? cap : 0);
   a.status = d_status;
   a.size_out = d_size_out;
   a.in_end = d_in_end;
@@ -820,10 +821,14 @@ cpk_status cpk_unpack_prefix_host(cpk_ctx* ctx, const uint8_t* h_packed, uint64_
   // device never writes past min(max_words, 128 * avail + 256) words
   const uint64_t room = std::min<uint64_t>(max_words, 128 * avail_bytes + 256);
   cpk_status st;
-  if ((st = ensure(&ctx->stage[0], &ctx->stage_size[0], room * 8 + 16)) != CPK_OK) return st;
+  // h_words NULL: a skip (serialize-packed.c++:185-299) -- parsed with nothing stored at all
+  const bool store_free = h_words == nullptr;
+  if (!store_free &&
+      (st = ensure(&ctx->stage[0], &ctx->stage_size[0], room * 8 + 16)) != CPK_OK)
+    return st;
   if ((st = ensure(&ctx->stage[1], &ctx->stage_size[1], avail_bytes + 16)) != CPK_OK) return st;
   if ((st = ensure(&ctx->stage[2], &ctx->stage_size[2], 80)) != CPK_OK) return st;
-  uint64_t* d_words = (uint64_t*)ctx->stage[0];
+  uint64_t* d_words = store_free ? nullptr : (uint64_t*)ctx->stage[0];
   uint8_t* d_packed = (uint8_t*)ctx->stage[1];
   uint64_t* d_in_off = (uint64_t*)ctx->stage[2];  // [2]
   uint64_t* d_word_off = d_in_off + 2;            // [2]
@@ -839,7 +844,7 @@ cpk_status cpk_unpack_prefix_host(cpk_ctx* ctx, const uint8_t* h_packed, uint64_
   // one exact-size chunk of max_words words (the flat-packed mode); with d_at given the
   // terminal record also reports where a short or overshooting read stops
   st = unpack_common(ctx, 1, d_packed, avail_bytes, d_in_off, 1, d_word_off, d_words, max_words,
-                     nullptr, d_status, d_at, 0, s, d_in_end);
+                     nullptr, d_status, d_at, 0, s, d_in_end, nullptr, store_free);
   if (st != CPK_OK) return st;
   if ((st = cpk_sync(ctx, s)) != CPK_OK) return st;
   uint64_t at[2] = {0, 0};  // in_end, words

@@ -347,8 +347,8 @@ size_t _::PackedInputStream::tryRead(void* buffer, size_t minBytes, size_t maxBy
 }
 
 void _::PackedInputStream::skip(size_t bytes) {
-  // serialize-packed.c++:185-299: the same parse with nothing stored -- the device decodes into
-  // its own scratch and no word comes back to the host
+  // serialize-packed.c++:185-299: the same parse with nothing stored -- the device parses with no
+  // output buffer at all (cpk_unpack_prefix_host with no destination)
   if (bytes == 0) return;
   if (bytes % 8 != 0) fail(CPK_ERR_INVALID_ARGUMENT, "PackedInputStream reads must be word-aligned.");
   if (readWords(nullptr, bytes / 8, bytes / 8) < bytes / 8)

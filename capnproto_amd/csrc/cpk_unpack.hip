@@ -403,7 +403,7 @@ __device__ __forceinline__ int32_t handle_record(const UnpackArgs& a, const uint
   }
   if (st == kOK && !mi.fits) st = kCap;
   if (mi.fits && !trunc1) {
-    a.words[mi.base + wb] = word;
+    if (a.words) a.words[mi.base + wb] = word;  // (NULL: a skip, nothing stored)
     if (a.rec_pos) a.rec_pos[mi.base + wb] = pabs;
     uint64_t n = cnt;
     if (over) n = mi.total - wb - 1;
@@ -427,7 +427,7 @@ __device__ __forceinline__ int32_t handle_record(const UnpackArgs& a, const uint
 __device__ __forceinline__ void run_jobs(const UnpackArgs& a, const RunJob& job,
                                          const uint8_t* d = nullptr, uint64_t dbase = 0,
                                          uint32_t dlen = 0) {
-  uint64_t pend = ballot(job.n != 0);
+  uint64_t pend = a.words ? ballot(job.n != 0) : 0ull;  // (no words: a skip)
   const int l = lane_id();
   while (pend) {
     const int j = lowest_bit(pend);
@@ -904,7 +904,7 @@ __device__ __forceinline__ void expand_records(const UnpackArgs& a, uint64_t A, 
   uint16_t* list = (uint16_t*)aux;
   // Fast expansion when every message touching the tile is in the window, has a valid header,
   // is not left to the fallback, fits the output, and no two messages start at the same byte.
-  bool fast = a.mode == 0 && mlast - (mfirst - 1) <= 63 && a.word_off;
+  bool fast = a.mode == 0 && mlast - (mfirst - 1) <= 63 && a.word_off && a.words;
   if (fast) {
     const int64_t m = win.mw + l;
     const bool inrange = m >= 0 && (uint64_t)m < mlast;

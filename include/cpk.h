@@ -240,7 +240,8 @@ cpk_status cpk_unpack_words_host(cpk_ctx* ctx, const uint8_t* h_packed, uint64_t
  * max_words (CPK_ERR_RUN_OVERSHOOT), or the buffer ends first (CPK_ERR_PREMATURE_EOF).  In all
  * three cases *consumed_out / *words_out are the record boundary where the read stopped -- for
  * the two failures the start of the record that did not fit -- and the words decoded before it,
- * which land in h_words (h_words may be NULL: a skip, nothing is copied back).  The stream
+ * which land in h_words (h_words NULL: a skip -- the records are parsed and checked with no
+ * output buffer at all, nothing stored on the device either).  The stream
  * caller keeps the unconsumed bytes in front of the next buffer and calls again. */
 cpk_status cpk_unpack_prefix_host(cpk_ctx* ctx, const uint8_t* h_packed, uint64_t avail_bytes,
                                   uint64_t* h_words, uint64_t max_words, uint64_t* words_out,
