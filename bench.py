@@ -80,6 +80,8 @@ def parse():
                     help="skip the manifest hash check (the device round trip is still checked)")
     ap.add_argument("--host-inclusive", action="store_true",
                     help="also time the serial (one stream) H2D/D2H-inclusive path")
+    ap.add_argument("--no-split", action="store_true",
+                    help="skip the stream-split (boundary discovery) measurement")
     ap.add_argument("--no-host", action="store_true",
                     help="skip the host-inclusive (pipelined) measurement")
     ap.add_argument("--ab", action="store_true",
@@ -565,10 +567,45 @@ def main():
             result["host_inclusive"] = hi
         if not args.no_host:
             result["small_message_latency"] = small_message_latency(codec)
+        if not args.no_split and world == 1:
+            result["stream_split"] = split_bench(codec, args.seed)
         print(json.dumps(result))
     codec.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def split_bench(codec, seed, n=1 << 20, reps=5):
+    """Stream boundary discovery (cpk_split_packed_stream) on a C5-shaped
+    stream: 1 Mi messages of 2^k + 1 words (k in 3..11), mixed profiles, packed back to back with
+    no index.  Timed: the whole split (flat decode of the stream + the block-parallel walk over
+    the message headers), device-resident; checked against the generator's layout."""
+    torch = codec.torch
+    off, total = codec.gen_offsets(n, seed=seed + 5)
+    words = codec.gen_messages("mixed", off, total, seed=seed + 5)
+    packed, poff, st = codec.pack_messages(words, off)
+    codec.sync()
+    nbytes = int(poff[-1].item())
+    out = torch.empty(total + 16, dtype=torch.int64, device=codec.device)
+    res = None
+    times = []
+    for i in range(reps + 1):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        res = codec.split_packed_stream(packed, total + 16, n + 1, nbytes=nbytes, words=out)
+        codec.sync()
+        if i:
+            times.append(time.perf_counter() - t0)
+    w2, woff, ioff, status, cnt = res
+    ok = (int(cnt.item()) == n and int(status[n].item()) == 0 and torch.equal(woff[:n + 1], off)
+          and torch.equal(ioff[:n + 1], poff) and torch.equal(w2[:total], words[:total]))
+    t = min(times)
+    del words, packed, out, w2
+    return {"messages": n, "unpacked_bytes": 8 * total, "packed_bytes": nbytes,
+            "ms": round(1e3 * t, 3), "GiBps": round(8 * total / t / 2**30, 2),
+            "split_exact": bool(ok),
+            "what": "flat decode of the stream + block-parallel message-chain walk; unpacked "
+                    "GiB/s, device-resident, wall clock of the call incl. its sync"}
 
 
 def small_message_latency(codec, reps=300):

@@ -603,11 +603,14 @@ cpk_status cpk_split_packed_stream(cpk_ctx* ctx, const uint8_t* d_packed, uint64
   if (order_streams(ctx, s) != CPK_OK) return CPK_ERR_HIP;
   // the record-head map (one u64 per output word) and 8 words of call state: in_off[2],
   // word_off[2], meta[4] (stop byte, stop word, decode status)
-  cpk_status st = ensure(&ctx->stage[4], &ctx->stage_size[4], words_capacity * 8 + 128);
+  const uint64_t rp_bytes = align16(words_capacity * 8 + 128);
+  cpk_status st = ensure(&ctx->stage[4], &ctx->stage_size[4],
+                         rp_bytes + cpk::split_scratch_bytes(words_capacity));
   if (st != CPK_OK) return st;
   uint64_t* state = (uint64_t*)ctx->stage[4];
   uint64_t* rec_pos = state + 8;
   uint64_t* meta = state + 4;
+  void* split_scr = (char*)ctx->stage[4] + rp_bytes;
   hipError_t e = cpk::launch_set_u64x4(state, 0, nbytes, 0, words_capacity, s);
   if (e == hipSuccess) e = cpk::launch_set_u64x4(meta, 0, 0, CPK_ERR_PREMATURE_EOF, 0, s);
   if (e == hipSuccess && words_capacity)
@@ -621,8 +624,8 @@ cpk_status cpk_split_packed_stream(cpk_ctx* ctx, const uint8_t* d_packed, uint64
     if (st != CPK_OK) return st;
   }
   return hip_status(cpk::launch_split_walk(d_packed, nbytes, d_words, rec_pos, meta, max_msgs,
-                                           limit, d_msg_word_off, d_msg_in_off, d_status,
-                                           d_nmsgs, s));
+                                           limit, words_capacity, split_scr, d_msg_word_off,
+                                           d_msg_in_off, d_status, d_nmsgs, s));
 }
 
 cpk_status cpk_unpacked_size(cpk_ctx* ctx, const uint8_t* d_packed, uint64_t total_bytes,

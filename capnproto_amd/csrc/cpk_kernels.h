@@ -112,10 +112,14 @@ hipError_t launch_unpack_init(uint32_t mode, const uint64_t* in_off, const uint6
 hipError_t launch_fill(void* p, uint64_t nbytes, uint8_t value, hipStream_t stream);
 hipError_t launch_set_u64x4(uint64_t* dst, uint64_t v0, uint64_t v1, uint64_t v2, uint64_t v3,
                             hipStream_t stream);
+// The message chain over the decoded words, block-parallel (cpk_stream.hip); scratch holds
+// split_scratch_bytes(words_capacity).
+uint64_t split_scratch_bytes(uint64_t words_capacity);
 hipError_t launch_split_walk(const uint8_t* packed, uint64_t nbytes, const uint64_t* words,
                              const uint64_t* rec_pos, const uint64_t* meta, uint64_t max_msgs,
-                             uint64_t limit, uint64_t* msg_word_off, uint64_t* msg_in_off,
-                             int32_t* status, uint64_t* nmsgs, hipStream_t stream);
+                             uint64_t limit, uint64_t words_capacity, void* scratch,
+                             uint64_t* msg_word_off, uint64_t* msg_in_off, int32_t* status,
+                             uint64_t* nmsgs, hipStream_t stream);
 
 hipError_t launch_gather_segments(const uint64_t* meta, uint32_t nseg, uint64_t total,
                                   uint64_t* out, hipStream_t stream);

@@ -47,8 +47,15 @@ struct Flat {
   const uint8_t* packed;
   uint64_t nbytes;
   const uint64_t* rec_pos;
+  const uint64_t* meta;  // (device) where the flat decode stopped: packed byte, word, status
   uint64_t Bc, Tc;  // packed byte / word where the flat decode stopped
   bool capped;      // ... because the output was full, not because the input ended
+
+  __device__ void load() {
+    Bc = meta[0];
+    Tc = meta[1];
+    capped = (int32_t)meta[2] != sEOF && Bc < nbytes;
+  }
 
   // packed byte of the record whose head is word x (x <= Tc); kNone inside a run
   __device__ uint64_t head(uint64_t x) const { return x == Tc ? Bc : rec_pos[x]; }
@@ -69,31 +76,85 @@ struct Flat {
   }
 };
 
-__global__ __launch_bounds__(64) void split_walk_kernel(Flat F, const uint64_t* __restrict__ words,
-                                                        const uint64_t* __restrict__ meta,
-                                                        uint64_t max_msgs, uint64_t limit,
-                                                        uint64_t* __restrict__ msg_word_off,
-                                                        uint64_t* __restrict__ msg_in_off,
-                                                        int32_t* __restrict__ status,
-                                                        uint64_t* __restrict__ nmsgs) {
+// One message of the chain at word s (s < Tc; hs = head(s)), checked the way
+// InputStreamMessageReader reads it from a PackedInputStream (serialize.c++:207-269): the first
+// word (no run may cross word 1), the rest of the table (nor its end), the segment-count and
+// traversal limits, the segments (nor the message end).  Single lane.  Returns the status; on
+// success *end / *he are the next message's first word and its record head, *single the
+// message's size when it has one segment (0 otherwise).
+__device__ int32_t message_at(const Flat& F, const uint64_t* __restrict__ words, uint64_t s,
+                              uint64_t limit, uint64_t* end, uint64_t* he, uint64_t* single) {
+  const uint64_t w0 = words[s];
+  const uint64_t h1 = F.head(s + 1);  // s < Tc, so s + 1 <= Tc
+  int32_t e = F.read_to(s + 1, h1);
+  if (e) return e;
+  const uint32_t nm1 = (uint32_t)w0;
+  if (nm1 >= 511) return sTooMany;  // :217
+  const uint32_t nseg = nm1 + 1;
+  const uint64_t tw = nseg / 2 + 1;
+  uint64_t total = w0 >> 32;
+  if (nseg > 1) {
+    // the other sizes ((nseg & ~1) u32 entries) in one read that ends with the table
+    e = F.read_to(s + tw, s + tw <= F.Tc ? F.head(s + tw) : kNone);
+    if (e) return e;
+    const uint32_t* t32 = reinterpret_cast<const uint32_t*>(words + s);
+    for (uint32_t i = 1; i < nseg; i++) total += t32[i + 1];
+  }
+  if (total > limit) return sTooLarge;  // :235
+  const uint64_t x = s + tw + total;
+  const uint64_t hx = x <= F.Tc ? F.head(x) : kNone;
+  e = F.read_to(x, hx);  // the segments: no run may cross the message end
+  if (e) return e;
+  *end = x;
+  *he = hx;
+  *single = nseg == 1 ? tw + total : 0;
+  return sOK;
+}
+
+// Where a walk stopped: k messages from its start, the next message's first word s and record
+// head hs, and why (kRunOn: it reached its word limit wend and the stream goes on).
+constexpr int32_t kRunOn = -1;
+struct WalkEnd {
+  uint64_t k, s, hs;
+  int32_t stop;
+};
+
+// The message chain from word s (head hs) by one wave, until a message would start at or past
+// word wend, kmax messages are out, the decoded words end, or a message fails its checks.
+// emit(i, s_i, hs_i) receives message i of the walk (on the lane that found it).  A stretch of
+// same-size single-segment messages (the common batch shape) is confirmed 64 messages per step:
+// lane j checks the header and both read boundaries of message k + j; any other message costs a
+// few dependent loads.
+// meet(s) (optional): true when the walk should stop at message start s (kMet), before it.
+constexpr int32_t kMet = -2;
+struct NoMeet {
+  __device__ bool operator()(uint64_t) const { return false; }
+  static constexpr bool kActive = false;
+};
+template <class Emit, class Meet = NoMeet>
+__device__ WalkEnd walk_messages(const Flat& F, const uint64_t* __restrict__ words, uint64_t s,
+                                 uint64_t hs, uint64_t kmax, uint64_t limit, uint64_t wend,
+                                 Emit emit, Meet meet = Meet()) {
   const int l = lane_id();
-  F.Bc = meta[0];
-  F.Tc = meta[1];
-  F.capped = (int32_t)meta[2] != sEOF && F.Bc < F.nbytes;
-  uint64_t s = 0, k = 0, hs = F.head(0);
+  uint64_t k = 0;
   uint64_t L = 0, prevL = 0;  // the last two message sizes (a stride is tried when they agree)
-  int32_t stop = sOK;
-  while (k < max_msgs) {
-    if (s == F.Tc) {
-      // the next message's first word lies past what decoded: end of input (clean when no
-      // bytes are left), a cut record, or a full output
-      if (F.Bc < F.nbytes || F.capped) stop = F.read_to(s + 1, kNone);
+  WalkEnd r;
+  r.stop = kRunOn;
+  while (k < kmax && s < wend) {
+    if (Meet::kActive && meet(s)) {
+      r.stop = kMet;
       break;
     }
-    if (L != 0 && L == prevL) {
+    if (s == F.Tc) {
+      // the next message's first word lies past what decoded: end of input (clean when no bytes
+      // are left), a cut record, or a full output
+      r.stop = (F.Bc < F.nbytes || F.capped) ? F.read_to(s + 1, kNone) : sOK;
+      break;
+    }
+    if (!Meet::kActive && L != 0 && L == prevL) {
       // ---- a stretch of messages of L words (single segment): 64 per step ----
       const uint64_t p = s + (uint64_t)l * L;
-      bool ok = k + (uint64_t)l < max_msgs && p + L <= F.Tc;
+      bool ok = k + (uint64_t)l < kmax && p < wend && p + L <= F.Tc;
       uint64_t w0 = 0, h1 = kNone, hL = kNone;
       if (ok) {
         w0 = words[p];
@@ -104,11 +165,7 @@ __global__ __launch_bounds__(64) void split_walk_kernel(Flat F, const uint64_t* 
       const uint64_t bad = ballot(!ok);
       const int n = bad ? lowest_bit(bad) : 64;
       const uint64_t hprev = shfl64(hL, l > 0 ? l - 1 : 0);
-      if (l < n) {
-        msg_word_off[k + l] = p;
-        msg_in_off[k + l] = l == 0 ? hs : hprev;
-        status[k + l] = sOK;
-      }
+      if (l < n) emit(k + l, p, l == 0 ? hs : hprev);
       if (n > 0) {
         hs = readlane64(hL, n - 1);
         s += (uint64_t)n * L;
@@ -118,61 +175,258 @@ __global__ __launch_bounds__(64) void split_walk_kernel(Flat F, const uint64_t* 
       prevL = 0;  // the stretch ended: the next message goes the serial way
       continue;
     }
-    // ---- one message (serialize.c++:207-269) ----
-    const uint64_t w0 = words[s];
-    const uint64_t h1 = F.head(s + 1);  // s < Tc, so s + 1 <= Tc
-    int32_t e = F.read_to(s + 1, h1);   // the first word: no run may cross word 1
+    uint64_t x = 0, hx = kNone, single = 0;
+    int32_t e = 0;
+    if (l == 0) e = message_at(F, words, s, limit, &x, &hx, &single);
+    e = (int32_t)readlane32((uint32_t)e, 0);
     if (e) {
-      stop = e;
+      r.stop = e;
       break;
     }
-    const uint32_t nm1 = (uint32_t)w0;
-    if (nm1 >= 511) {  // :217
-      stop = sTooMany;
-      break;
-    }
-    const uint32_t nseg = nm1 + 1;
-    const uint64_t tw = nseg / 2 + 1;
-    uint64_t total = w0 >> 32;
-    if (nseg > 1) {
-      // the other sizes ((nseg & ~1) u32 entries) in one read that ends with the table
-      e = F.read_to(s + tw, s + tw <= F.Tc ? F.head(s + tw) : kNone);
-      if (e) {
-        stop = e;
-        break;
-      }
-      const uint32_t* t32 = reinterpret_cast<const uint32_t*>(words + s);
-      uint64_t part = 0;
-      for (uint32_t i = 1 + (uint32_t)l; i < nseg; i += 64) part += t32[i + 1];
-      total += wave_sum64(part);
-    }
-    if (total > limit) {  // :235
-      stop = sTooLarge;
-      break;
-    }
-    const uint64_t end = s + tw + total;
-    const uint64_t he = end <= F.Tc ? F.head(end) : kNone;
-    e = F.read_to(end, he);  // the segments: no run may cross the message end
-    if (e) {
-      stop = e;
-      break;
-    }
-    if (l == 0) {
-      msg_word_off[k] = s;
-      msg_in_off[k] = hs;
-      status[k] = sOK;
-    }
+    if (l == 0) emit(k, s, hs);
     k++;
     prevL = L;
-    L = nseg == 1 ? tw + total : 0;
-    s = end;
-    hs = he;
+    L = readlane64(single, 0);
+    s = readlane64(x, 0);
+    hs = readlane64(hx, 0);
+  }
+  r.k = k;
+  r.s = s;
+  r.hs = hs;
+  return r;
+}
+
+// ---- block-parallel split ------------------------------------------------------------------
+// The decoded words are cut into blocks of kSplitBlock words.  Every block guesses where the
+// chain first enters it -- the first record head from which two messages in a row pass their
+// checks (a guess is only a guess: a wrong one is caught below) -- and walks the chain from
+// there to the block end, keeping up to kSplitList message starts.  One wave then runs over the
+// blocks in order: a block whose true entry (the previous block's exit) is its guess keeps its
+// walk; any other block is walked again from its true entry.  A last pass writes every block's
+// messages at their global index.
+constexpr uint64_t kSplitBlock = 1ull << 20;  // words per block
+constexpr uint32_t kSplitList = 4096;          // message starts a block keeps
+constexpr uint64_t kSplitScan = 1ull << 16;    // words a block searches for its guess
+
+struct SplitBlock {
+  uint64_t g, x, hx, k;  // guess (kNone: none), exit word / head, messages
+  int32_t stop;          // kRunOn, or why the walk from the guess ended inside the block
+  uint32_t over;         // more messages than the list holds
+  uint64_t entry, kbase, kend;  // resolved: true entry (kNone: none), first / end global index
+};
+
+__global__ __launch_bounds__(64) void split_spec_kernel(Flat F, const uint64_t* __restrict__ words,
+                                                        uint64_t limit, SplitBlock* blocks,
+                                                        uint64_t* lists) {
+  F.load();
+  const int l = lane_id();
+  const uint64_t b = blockIdx.x;
+  const uint64_t w0 = b * kSplitBlock;
+  const uint64_t w1 = w0 + kSplitBlock;
+  SplitBlock r;
+  r.g = kNone;
+  r.x = kNone;
+  r.hx = kNone;
+  r.k = 0;
+  r.stop = kRunOn;
+  r.over = 0;
+  uint64_t* const list = lists + b * kSplitList;
+  auto walk_from = [&](uint64_t g, uint64_t hg) {
+    const WalkEnd we = walk_messages(F, words, g, hg, ~0ull, limit, w1,
+                                     [&](uint64_t i, uint64_t s, uint64_t) {
+                                       if (i < kSplitList) list[i] = s;
+                                     });
+    r.g = g;
+    r.x = we.s;
+    r.hx = we.hs;
+    r.k = we.k;
+    r.stop = we.stop;
+    r.over = we.k > kSplitList ? 1u : 0u;
+  };
+  if (b == 0) {
+    walk_from(0, F.head(0));
+  } else {
+    // the first record head from which two messages in a row pass their checks and whose chain
+    // then runs to the block end without failing (the true chain of a readable stream never
+    // fails inside it; a chain through words that only look like segment tables soon does)
+    const uint64_t lim = min(min(w1, F.Tc), w0 + kSplitScan);
+    for (uint64_t base = w0; base < lim;) {
+      const uint64_t p = base + (uint64_t)l;
+      bool cand = false;
+      uint64_t hp = kNone;
+      if (p < lim) {
+        hp = F.rec_pos[p];
+        if (hp != kNone && (uint32_t)words[p] < 511) {
+          uint64_t x = 0, hx = 0, single = 0;
+          if (message_at(F, words, p, limit, &x, &hx, &single) == sOK) {
+            uint64_t x2 = 0, hx2 = 0;
+            cand = x == F.Tc || message_at(F, words, x, limit, &x2, &hx2, &single) == sOK;
+          }
+        }
+      }
+      const uint64_t cb = ballot(cand);
+      if (!cb) {
+        base += 64;
+        continue;
+      }
+      const int j = lowest_bit(cb);
+      walk_from(base + (uint64_t)j, readlane64(hp, j));
+      if (r.stop == kRunOn || r.stop == sOK) break;  // ran to the block end (or the stream's)
+      r.g = kNone;  // failed inside the block: not the chain; the next candidate
+      base += (uint64_t)j + 1;
+    }
   }
   if (l == 0) {
-    msg_word_off[k] = s;
-    msg_in_off[k] = hs;
-    status[k] = stop;
-    *nmsgs = k;
+    r.entry = kNone;
+    r.kbase = r.kend = 0;
+    blocks[b] = r;
+  }
+}
+
+// Meets a block's listed starts (ascending) -- lane 0 keeps the list position.
+struct Meet2 {
+  const uint64_t* list;
+  uint64_t n;
+  uint64_t* j;
+  static constexpr bool kActive = true;
+  __device__ bool operator()(uint64_t s) const {
+    bool met = false;
+    if (lane_id() == 0) {
+      while (*j < n && list[*j] < s) (*j)++;
+      met = *j < n && list[*j] == s;
+    }
+    return readlane32(met ? 1u : 0u, 0) != 0;
+  }
+};
+
+// One wave over the blocks in order: each block's true entry, global message range and the
+// stream's stop.  A block whose entry is its guess (or that the chain passes over) costs a load;
+// any other block is walked again here.
+__global__ __launch_bounds__(64) void split_resolve_kernel(Flat F, const uint64_t* __restrict__ words,
+                                                           uint64_t limit, uint64_t max_msgs,
+                                                           SplitBlock* blocks,
+                                                           const uint64_t* __restrict__ lists,
+                                                           uint64_t nblocks,
+                                                           uint64_t* __restrict__ msg_word_off,
+                                                           uint64_t* __restrict__ msg_in_off,
+                                                           int32_t* __restrict__ status,
+                                                           uint64_t* __restrict__ nmsgs) {
+  F.load();
+  const int l = lane_id();
+  uint64_t E = 0, hE = F.head(0), K = 0;
+  int32_t stop = kRunOn;
+  for (uint64_t base = 0; base < nblocks && stop == kRunOn; base += 64) {
+    // the next 64 blocks' walks in one round trip (lane j: block base + j)
+    SplitBlock mine = {};
+    if (base + l < nblocks) mine = blocks[base + l];
+    for (int j = 0; j < 64 && base + j < nblocks && stop == kRunOn; j++) {
+      const uint64_t b = base + j;
+      const uint64_t w1 = (b + 1) * kSplitBlock;
+      if (E >= w1) continue;  // the chain passes over the block (a message longer than it)
+      const uint64_t g = readlane64(mine.g, j);
+      uint64_t x, hx, k;
+      int32_t st;
+      bool redo = readlane32(mine.over, j) != 0;
+      if (g == E) {
+        x = readlane64(mine.x, j);
+        hx = readlane64(mine.hx, j);
+        k = readlane64(mine.k, j);
+        st = (int32_t)readlane32((uint32_t)mine.stop, j);
+      } else {
+        // the guess was not the entry: walk the block from its true entry until the chain meets
+        // the guess's chain (a guess whose chain ran to the block end without failing nearly
+        // always joined the true chain early: a few messages here), then take the rest from it
+        const uint64_t gk = readlane64(mine.k, j);
+        const bool listed = g != kNone && gk <= kSplitList;
+        const uint64_t* const list = lists + b * kSplitList;
+        uint64_t jl = 0;  // next listed start to compare with (both chains ascend)
+        Meet2 mt{list, listed ? gk : 0, &jl};
+        const WalkEnd we = walk_messages(F, words, E, hE, ~0ull, limit, w1,
+                                         [&](uint64_t, uint64_t, uint64_t) {}, mt);
+        jl = readlane64(jl, 0);
+        if (we.stop == kMet) {
+          x = readlane64(mine.x, j);
+          hx = readlane64(mine.hx, j);
+          k = we.k + (gk - jl);
+          st = (int32_t)readlane32((uint32_t)mine.stop, j);
+        } else {
+          x = we.s;
+          hx = we.hs;
+          k = we.k;
+          st = we.stop;
+        }
+        redo = true;
+      }
+      uint64_t kend = K + k;
+      if (kend >= max_msgs) {
+        // the message limit falls in this block: the writer walks it and stops there
+        kend = max_msgs;
+        redo = true;
+        st = kRunOn;
+      }
+      if (l == 0) {
+        SplitBlock* const B = blocks + b;
+        B->entry = E;
+        B->kbase = K;
+        B->kend = kend;
+        B->over = redo ? 1u : 0u;  // the writer walks the block itself
+      }
+      K = kend;
+      if (K >= max_msgs) {
+        stop = sOK;  // max_msgs messages; the next one starts where the writer stops
+        break;
+      }
+      E = x;
+      hE = hx;
+      stop = st;
+    }
+  }
+  if (stop == kRunOn) stop = sOK;  // (nblocks covers every decoded word)
+  if (l == 0) {
+    *nmsgs = K;
+    status[K] = stop;
+    if (K < max_msgs || max_msgs == 0) {
+      msg_word_off[K] = E;
+      msg_in_off[K] = hE;
+    }
+  }
+}
+
+// Every block's messages at their global index: copied from the block's list, or walked again
+// when the list did not hold them (or the guess was off the chain, or the limit cuts the block).
+__global__ __launch_bounds__(64) void split_write_kernel(Flat F, const uint64_t* __restrict__ words,
+                                                         uint64_t limit, const SplitBlock* blocks,
+                                                         const uint64_t* lists,
+                                                         uint64_t* __restrict__ msg_word_off,
+                                                         uint64_t* __restrict__ msg_in_off,
+                                                         int32_t* __restrict__ status,
+                                                         uint64_t max_msgs) {
+  F.load();
+  const int l = lane_id();
+  const uint64_t b = blockIdx.x;
+  const SplitBlock B = blocks[b];
+  if (B.entry == kNone || B.kend <= B.kbase) return;
+  const uint64_t n = B.kend - B.kbase;
+  if (!B.over) {
+    const uint64_t* const list = lists + b * kSplitList;
+    for (uint64_t i = l; i < n; i += 64) {
+      const uint64_t s = list[i];
+      msg_word_off[B.kbase + i] = s;
+      msg_in_off[B.kbase + i] = F.head(s);
+      status[B.kbase + i] = sOK;
+    }
+    return;
+  }
+  const WalkEnd we = walk_messages(F, words, B.entry, F.head(B.entry), n, limit,
+                                   (b + 1) * kSplitBlock, [&](uint64_t i, uint64_t s, uint64_t hs) {
+                                     msg_word_off[B.kbase + i] = s;
+                                     msg_in_off[B.kbase + i] = hs;
+                                     status[B.kbase + i] = sOK;
+                                   });
+  // the message limit cut this block: the entry after the last message
+  if (B.kend == max_msgs && l == 0) {
+    msg_word_off[max_msgs] = we.s;
+    msg_in_off[max_msgs] = we.hs;
   }
 }
 
@@ -231,18 +485,29 @@ hipError_t launch_set_u64x4(uint64_t* dst, uint64_t v0, uint64_t v1, uint64_t v2
   return hipGetLastError();
 }
 
+uint64_t split_scratch_bytes(uint64_t words_capacity) {
+  const uint64_t nb = words_capacity / kSplitBlock + 1;
+  return nb * (sizeof(SplitBlock) + 8ull * kSplitList) + 64;
+}
+
 hipError_t launch_split_walk(const uint8_t* packed, uint64_t nbytes, const uint64_t* words,
                              const uint64_t* rec_pos, const uint64_t* meta, uint64_t max_msgs,
-                             uint64_t limit, uint64_t* msg_word_off, uint64_t* msg_in_off,
-                             int32_t* status, uint64_t* nmsgs, hipStream_t stream) {
+                             uint64_t limit, uint64_t words_capacity, void* scratch,
+                             uint64_t* msg_word_off, uint64_t* msg_in_off, int32_t* status,
+                             uint64_t* nmsgs, hipStream_t stream) {
   Flat F;
   F.packed = packed;
   F.nbytes = nbytes;
   F.rec_pos = rec_pos;
-  F.Bc = F.Tc = 0;
-  F.capped = false;
-  split_walk_kernel<<<1, 64, 0, stream>>>(F, words, meta, max_msgs, limit, msg_word_off,
-                                          msg_in_off, status, nmsgs);
+  F.meta = meta;
+  const uint64_t nb = words_capacity / kSplitBlock + 1;
+  SplitBlock* blocks = (SplitBlock*)scratch;
+  uint64_t* lists = (uint64_t*)((char*)scratch + ((nb * sizeof(SplitBlock) + 15) & ~15ull));
+  split_spec_kernel<<<(unsigned)nb, 64, 0, stream>>>(F, words, limit, blocks, lists);
+  split_resolve_kernel<<<1, 64, 0, stream>>>(F, words, limit, max_msgs, blocks, lists, nb,
+                                             msg_word_off, msg_in_off, status, nmsgs);
+  split_write_kernel<<<(unsigned)nb, 64, 0, stream>>>(F, words, limit, blocks, lists,
+                                                      msg_word_off, msg_in_off, status, max_msgs);
   return hipGetLastError();
 }
 

@@ -187,3 +187,77 @@ def test_large_uniform_stream(codec, oracle):
     assert int(cnt.item()) == n and int(status[n].item()) == P.OK
     assert torch.equal(woff[:n + 1], off) and torch.equal(ioff[:n + 1], poff)
     assert torch.equal(w2[:total], words[:total])
+
+
+def _mixed_stream(codec, n, seed):
+    """n messages of 2^k + 1 words (k in 3..11; C5's shape), mixed profiles, packed back to
+    back: (words, word offsets, packed bytes, packed offsets, total words, packed length)."""
+    off, total = codec.gen_offsets(n, seed=seed)
+    words = codec.gen_messages("mixed", off, total, seed=seed)
+    packed, poff, st = codec.pack_messages(words, off)
+    codec.sync()
+    assert (st == 0).all()
+    return words, off, packed, poff, total, int(poff[-1].item())
+
+
+def test_split_c5_shape_million_messages(codec):
+    """1 Mi mixed-size messages (C5's shape: 2^k-word messages of three profiles) in one stream,
+    split across many 1 Mi-word blocks: every message boundary, packed offset and word against
+    the generator's layout (whose packed bytes are pinned to the reference elsewhere)."""
+    import torch
+
+    n = 1 << 20
+    words, off, packed, poff, total, nbytes = _mixed_stream(codec, n, 11)
+    w2, woff, ioff, status, cnt = codec.split_packed_stream(packed, total + 16, n + 1,
+                                                            nbytes=nbytes)
+    codec.sync()
+    assert int(cnt.item()) == n and int(status[n].item()) == P.OK
+    assert (status[:n] == 0).all()
+    assert torch.equal(woff[:n + 1], off) and torch.equal(ioff[:n + 1], poff)
+    assert torch.equal(w2[:total], words[:total])
+
+
+def test_split_limit_and_cut_in_later_blocks(codec):
+    """max_msgs ending deep in the stream, and a stream cut inside a message many blocks in: the
+    split stops exactly where the reference's reader loop would."""
+    import torch
+
+    n = 1 << 16
+    words, off, packed, poff, total, nbytes = _mixed_stream(codec, n, 12)
+    m = 40000  # several blocks in
+    w2, woff, ioff, status, cnt = codec.split_packed_stream(packed, total + 16, m, nbytes=nbytes)
+    codec.sync()
+    assert int(cnt.item()) == m and int(status[m].item()) == P.OK
+    assert torch.equal(woff[:m + 1], off[:m + 1]) and torch.equal(ioff[:m + 1], poff[:m + 1])
+    # cut 3 bytes into message m's packed bytes: m whole messages, then premature end of input
+    cut = int(poff[m].item()) + 3
+    w2, woff, ioff, status, cnt = codec.split_packed_stream(packed, total + 16, n + 1, nbytes=cut)
+    codec.sync()
+    assert int(cnt.item()) == m and int(status[m].item()) == P.PREMATURE_EOF
+    assert torch.equal(woff[:m + 1], off[:m + 1]) and torch.equal(ioff[:m + 1], poff[:m + 1])
+    mw = int(off[m].item())
+    assert torch.equal(w2[:mw], words[:mw])
+
+
+def test_split_guess_off_chain(codec, oracle):
+    """Messages whose words look like segment tables (valid one-segment headers at record heads)
+    everywhere, so the guesses of the blocks land off the chain: the resolve walks those blocks
+    again and the split is still the reference reader loop's (message lengths and their packed
+    lengths from the oracle)."""
+    rng = np.random.default_rng(21)
+    msgs = []
+    for _ in range(400):
+        nw = int(rng.integers(20000, 40000))
+        body = np.zeros(nw, "<u8")
+        # every other word a plausible one-segment header of a 1..8-word message
+        body[::2] = (rng.integers(0, 8, (nw + 1) // 2).astype(np.uint64) << np.uint64(32))
+        body[1::2] = rng.integers(1 << 40, 1 << 62, nw // 2, dtype=np.uint64)
+        msgs.append(np.concatenate([np.array([nw << 32], "<u8"), body]))
+    packs = [oracle.pack_flat(m)[0] for m in msgs]
+    data = b"".join(packs)
+    gw, gwoff, gioff, gstop, gst = gpu_split(codec, data, cap=sum(len(m) for m in msgs) + 16,
+                                             max_msgs=len(msgs) + 1)
+    assert gstop == P.OK and (gst == P.OK).all() and len(gwoff) == len(msgs) + 1
+    assert (gwoff == np.cumsum([0] + [len(m) for m in msgs])).all()
+    assert (gioff == np.cumsum([0] + [len(p) for p in packs])).all()
+    assert gw.tobytes() == np.concatenate(msgs).tobytes()
