@@ -19,7 +19,7 @@ for v in ${VARIANTS:-base}; do
   if [ "$v" = base ]; then cp /tmp/cpk_base.so capnproto_amd/libcpk_hip.so
   else cp capnproto_amd/var_$v.so capnproto_amd/libcpk_hip.so; fi
   for c in ${CFGS-c2 c4}; do
-    timeout -k 10 300 python bench.py --config $c --sub none --steps ${STEPS:-10} --warmup 2 \
+    timeout -k 10 300 python bench.py --config $c --sub none --steps ${STEPS:-10} --warmup 2 --no-split \
       --no-cpu-baseline > gpurun_out/${TAG}_${v}_$c.json 2> gpurun_out/${TAG}_${v}_$c.err \
       || { echo "bench $v $c failed"; tail -20 gpurun_out/${TAG}_${v}_$c.err; exit 1; }
     python - gpurun_out/${TAG}_${v}_$c.json $v <<'PY'

@@ -15,7 +15,7 @@ for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU S
            "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
   timeout -s KILL 240 rocprofv3 --pmc $set --kernel-trace --output-format csv -d "$R/gpurun_out/${TAG}_p$i" -o run \
-    -- python3 "$R/bench.py" --config $CFG --sub none --steps 2 --warmup 1 --no-cpu-baseline --no-host > "$R/gpurun_out/${TAG}_p$i.log" 2>&1 \
+    -- python3 "$R/bench.py" --config $CFG --sub none --steps 2 --warmup 1 --no-cpu-baseline --no-host --no-split > "$R/gpurun_out/${TAG}_p$i.log" 2>&1 \
     || { echo "pass $i failed"; tail -5 "$R/gpurun_out/${TAG}_p$i.log"; exit 1; }
   echo "pass $i done"
 done

@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 cd /tmp
 for c in ${CFGS:-c2 c4}; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/${TAG}_${c}_prof" -o run \
-    -- python3 "$R/bench.py" --config $c --sub none --steps ${STEPS:-10} --warmup 2 --no-cpu-baseline --no-host \
+    -- python3 "$R/bench.py" --config $c --sub none --steps ${STEPS:-10} --warmup 2 --no-cpu-baseline --no-host --no-split \
     > "$R/gpurun_out/${TAG}_${c}_prof.log" 2>&1 || { echo "rocprof $c failed"; tail -20 "$R/gpurun_out/${TAG}_${c}_prof.log"; exit 1; }
   f=$(find "$R/gpurun_out/${TAG}_${c}_prof" -name '*kernel_stats.csv' | head -1)
   echo "== $c"; python3 - "$f" <<'PY'

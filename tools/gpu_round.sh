@@ -21,7 +21,7 @@ timeout -k 10 300 python bench.py --host-inclusive > gpurun_out/${TAG}_bench_c2.
   || { echo "bench failed"; tail -20 gpurun_out/${TAG}_bench_c2.err; exit 1; }
 cat gpurun_out/${TAG}_bench_c2.json; tail -2 gpurun_out/${TAG}_bench_c2.err
 for c in ${CFGS-c3 c4 c5}; do
-  timeout -k 10 300 python bench.py --config $c --steps 10 --warmup 2 --no-cpu-baseline \
+  timeout -k 10 300 python bench.py --config $c --steps 10 --warmup 2 --no-cpu-baseline --no-split --no-host \
     > gpurun_out/${TAG}_bench_$c.json 2> gpurun_out/${TAG}_bench_$c.err \
     || { echo "bench $c failed"; tail -20 gpurun_out/${TAG}_bench_$c.err; exit 1; }
   cat gpurun_out/${TAG}_bench_$c.json
@@ -33,6 +33,6 @@ cat gpurun_out/${TAG}_stamps.log
 fi
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/${TAG}_prof" -o run \
-  -- python3 "$R/bench.py" --sub none --steps 20 --warmup 3 --no-cpu-baseline --no-host > "$R/gpurun_out/${TAG}_prof.log" 2>&1 \
+  -- python3 "$R/bench.py" --sub none --steps 20 --warmup 3 --no-cpu-baseline --no-host --no-split > "$R/gpurun_out/${TAG}_prof.log" 2>&1 \
   || { echo "rocprof failed"; tail -20 "$R/gpurun_out/${TAG}_prof.log"; exit 1; }
 echo "rocprof done"
