@@ -1,7 +1,7 @@
 #!/bin/bash
 # One gpurun call covering the round-end evidence: parity tests, smoke, the default bench line
-# (C2, with CPU baseline and host-inclusive rate), bench lines for C3-C5, per-phase stamps, and a
-# rocprofv3 kernel-trace summary of the default bench.
+# (C2, with CPU baseline, host-inclusive rate, small-message latency and the stream split), bench
+# lines for C3-C5, and a rocprofv3 kernel-trace summary of the default bench.
 #   gpurun --timeout 1100 -- bash tools/gpu_round.sh TAG
 set -o pipefail
 TAG=${1:-r01}
@@ -26,11 +26,6 @@ for c in ${CFGS-c3 c4 c5}; do
     || { echo "bench $c failed"; tail -20 gpurun_out/${TAG}_bench_$c.err; exit 1; }
   cat gpurun_out/${TAG}_bench_$c.json
 done
-if [ -z "$SKIP_STAMPS" ]; then
-CPK_STAMPS=1 timeout -k 10 120 python tools/stamps.py c2 > gpurun_out/${TAG}_stamps.log 2>&1 \
-  || { echo "stamps failed"; tail -20 gpurun_out/${TAG}_stamps.log; exit 1; }
-cat gpurun_out/${TAG}_stamps.log
-fi
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/${TAG}_prof" -o run \
   -- python3 "$R/bench.py" --sub none --steps 20 --warmup 3 --no-cpu-baseline --no-host --no-split > "$R/gpurun_out/${TAG}_prof.log" 2>&1 \
