@@ -191,33 +191,42 @@ __device__ __forceinline__ uint32_t wait_nonzero32(const uint32_t* p, uint32_t* 
 }
 
 // Blocks past `first_block` of a prologue kernel compute tile_first (TileFirstJob, cpk_kernels.h):
-// binary search of each tile's start in the sorted positions.  True when this block did so.
+// tile t's first position index m with pos[m] >= t*T.  One thread per position index m scatters
+// m to the tiles whose start lies in (pos[m-1], pos[m]] (the intervals partition the tiles; the
+// last index also takes the tiles past the last position) -- no per-tile binary search over the
+// positions, whose 10-20 dependent loads per tile set the time of these launches.  Further
+// blocks zero tf.zero.  True when this block did either job.
 constexpr uint64_t kZeroBlockWords = 4096;  // u64 per zeroing block (256 threads x 16)
 __device__ __forceinline__ bool run_tile_first(const TileFirstJob& tf, uint32_t first_block) {
   if (blockIdx.x < first_block) return false;
-  const uint32_t tfb = (uint32_t)((tf.ntiles + 255) / 256);
+  const uint32_t tfb = tf.ntiles ? (uint32_t)((tf.npos + 1 + 255) / 256) : 0u;
   if (blockIdx.x - first_block >= tfb) {
     const uint64_t z0 = (uint64_t)(blockIdx.x - first_block - tfb) * kZeroBlockWords;
     for (uint64_t i = z0 + threadIdx.x; i < z0 + kZeroBlockWords && i < tf.zero_words; i += 256)
       tf.zero[i] = 0;
     return true;
   }
-  const uint64_t t = (uint64_t)(blockIdx.x - first_block) * blockDim.x + threadIdx.x;
-  if (t < tf.ntiles) {
-    const uint64_t key = t * tf.T;
-    uint64_t lo = 0, hi = tf.npos + 1;
-    while (lo < hi) {
-      const uint64_t mid = (lo + hi) >> 1;
-      if (tf.pos[mid] < key) lo = mid + 1;
-      else hi = mid;
+  const uint64_t m = (uint64_t)(blockIdx.x - first_block) * blockDim.x + threadIdx.x;
+  if (m > tf.npos) return true;
+  const uint64_t pm = tf.pos[m];
+  const uint64_t lo = m == 0 ? 0 : tf.pos[m - 1] / tf.T + 1;  // first tile starting past pos[m-1]
+  uint64_t hi = pm / tf.T;                                     // last tile starting at or before pos[m]
+  if (hi >= tf.ntiles) hi = tf.ntiles - 1;
+  for (uint64_t t = lo; t <= hi && lo <= hi; t++) {
+    tf.out[t] = m;
+    if (tf.outpos) tf.outpos[t] = pm;
+  }
+  if (m == tf.npos) {
+    // tiles starting past the last position: none of them has a first position
+    for (uint64_t t = (pm / tf.T) + 1; t < tf.ntiles; t++) {
+      tf.out[t] = tf.npos + 1;
+      if (tf.outpos) tf.outpos[t] = ~0ull;
     }
-    tf.out[t] = lo;
-    if (tf.outpos) tf.outpos[t] = lo <= tf.npos ? tf.pos[lo] : ~0ull;
   }
   return true;
 }
 inline unsigned tile_first_blocks(const TileFirstJob& tf) {
-  return (unsigned)((tf.ntiles + 255) / 256 +
+  return (unsigned)((tf.ntiles ? (tf.npos + 1 + 255) / 256 : 0) +
                     (tf.zero ? (tf.zero_words + kZeroBlockWords - 1) / kZeroBlockWords : 0));
 }
 

@@ -95,7 +95,32 @@ __global__ void header_kernel(const uint8_t* __restrict__ packed,
   uint64_t p = in_off[m];
   const uint64_t end = in_off[m + 1];
   uint64_t first = 0;
-  int32_t st = decode_exact(packed, p, end, 1, [&](uint64_t, uint64_t w) { first = w; });
+  int32_t st;
+  if (end - p >= 16) {
+    // the first word's record (<= 10 bytes) from one 16-byte read: decode_exact's steps for
+    // one word, with every byte present (a run record's count must be 0 -- it may not cross
+    // word 1 -- so its raw bytes are never needed)
+    uint64_t v0, v1;
+    __builtin_memcpy(&v0, packed + p, 8);
+    __builtin_memcpy(&v1, packed + p + 8, 8);
+    auto byte_at = [&](uint32_t k) -> uint32_t {
+      return (uint32_t)((k < 8 ? v0 >> (8 * k) : v1 >> (8 * (k - 8))) & 0xff);
+    };
+    const uint32_t tag = (uint32_t)(v0 & 0xff);
+    uint32_t k = 1;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      if ((tag >> i) & 1) first |= (uint64_t)byte_at(k++) << (8 * i);
+    }
+    st = kOK;
+    if (tag == 0 || tag == 0xff) {
+      if (byte_at(k) > 0) st = kOvershoot;
+      k++;
+    }
+    p += k;
+  } else {
+    st = decode_exact(packed, p, end, 1, [&](uint64_t, uint64_t w) { first = w; });
+  }
   uint64_t words = 0;
   if (st == kOK) {
     const uint32_t segm1 = (uint32_t)first;
@@ -1205,13 +1230,13 @@ __device__ __forceinline__ void expand_records(const UnpackArgs& a, uint64_t A, 
       }
       const uint64_t pabs = A + p;
       if (special) {
+        const int64_t m = win.mw + wl;
         MsgInfo mi;
         mi.base = mbase;
         mi.total = mtotal;
         mi.end = mend;
         mi.ok = true;
         mi.fits = true;
-        const int64_t m = win.mw + wl;
         const int32_t st = handle_record(a, d, p, pabs, wb, mi, &job, word);
         if (st >= 0) {
           a.status[m] = st;

@@ -1,4 +1,3 @@
 cd $GRAFT_REPO_ROOT
-for c in c2 c3 c4; do bash tools/gpu_pmc3.sh r03_$c $c > gpurun_out/r03_pmc_$c.log 2>&1 || { echo "pmc $c failed"; tail -5 gpurun_out/r03_pmc_$c.log; exit 1; }; done
-echo pmc done
-CFGS="c2 c3 c4" bash tools/gpu_prof.sh r03p
+timeout -k 10 400 python -u -m pytest tests -m gpu -q -x --timeout 150 --timeout-method thread -p no:cacheprovider > gpurun_out/f19_tests.log 2>&1; tail -2 gpurun_out/f19_tests.log; grep -E "^FAILED" gpurun_out/f19_tests.log | head -5
+TESTS=none CFGS="c2 c3 c5" bash tools/gpu_check.sh f19
