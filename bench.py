@@ -508,10 +508,12 @@ def main():
     if world == 1 and not args.no_host:
         # the path starts and ends in host memory: serial and pipelined host-inclusive rates
         words, off, packed, moff, total, cap = head["tensors"]
-        extra = [capnproto_amd.Codec(local) for _ in range(3)]
+        # two streams, 16 chunks: the best of tools/pcie_probe.py's sweep (the box's PCIe moves
+        # about 57 GB/s one way and not much more both ways at once: profiles/r03_pcie_probe.txt)
+        extra = [capnproto_amd.Codec(local)]
         hi = {"pipelined": host_inclusive_pipelined([codec] + extra, words, off, total,
                                                     head["n"], moff, min(args.steps, 10),
-                                                    chunks=24)}
+                                                    chunks=16)}
         for c in extra:
             c.close()
         if args.host_inclusive:
