@@ -191,19 +191,46 @@ __device__ __forceinline__ uint32_t wait_nonzero32(const uint32_t* p, uint32_t* 
 }
 
 // Blocks past `first_block` of a prologue kernel compute tile_first (TileFirstJob, cpk_kernels.h):
-// tile t's first position index m with pos[m] >= t*T.  One thread per position index m scatters
-// m to the tiles whose start lies in (pos[m-1], pos[m]] (the intervals partition the tiles; the
-// last index also takes the tiles past the last position) -- no per-tile binary search over the
-// positions, whose 10-20 dependent loads per tile set the time of these launches.  Further
-// blocks zero tf.zero.  True when this block did either job.
+// tile t's first position index m with pos[m] >= t*T.  With about as many positions as tiles,
+// one thread per position index m scatters m to the tiles whose start lies in (pos[m-1], pos[m]]
+// (the intervals partition the tiles; the last index also takes the tiles past the last
+// position) -- no per-tile binary search, whose 10-20 dependent loads per tile would set the
+// time of the launch.  With many tiles per position (large messages: a serial scatter of
+// thousands of tiles per thread) one thread per tile searches the few positions instead.
+// Further blocks zero tf.zero.  True when this block did either job.
 constexpr uint64_t kZeroBlockWords = 4096;  // u64 per zeroing block (256 threads x 16)
+__host__ __device__ inline bool tile_first_search(const TileFirstJob& tf) {
+  return tf.ntiles > 16 * (tf.npos + 1);
+}
+__host__ __device__ inline uint64_t tile_first_threads(const TileFirstJob& tf) {
+  return !tf.ntiles ? 0 : (tile_first_search(tf) ? tf.ntiles : tf.npos + 1);
+}
 __device__ __forceinline__ bool run_tile_first(const TileFirstJob& tf, uint32_t first_block) {
   if (blockIdx.x < first_block) return false;
-  const uint32_t tfb = tf.ntiles ? (uint32_t)((tf.npos + 1 + 255) / 256) : 0u;
+  const uint32_t tfb = (uint32_t)((tile_first_threads(tf) + 255) / 256);
   if (blockIdx.x - first_block >= tfb) {
     const uint64_t z0 = (uint64_t)(blockIdx.x - first_block - tfb) * kZeroBlockWords;
     for (uint64_t i = z0 + threadIdx.x; i < z0 + kZeroBlockWords && i < tf.zero_words; i += 256)
       tf.zero[i] = 0;
+    return true;
+  }
+  if (tile_first_search(tf)) {
+    const uint64_t t = (uint64_t)(blockIdx.x - first_block) * blockDim.x + threadIdx.x;
+    if (t >= tf.ntiles) return true;
+    // first m in [0, npos] with pos[m] >= t*T (npos + 1: none)
+    const uint64_t x = t * tf.T;
+    uint64_t lo = 0, n = tf.npos + 1;
+    while (n > 0) {
+      const uint64_t h = n >> 1;
+      if (tf.pos[lo + h] < x) {
+        lo += h + 1;
+        n -= h + 1;
+      } else {
+        n = h;
+      }
+    }
+    tf.out[t] = lo;
+    if (tf.outpos) tf.outpos[t] = lo <= tf.npos ? tf.pos[lo] : ~0ull;
     return true;
   }
   const uint64_t m = (uint64_t)(blockIdx.x - first_block) * blockDim.x + threadIdx.x;
@@ -226,7 +253,7 @@ __device__ __forceinline__ bool run_tile_first(const TileFirstJob& tf, uint32_t 
   return true;
 }
 inline unsigned tile_first_blocks(const TileFirstJob& tf) {
-  return (unsigned)((tf.ntiles ? (tf.npos + 1 + 255) / 256 : 0) +
+  return (unsigned)((tile_first_threads(tf) + 255) / 256 +
                     (tf.zero ? (tf.zero_words + kZeroBlockWords - 1) / kZeroBlockWords : 0));
 }
 
