@@ -90,10 +90,12 @@ def parse():
 
 
 def kernel_source_hash() -> str:
-    """Content hash of the device code (pins a committed PMC traffic file to these kernels)."""
+    """Content hash of the device code and of the host code that sequences its launches, carves
+    its scratch and zeroes it (pins a committed PMC traffic file to what it measured)."""
     h = hashlib.sha256()
     for p in sorted(glob.glob(os.path.join(ROOT, "capnproto_amd", "csrc", "*.hip")) +
-                    glob.glob(os.path.join(ROOT, "capnproto_amd", "csrc", "*.h"))):
+                    glob.glob(os.path.join(ROOT, "capnproto_amd", "csrc", "*.h")) +
+                    glob.glob(os.path.join(ROOT, "capnproto_amd", "csrc", "*.cpp"))):
         h.update(os.path.basename(p).encode())
         h.update(open(p, "rb").read())
     return h.hexdigest()
@@ -490,6 +492,12 @@ def main():
     copy_gbps = measure_copy(torch, codec.device)
     head = run_config(args.config, args, args.steps, args.warmup, rank, world, dist, codec)
     ok = head["ok_all"]
+    exchange = None
+    if world > 1:
+        try:
+            exchange = batch_exchange(codec, head, args, rank, world, dist)
+        except Exception as e:  # noqa: BLE001 -- reported, never fatal to the timed result
+            exchange = {"error": f"{type(e).__name__}: {e}"}
 
     cb = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -567,6 +575,8 @@ def main():
                 result["sub_results"].append(sr)
         if hi is not None:
             result["host_inclusive"] = hi
+        if exchange is not None:
+            result["batch_exchange"] = exchange
         if not args.no_host:
             result["small_message_latency"] = small_message_latency(codec)
         if not args.no_split and world == 1:
@@ -575,6 +585,60 @@ def main():
     codec.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def batch_exchange(codec, head, args, rank, world, dist, reps=3):
+    """The batch case at N > 1: every rank's packed bytes gathered onto rank 0
+    at their global offsets (capnproto_amd.shard.gather_packed: an all-gather of per-rank totals,
+    then RCCL send/recv over xGMI into slices of rank 0's buffer), outside the timed step.
+    Timed on every rank between barriers; rank 0 then unpacks the gathered stream with the
+    global offsets and, for contiguous shards, checks it against the global batch regenerated on
+    the device.  Reported as its own number, never folded into `value`."""
+    import torch
+
+    from capnproto_amd.shard import gather_packed
+
+    words, off, packed, moff, total, cap = head["tensors"]
+    n = head["n"]
+    times = []
+    out = offs = None
+    for _ in range(reps):
+        out = offs = None
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        out, offs = gather_packed(packed, moff, n, dst=0, dist=dist, device=codec.device)
+        torch.cuda.synchronize()
+        dist.barrier()
+        times.append(time.perf_counter() - t0)
+    t = min(times)
+    if rank != 0:
+        return None
+    G = int(offs[-1].item())
+    res = {"to_rank": 0, "ranks": world, "packed_bytes": G, "ms": round(1e3 * t, 3),
+           "GBps": round(G / t / 1e9, 2),
+           "what": "all ranks' packed bytes + message offsets gathered onto rank 0 at their "
+                   "global offsets (all-gather of totals, then RCCL send/recv)"}
+    cfg = CONFIGS[args.config]
+    nglob = int(offs.numel()) - 1
+    if G > (24 << 30):
+        res["verified"] = "skipped (gathered stream too large to re-decode beside the batch)"
+        return res
+    U = head["U_all"]
+    back, woff, ust = codec.unpack_messages(out, offs, int(U) // 8, nbytes=G)
+    codec.sync()
+    ok = bool((ust == 0).all().item()) and int(woff[-1].item()) * 8 == int(U)
+    mode = args.shard or cfg.get("shard", "block")
+    if ok and mode != "round_robin":
+        goff, gtot = codec.gen_offsets(nglob, nseg=cfg["nseg"], seg_words=cfg["seg_words"],
+                                       seed=args.seed)
+        gw = codec.gen_messages(cfg["profile"], goff, gtot, nseg=cfg["nseg"], seed=args.seed)
+        ok = torch.equal(woff, goff) and torch.equal(back[:gtot], gw[:gtot])
+        del gw, goff
+    res["round_trip_exact"] = ok
+    del back, out
+    torch.cuda.empty_cache()
+    return res
 
 
 def split_bench(codec, seed, n=1 << 20, reps=5):

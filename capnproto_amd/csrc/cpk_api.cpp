@@ -125,9 +125,12 @@ struct TimedLaunch {
 // capture the previous stream's work is outside the graph: captured sequences use one stream.)
 cpk_status order_streams(cpk_ctx* ctx, hipStream_t s) {
   if (ctx->used && s != ctx->last_stream) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    // an event recorded on (or waited for by) a capturing stream would join the other stream to
+    // the graph or invalidate the capture: skip the ordering when either stream is capturing
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone, cl = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(s, &cs) != hipSuccess) return CPK_ERR_HIP;
-    if (cs == hipStreamCaptureStatusNone) {
+    if (hipStreamIsCapturing(ctx->last_stream, &cl) != hipSuccess) cl = hipStreamCaptureStatusNone;
+    if (cs == hipStreamCaptureStatusNone && cl == hipStreamCaptureStatusNone) {
       if (!ctx->order_ev &&
           hipEventCreateWithFlags(&ctx->order_ev, hipEventDisableTiming) != hipSuccess)
         return CPK_ERR_HIP;

@@ -3,7 +3,11 @@
 The path shards by message: every message is packed / unpacked independently (a packed message
 never refers to another), so N ranks -- one process per GPU -- each own a disjoint set of
 messages and there is no exchange on the data path.  The only collectives are the bench's
-timing / byte-count reductions (``reduce_step``), which run once per measurement, not per step.
+timing / byte-count reductions (``reduce_step``), which run once per measurement, not per step,
+and -- for the batch case, where the outputs must land on one GPU --
+``gather_packed``: one all-gather of per-rank totals, then every rank's packed bytes sent point to
+point (RCCL send/recv over xGMI under the "nccl" backend) straight into their global offset in the
+destination rank's buffer.
 
 Two assignments of a global batch of ``n_global`` messages to ``world`` ranks:
   * ``block``       rank r owns messages [r*n_local, (r+1)*n_local)   (configs C2-C4)
@@ -64,6 +68,67 @@ def global_offsets(local_packed_total: int, dist=None, device=None):
     vals = [int(p.item()) for p in parts]
     r = dist.get_rank()
     return sum(vals[:r]), sum(vals)
+
+
+def gather_packed(packed, msg_out_off, nmsgs: int, dst: int = 0, dist=None, device=None):
+    """The batch case of SURVEY.md 8(e): every rank's packed messages land on rank ``dst`` as ONE
+    packed stream, rank r's bytes at the sum of the packed totals of ranks < r (the offsets
+    ``global_offsets`` computes), with the global per-message offsets.
+
+    packed: u8 tensor holding this rank's packed batch (at least P bytes); msg_out_off: its
+    nmsgs + 1 int64 byte offsets (``Codec.pack_messages``).  One all-gather of (P, nmsgs) per
+    rank, then point-to-point sends of the bytes and the offsets, received in place -- into
+    slices of the destination's output at their global positions, so nothing is copied after the
+    receive but the rebasing of the received offsets.  With block or byte-balanced shards
+    (contiguous message ranges) the result is the packed stream of the global batch in message
+    order, i.e. what a single rank packing every message writes.
+
+    Returns (stream, offsets) on ``dst`` -- the u8 stream of the global total and the
+    N_global + 1 int64 message offsets -- and (None, None) on the other ranks."""
+    import torch
+
+    P = int(msg_out_off[nmsgs].item())
+    if dist is None:
+        return packed[:P], msg_out_off[: nmsgs + 1]
+    world, rank = dist.get_world_size(), dist.get_rank()
+    meta = torch.tensor([P, nmsgs], dtype=torch.int64, device=device)
+    parts = [torch.zeros_like(meta) for _ in range(world)]
+    dist.all_gather(parts, meta)
+    sizes = [int(p[0].item()) for p in parts]
+    counts = [int(p[1].item()) for p in parts]
+    bases = [sum(sizes[:r]) for r in range(world)]
+    mbase = [sum(counts[:r]) for r in range(world)]
+    if rank != dst:
+        ops = []
+        if P:
+            ops.append(dist.P2POp(dist.isend, packed[:P].contiguous(), dst))
+        if nmsgs:
+            ops.append(dist.P2POp(dist.isend, msg_out_off[:nmsgs].contiguous(), dst))
+        if ops:
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
+        return None, None
+    total, ntotal = sum(sizes), sum(counts)
+    out = torch.empty(total, dtype=torch.uint8, device=packed.device)
+    offs = torch.empty(ntotal + 1, dtype=torch.int64, device=packed.device)
+    ops = []
+    for r in range(world):
+        if r == dst:
+            continue
+        if sizes[r]:
+            ops.append(dist.P2POp(dist.irecv, out[bases[r]:bases[r] + sizes[r]], r))
+        if counts[r]:
+            ops.append(dist.P2POp(dist.irecv, offs[mbase[r]:mbase[r] + counts[r]], r))
+    reqs = dist.batch_isend_irecv(ops) if ops else []
+    out[bases[dst]:bases[dst] + P].copy_(packed[:P])
+    offs[mbase[dst]:mbase[dst] + nmsgs].copy_(msg_out_off[:nmsgs])
+    for req in reqs:
+        req.wait()
+    for r in range(world):  # rank-local offsets -> global
+        if counts[r] and bases[r]:
+            offs[mbase[r]:mbase[r] + counts[r]] += bases[r]
+    offs[ntotal] = total
+    return out, offs
 
 
 def reduce_step(dt_s: float, unpacked: float, packed: float, pack_ms: float, unpack_ms: float,

@@ -9,8 +9,10 @@
 //
 //   tryReadMessage  reads from the stream into a byte buffer, asks the device for one message
 //                   (cpk_read_packed_message_host); CPK_ERR_PREMATURE_EOF means "read more and
-//                   retry" and the next stream read is at least as large as what is buffered, so
-//                   a message costs O(log size) device attempts.  Bytes past the message stay
+//                   retry".  A stream read may return any amount, so after a failed attempt the
+//                   next one waits until the buffered bytes have doubled (or the stream ends):
+//                   a message costs O(log size) device attempts and O(size) bytes uploaded in
+//                   all, however the socket fragments it.  Bytes past the message stay
 //                   buffered for the next call (back-to-back messages, one stream read).  A clean
 //                   end before the first byte is kj::none; an end inside a message is
 //                   DISCONNECTED "Premature EOF." (serialize-async.c++:92, :525).  The flat
@@ -19,7 +21,8 @@
 //   writeMessage    one device pack (the façade's writePackedMessage), one stream write.
 //   writeMessages   the whole batch gathered flat and packed in ONE device call
 //                   (cpk_pack_messages_host), one stream write.
-//   getSendBufferSize / end   as AsyncIoMessageStream (serialize-async.c++:457-486).
+//   getSendBufferSize  the reference's AsyncIoMessageStream answer for the same stream
+//                   (serialize-async.c++:457-486); end  shutdownWrite, as it does.
 // File descriptors attached to messages are not carried (no part of the packed path): a write
 // with fds is refused, reads return no fds.
 #pragma once
@@ -126,17 +129,9 @@ class PackedMessageStream final : public capnp::MessageStream {
   }
 
   kj::Maybe<int> getSendBufferSize() override {
-    // serialize-async.c++:457-477: SO_SNDBUF when the stream is a socket, else none.
-    int bufSize = 0;
-    KJ_IF_SOME(e, kj::runCatchingExceptions([&]() {
-                 uint len = sizeof(int);
-                 stream_.getsockopt(SOL_SOCKET, SO_SNDBUF, &bufSize, &len);
-                 KJ_ASSERT(len == sizeof(bufSize)) { break; }
-               })) {
-      (void)e;
-      return kj::none;
-    }
-    return bufSize;
+    // the reference's own answer for this stream (SO_SNDBUF on a socket, none otherwise):
+    // AsyncIoMessageStream::getSendBufferSize, serialize-async.c++:484-486
+    return capnp::AsyncIoMessageStream(stream_).getSendBufferSize();
   }
 
   kj::Promise<void> end() override {
@@ -191,10 +186,13 @@ class PackedMessageStream final : public capnp::MessageStream {
 
   kj::Promise<kj::Maybe<capnp::MessageReaderAndFds>> readLoop(capnp::ReaderOptions options,
                                                                kj::ArrayPtr<capnp::word> scratch) {
-    if (end_ > begin_) {
+    if (end_ > begin_ && end_ - begin_ >= retryAt_) {
       KJ_IF_SOME(r, tryDecode(options, scratch)) {
+        retryAt_ = failedAt_ = 0;
         return kj::Maybe<capnp::MessageReaderAndFds>(capnp::MessageReaderAndFds{kj::mv(r), nullptr});
       }
+      failedAt_ = end_ - begin_;
+      retryAt_ = 2 * failedAt_;  // next attempt once the buffered bytes have doubled
     }
     // Need more input: compact, then read at least as much as is already buffered.
     if (begin_ > 0) {
@@ -208,6 +206,14 @@ class PackedMessageStream final : public capnp::MessageStream {
         .then([this, options, scratch](size_t n) mutable -> kj::Promise<kj::Maybe<capnp::MessageReaderAndFds>> {
           if (n == 0) {
             if (end_ == begin_) return kj::Maybe<capnp::MessageReaderAndFds>(kj::none);
+            if (end_ - begin_ != failedAt_) {
+              // the stream ended before the buffer doubled: one last attempt at what there is
+              KJ_IF_SOME(r, tryDecode(options, scratch)) {
+                retryAt_ = failedAt_ = 0;
+                return kj::Maybe<capnp::MessageReaderAndFds>(
+                    capnp::MessageReaderAndFds{kj::mv(r), nullptr});
+              }
+            }
             kj::throwRecoverableException(KJ_EXCEPTION(DISCONNECTED, "Premature EOF."));
             return kj::Maybe<capnp::MessageReaderAndFds>(kj::none);
           }
@@ -220,6 +226,8 @@ class PackedMessageStream final : public capnp::MessageStream {
   size_t readSize_;
   std::vector<uint8_t> buf_;
   size_t begin_ = 0, end_ = 0;
+  size_t retryAt_ = 0;   // buffered bytes needed before the next device attempt
+  size_t failedAt_ = 0;  // buffered bytes at the last failed attempt
 };
 
 }  // namespace cpk_kj

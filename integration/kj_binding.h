@@ -6,7 +6,10 @@
 //
 //   capnp::writePackedMessage(out, builder)      -> cpk_kj::writePackedMessage(out, builder)
 //   capnp::writePackedMessageToFd(fd, builder)   -> cpk_kj::writePackedMessageToFd(fd, builder)
+//   (both for kj::BufferedOutputStream and for an unbuffered kj::OutputStream)
 //   capnp::PackedMessageReader reader(in, opts)  -> cpk_kj::PackedMessageReader reader(in, opts)
+//   capnp::PackedFdMessageReader message(fd)     -> cpk_kj::PackedFdMessageReader message(fd)
+//   (fd as int, borrowed, or as kj::OwnFd, owned)
 //   capnp::computeUnpackedSizeInWords(bytes)     -> cpk_kj::computeUnpackedSizeInWords(bytes)
 //
 // cpk_kj::PackedMessageReader IS a capnp::MessageReader, so getRoot<T>() works unchanged.
@@ -117,6 +120,37 @@ inline void writePackedMessage(kj::BufferedOutputStream& output,
 inline void writePackedMessage(kj::BufferedOutputStream& output, capnp::MessageBuilder& builder) {
   writePackedMessage(output, builder.getSegmentsForOutput());
 }
+// serialize-packed.h:94-98, :118-120 (serialize-packed.c++:466-475): an unbuffered kj stream.  The
+// reference packs straight into a kj::BufferedOutputStream when the stream is one, else through
+// an 8 KiB buffer; here the façade's OutputStream overload does the buffering (one device call
+// per message, then one write() of the packed bytes).
+class KjPlainOut final : public cpk_capnp::OutputStream {
+ public:
+  explicit KjPlainOut(kj::OutputStream& k) : k_(k) {}
+  void write(const void* p, size_t n) override {
+    k_.write(kj::arrayPtr(static_cast<const kj::byte*>(p), n));
+  }
+  using cpk_capnp::OutputStream::write;
+
+ private:
+  kj::OutputStream& k_;
+};
+inline void writePackedMessage(kj::OutputStream& output,
+                               kj::ArrayPtr<const kj::ArrayPtr<const capnp::word>> segments) {
+  KJ_IF_SOME(buffered, kj::dynamicDowncastIfAvailable<kj::BufferedOutputStream>(output)) {
+    writePackedMessage(buffered, segments);
+  } else {
+    auto v = segments_of(segments);
+    KjPlainOut out(output);
+    cpk_capnp::writePackedMessage(
+        out, cpk_capnp::ArrayPtr<const cpk_capnp::ArrayPtr<const cpk_capnp::word>>(v.data(),
+                                                                                   v.size()));
+  }
+}
+inline void writePackedMessage(kj::OutputStream& output, capnp::MessageBuilder& builder) {
+  writePackedMessage(output, builder.getSegmentsForOutput());
+}
+
 inline void writePackedMessageToFd(int fd,
                                    kj::ArrayPtr<const kj::ArrayPtr<const capnp::word>> segments) {
   auto v = segments_of(segments);
@@ -130,7 +164,7 @@ inline void writePackedMessageToFd(int fd, capnp::MessageBuilder& builder) {
 
 // serialize-packed.h:65-71 as a capnp::MessageReader: segments are read (lazily, as the
 // reference does) by the façade reader; getRoot<T>() and the rest come from MessageReader.
-class PackedMessageReader final : public capnp::MessageReader {
+class PackedMessageReader : public capnp::MessageReader {
  public:
   PackedMessageReader(kj::BufferedInputStream& in,
                       capnp::ReaderOptions options = capnp::ReaderOptions(),
@@ -154,6 +188,30 @@ class PackedMessageReader final : public capnp::MessageReader {
   }
   KjIn in_;
   cpk_capnp::PackedMessageReader reader_;
+};
+
+namespace _ {
+// The descriptor side of PackedFdMessageReader: kj::FdInputStream (owning the fd or not) and the
+// reference's own BufferedInputStreamWrapper over it, constructed before the reader that reads
+// through them (serialize-packed.c++:444-456).
+struct FdInput {
+  kj::FdInputStream fdIn;
+  kj::BufferedInputStreamWrapper buffered;
+  explicit FdInput(int fd) : fdIn(fd), buffered(fdIn) {}
+  explicit FdInput(kj::OwnFd fd) : fdIn(kj::mv(fd)), buffered(fdIn) {}
+};
+}  // namespace _
+
+// serialize-packed.h:73-89: read a packed message from a file descriptor, borrowing it (int) or
+// owning it (kj::OwnFd), as samples/addressbook.c++:79 does (`PackedFdMessageReader message(fd)`).
+class PackedFdMessageReader final : private _::FdInput, public PackedMessageReader {
+ public:
+  PackedFdMessageReader(int fd, capnp::ReaderOptions options = capnp::ReaderOptions(),
+                        kj::ArrayPtr<capnp::word> scratch = nullptr)
+      : _::FdInput(fd), PackedMessageReader(buffered, options, scratch) {}
+  PackedFdMessageReader(kj::OwnFd fd, capnp::ReaderOptions options = capnp::ReaderOptions(),
+                        kj::ArrayPtr<capnp::word> scratch = nullptr)
+      : _::FdInput(kj::mv(fd)), PackedMessageReader(buffered, options, scratch) {}
 };
 
 // serialize-packed.h:107

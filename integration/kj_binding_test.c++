@@ -10,6 +10,8 @@
 //   2. writePackedMessage / PackedMessageReader over the reference's fixtures (testdata/binary ->
 //      packed, segmented -> segmented-packed), segments compared with capnp::FlatArrayMessageReader;
 //   3. the addressbook flow of samples/addressbook.c++:47-79: writePackedMessageToFd into a pipe,
+//      PackedFdMessageReader message(fd) (borrowed int fd, then an owned kj::OwnFd after a
+//      MallocMessageBuilder write), writePackedMessage over an unbuffered kj::OutputStream,
 //      PackedMessageReader over kj::FdInputStream, getRoot<AnyPointer>() walked to the two people
 //      the sample writes (ids 123 / 456, names, emails, phone counts).
 //
@@ -208,11 +210,9 @@ void addressbook(const std::string& dir) {
   check(pipe(fds) == 0, "pipe 2");
   check(::write(fds[1], packed.data(), packed.size()) == (ssize_t)packed.size(), "pipe write");
   close(fds[1]);
-  kj::FdInputStream fin(fds[0]);
-  kj::BufferedInputStreamWrapper bin(fin);
   {
-    cpk_kj::PackedMessageReader message(bin);
-    check_same_segments(message, f, "addressbook: PackedMessageReader");
+    cpk_kj::PackedFdMessageReader message(fds[0]);
+    check_same_segments(message, f, "addressbook: PackedFdMessageReader");
     auto book = message.getRoot<capnp::AnyPointer>().getAs<capnp::AnyStruct>();
     auto people = book.getPointerSection()[0].getAs<capnp::AnyList>().as<capnp::List<capnp::AnyStruct>>();
     check(people.size() == 2, "addressbook: two people");
@@ -234,6 +234,49 @@ void addressbook(const std::string& dir) {
     }
   }
   close(fds[0]);
+  // the sample's shape with a MessageBuilder (samples/addressbook.c++:47-79): the message built
+  // in a capnp::MallocMessageBuilder (a copy of the fixture's root), writePackedMessageToFd(fd,
+  // builder), then PackedFdMessageReader over an owned descriptor (kj::OwnFd)
+  capnp::MallocMessageBuilder builder;
+  builder.setRoot(f.reader->getRoot<capnp::AnyPointer>());
+  auto bsegs = builder.getSegmentsForOutput();
+  check(pipe(fds) == 0, "pipe 3");
+  cpk_kj::writePackedMessageToFd(fds[1], builder);
+  close(fds[1]);
+  {
+    cpk_kj::PackedFdMessageReader message{kj::OwnFd(fds[0])};
+    for (uint i = 0; i < bsegs.size(); i++) {
+      auto s = message.getSegment(i);
+      check(s.size() == bsegs[i].size() &&
+                memcmp(s.begin(), bsegs[i].begin(), s.size() * sizeof(capnp::word)) == 0,
+            "addressbook: builder -> fd -> PackedFdMessageReader(OwnFd) segment");
+    }
+    auto people = message.getRoot<capnp::AnyPointer>().getAs<capnp::AnyStruct>()
+                      .getPointerSection()[0].getAs<capnp::AnyList>();
+    check(people.size() == 2, "addressbook: builder round trip, two people");
+  }
+  // writePackedMessage over an unbuffered kj::OutputStream (serialize-packed.h:94-98): same bytes
+  // as the buffered path
+  {
+    kj::VectorOutputStream vec;
+    class Unbuffered final : public kj::OutputStream {
+     public:
+      explicit Unbuffered(kj::VectorOutputStream& v) : v_(v) {}
+      void write(kj::ArrayPtr<const kj::byte> data) override { v_.write(data); }
+     private:
+      kj::VectorOutputStream& v_;
+    } plain(vec);
+    cpk_kj::writePackedMessage(static_cast<kj::OutputStream&>(plain), f.pieces());
+    auto got = vec.getArray();
+    check(got.size() == packed.size() && memcmp(got.begin(), packed.data(), packed.size()) == 0,
+          "addressbook: writePackedMessage(kj::OutputStream&) bytes == the sample's");
+    kj::VectorOutputStream vec2;
+    cpk_kj::writePackedMessage(static_cast<kj::OutputStream&>(vec2), builder);
+    kj::ArrayInputStream in(vec2.getArray());
+    cpk_kj::PackedMessageReader r(in);
+    check(r.getSegment(0).size() == bsegs[0].size(),
+          "addressbook: writePackedMessage(kj::OutputStream& buffered, builder)");
+  }
 }
 
 }  // namespace

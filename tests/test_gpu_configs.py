@@ -106,8 +106,12 @@ def run_config(codec, name, prefix=False, limit=None):
     return words, back, woff, ust, off, total
 
 
+C5_SHARDS = [f"c5r{r}of8" for r in range(8)]  # the 8-GPU round-robin shards of C5
+
+
 @pytest.mark.parametrize("name,prefix", [("c2", False), ("c3", True), ("c3", False),
-                                         ("c4", True), ("c5", True), ("c5r0of8", True)])
+                                         ("c4", True), ("c5", True)] +
+                         [(s, True) for s in C5_SHARDS])
 def test_config_pack_matches_reference_and_round_trips(codec, name, prefix):
     words, back, woff, ust, off, total = run_config(codec, name, prefix)
     assert int((ust != 0).sum().item()) == 0
@@ -118,10 +122,11 @@ def test_config_pack_matches_reference_and_round_trips(codec, name, prefix):
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("name", ["c4", "c5", "c5r0of8"])
+@pytest.mark.parametrize("name", ["c4", "c5"] + C5_SHARDS)
 def test_config_full_size(codec, name):
-    """Full C4 (256 x 64 MiB at exactly the 8 Mi-word traversal limit, 16 GiB) and the full C5
-    shards (4 Mi mixed messages, about 14 GiB)."""
+    """Full C4 (256 x 64 MiB at exactly the 8 Mi-word traversal limit, 16 GiB), full C5 (its
+    first 4 Mi messages) and every one of the eight round-robin shards of the 8-GPU C5 run (4 Mi
+    mixed messages each, about 14 GiB): packed bytes hashed against the reference's."""
     import torch
 
     words, back, woff, ust, off, total = run_config(codec, name)

@@ -266,3 +266,33 @@ def test_concurrent_contexts_two_streams(codec):
             assert torch.equal(back[:total], words[:total]) and torch.equal(wo, off)
     finally:
         other.close()
+
+
+def test_captured_then_eager_calls(codec):
+    """A context whose previous call was captured into a HIP graph (on torch's capture stream)
+    and whose next call comes eagerly on another stream: the cross-stream ordering event is
+    skipped for a capturing stream, so neither the capture nor the eager call fails, and both
+    give the sequential result (cpk_api.cpp order_streams)."""
+    import torch
+
+    off, total = codec.gen_offsets(64, seed=11)
+    words = codec.gen_messages("mixed", off, total, seed=11)
+    ref, rmoff, _ = codec.pack_messages(words, off)
+    codec.sync()
+    P = int(rmoff[-1].item())
+    packed = torch.empty_like(ref)
+    moff = torch.empty_like(rmoff)
+    st = torch.empty(64, dtype=torch.int32, device=codec.device)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        codec.pack_messages(words, off, out=packed, msg_out_off=moff, status=st)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        back, wo, ust = codec.unpack_messages(ref, rmoff, total, nbytes=P, stream=s)
+    s.synchronize()
+    codec.sync(s)
+    g.replay()
+    torch.cuda.synchronize()
+    codec.sync()
+    assert torch.equal(packed[:P], ref[:P]) and torch.equal(moff, rmoff) and (st == 0).all()
+    assert torch.equal(back[:total], words[:total]) and (ust == 0).all()

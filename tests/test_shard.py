@@ -112,3 +112,57 @@ def test_balanced_ranges(world):
     assert [f for f, _ in parts] == list(np.cumsum([0] + [c for _, c in parts])[:-1])
     loads = [int(off[f + c] - off[f]) for f, c in parts]
     assert max(loads) - min(loads) <= 2 * int(sizes.max())
+
+
+def _gather_worker(rank, world, port, dst, q):
+    import torch
+    import torch.distributed as dist
+
+    from capnproto_amd.shard import gather_packed
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import pyoracle
+
+        msgs = _global_batch()
+        first, stride, count = shard_messages(rank, world, len(msgs), "block")
+        mine = msgs[first:first + count]
+        off = np.cumsum([0] + [len(m) for m in mine]).astype(np.uint64)
+        packed, poff, st = pyoracle.Oracle().pack_batch(
+            np.concatenate(mine) if count else np.zeros(0, np.uint64), off)
+        # the device buffer shape of Codec.pack_messages: capacity past P, int64 offsets
+        buf = torch.zeros(int(poff[-1]) + 64, dtype=torch.uint8)
+        buf[: int(poff[-1])] = torch.from_numpy(np.asarray(packed[: int(poff[-1])]).copy())
+        moff = torch.from_numpy(poff.astype(np.int64))
+        out, offs = gather_packed(buf, moff, count, dst=dst, dist=dist)
+        q.put((rank, None if out is None else (bytes(out.numpy()), offs.numpy().tolist())))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,dst", [(2, 0), (2, 1), (3, 1)])
+def test_gloo_gather_packed_equals_single_rank_pack(world, dst):
+    """The batch case: block shards packed on each rank, gathered onto rank
+    `dst` by point-to-point sends into their global offsets -- the gathered stream and message
+    offsets equal a single rank packing the whole batch."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, dst, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(out[r] is None for r in range(world) if r != dst)
+    got, goff = out[dst]
+    import pyoracle
+
+    msgs = _global_batch()
+    off = np.cumsum([0] + [len(m) for m in msgs]).astype(np.uint64)
+    packed, poff, st = pyoracle.Oracle().pack_batch(np.concatenate(msgs), off)
+    assert got == bytes(packed[: int(poff[-1])])
+    assert goff == [int(x) for x in poff]

@@ -38,6 +38,9 @@ CONFIGS = {
     # rank 0 of the 8-GPU round-robin shard (bench.py --gpus 8: first_msg = rank, stride = 8)
     "c5r0of8": ((32 << 20) // 8, 1, 0, "mixed", 0, 8, 65536, 262144),
 }
+# ranks 1-7 of the same 8-GPU round-robin shard (first_msg = rank)
+for _r in range(1, 8):
+    CONFIGS[f"c5r{_r}of8"] = ((32 << 20) // 8, 1, 0, "mixed", _r, 8, 65536, 262144)
 OUT = os.path.join(ROOT, "tests", "golden", "manifest.json")
 
 
@@ -89,7 +92,9 @@ def main():
                                 "oracle/cpk_oracle.c cpko_gen_*)")
     man.setdefault("configs", {})
     for nm in names:
-        man["configs"][nm] = run(nm, ora, ref)
+        rec = run(nm, ora, ref)
+        man = json.load(open(OUT)) if os.path.exists(OUT) else man  # (another run may have added)
+        man.setdefault("configs", {})[nm] = rec
         with open(OUT, "w") as f:
             json.dump(man, f, indent=1, sort_keys=True)
             f.write("\n")
