@@ -86,6 +86,7 @@ def load_library():
         "cpk_timing_read": (C.c_int, [vp, C.POINTER(C.c_double), C.POINTER(u64),
                                       C.POINTER(C.c_double), C.POINTER(u64)]),
         "cpk_timing_read_all": (C.c_int, [vp, C.POINTER(C.c_double), C.POINTER(u64)]),
+        "cpk_debug_copy": (C.c_int, [vp, vp, u64, u32, vp]),
     }
     for name, (res, args) in sigs.items():
         f = getattr(L, name)

@@ -10,12 +10,23 @@
 namespace cpk {
 namespace {
 
+// Marks word p as a chunk start (and, at a pack tile start, the tile's bit).
+__device__ __forceinline__ void mark(unsigned long long* bits, unsigned long long* tstarts,
+                                     uint64_t p) {
+  atomicOr(bits + (p >> 6), 1ull << (p & 63));
+  if (p % kPackTileWords == 0 && p) {  // (tile 0 has no predecessor to read its bit)
+    const uint64_t t = p / kPackTileWords;
+    atomicOr(tstarts + (t >> 6), 1ull << (t & 63));
+  }
+}
+
 // Chunk-start bitmap + per-message framing status for a batch of flat messages.
 // Message i = words[off[i], off[i+1]): segment table (serializeSegmentTable serialize.c++:
 // 311-330) then segments; chunk starts = message start, table end, each segment start.
 __global__ void message_bits_kernel(const uint64_t* __restrict__ words,
                                     const uint64_t* __restrict__ off, uint64_t n,
                                     unsigned long long* __restrict__ bits,
+                                    unsigned long long* __restrict__ tstarts,
                                     int32_t* __restrict__ status, TileFirstJob tf,
                                     uint32_t tf_block) {
   if (run_tile_first(tf, tf_block)) return;
@@ -27,7 +38,7 @@ __global__ void message_bits_kernel(const uint64_t* __restrict__ words,
     if (status) status[i] = 11;  // CPK_ERR_EMPTY_MESSAGE
     return;
   }
-  atomicOr(bits + (w0 >> 6), 1ull << (w0 & 63));
+  mark(bits, tstarts, w0);
   const uint64_t nw = w1 - w0;
   const uint32_t* t32 = (const uint32_t*)(words + w0);
   const uint64_t nseg = (uint64_t)t32[0] + 1;
@@ -42,44 +53,46 @@ __global__ void message_bits_kernel(const uint64_t* __restrict__ words,
     st = 6;  // CPK_ERR_BAD_FRAMING: packed as one chunk
   } else {
     uint64_t p = w0 + tw;
-    if (p < w1) atomicOr(bits + (p >> 6), 1ull << (p & 63));
+    if (p < w1) mark(bits, tstarts, p);
     for (uint64_t s = 0; s + 1 < nseg; s++) {
       p += t32[s + 1];
-      if (p < w1) atomicOr(bits + (p >> 6), 1ull << (p & 63));
+      if (p < w1) mark(bits, tstarts, p);
     }
   }
   if (status) status[i] = st;
 }
 
 __global__ void chunk_bits_kernel(const uint64_t* __restrict__ off, uint64_t n, uint64_t N,
-                                  unsigned long long* __restrict__ bits, TileFirstJob tf,
+                                  unsigned long long* __restrict__ bits,
+                                  unsigned long long* __restrict__ tstarts, TileFirstJob tf,
                                   uint32_t tf_block) {
   if (run_tile_first(tf, tf_block)) return;
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i == 0 && N > 0) atomicOr(bits, 1ull);  // word 0 always starts a chunk
+  if (i == 0 && N > 0) mark(bits, tstarts, 0);  // word 0 always starts a chunk
   if (i >= n) return;
   const uint64_t p = off[i];
-  if (p < N && off[i + 1] > p) atomicOr(bits + (p >> 6), 1ull << (p & 63));
+  if (p < N && off[i + 1] > p) mark(bits, tstarts, p);
 }
 
 }  // namespace
 
 hipError_t launch_message_bits(const uint64_t* words, const uint64_t* off, uint64_t n,
-                               uint64_t* bits, int32_t* status, const TileFirstJob& tf,
-                               hipStream_t stream) {
+                               uint64_t* bits, uint64_t* tstarts, int32_t* status,
+                               const TileFirstJob& tf, hipStream_t stream) {
   const unsigned nb = (unsigned)((n + 255) / 256);
   if (nb + tile_first_blocks(tf) == 0) return hipSuccess;
   hipLaunchKernelGGL(message_bits_kernel, dim3(nb + tile_first_blocks(tf)), dim3(256), 0, stream,
-                     words, off, n, (unsigned long long*)bits, status, tf, nb);
+                     words, off, n, (unsigned long long*)bits, (unsigned long long*)tstarts,
+                     status, tf, nb);
   return hipGetLastError();
 }
 
 hipError_t launch_chunk_bits(const uint64_t* off, uint64_t n, uint64_t N, uint64_t* bits,
-                             const TileFirstJob& tf, hipStream_t stream) {
+                             uint64_t* tstarts, const TileFirstJob& tf, hipStream_t stream) {
   const unsigned nb = (n == 0 && N == 0) ? 0u : (unsigned)((n + 256) / 256);
   if (nb + tile_first_blocks(tf) == 0) return hipSuccess;
   hipLaunchKernelGGL(chunk_bits_kernel, dim3(nb + tile_first_blocks(tf)), dim3(256), 0, stream,
-                     off, n, N, (unsigned long long*)bits, tf, nb);
+                     off, n, N, (unsigned long long*)bits, (unsigned long long*)tstarts, tf, nb);
   return hipGetLastError();
 }
 

@@ -14,7 +14,10 @@ constexpr uint64_t kUnpackTileBytes = 4096;     // packed bytes per unpack tile 
 struct PackTileArgs {
   const uint64_t* words;       // batch of words (all chunks back to back)
   uint64_t nwords;
-  const uint64_t* chunk_bits;  // bit i set <=> word i starts a chunk (word 0 always)
+  uint64_t* chunk_bits;        // bit i set <=> word i starts a chunk (word 0 always); zero at
+                               // rest: each tile clears the words of its own 2048 words
+  uint64_t* tile_starts;       // bit t set <=> tile t's first word starts a chunk (read and
+                               // cleared by tile t - 1)
   uint64_t ntiles;
   uint8_t* out;
   uint64_t out_capacity;
@@ -32,12 +35,21 @@ struct PackTileArgs {
   uint32_t* thole;             // byte of a tile's provisional count (~0: none)
   uint32_t* tpatch;            // the next tile's final value for it (0x100 | v; 0: none)
   uint32_t* err;
+  // direct pack (pack_direct_kernel), all zeroed: tile tickets, tile AGG descriptors, per
+  // 64-tile group (count << 48) + bytes, per group the inclusive byte prefix
+  uint32_t* ticket;
+  uint64_t* desc;
+  uint64_t* gword;
+  uint64_t* gincl;
 };
 
 // tiles -> scratch slots (tile_bytes, thole, tpatch), then (after the scan of tile_bytes into
 // tile_off) scratch -> out
 hipError_t launch_pack_tiles(const PackTileArgs& a, hipStream_t stream);
 hipError_t launch_pack_place(const PackTileArgs& a, hipStream_t stream);
+// tiles -> out directly (persistent, ticketed, two-level look-back resolved one tile late): no
+// scratch slots, no scan, no placement
+hipError_t launch_pack_direct(const PackTileArgs& a, hipStream_t stream);
 // tile_first (first i with pos[i] >= tile start, per tile) as extra blocks of a prologue
 // kernel: one launch fewer per call.  ntiles == 0: no such job.
 struct TileFirstJob {
@@ -50,11 +62,14 @@ struct TileFirstJob {
   uint64_t* zero = nullptr;
   uint64_t zero_words = 0;
 };
+// The chunk-start bitmap (OR-ed into zeroed bits, and into tstarts for the first word of a
+// pack tile of kPackTileWords words), tile_first and the zeroing of TileFirstJob::zero in one
+// launch.
 hipError_t launch_message_bits(const uint64_t* words, const uint64_t* off, uint64_t n,
-                               uint64_t* bits, int32_t* status, const TileFirstJob& tf,
-                               hipStream_t stream);
+                               uint64_t* bits, uint64_t* tstarts, int32_t* status,
+                               const TileFirstJob& tf, hipStream_t stream);
 hipError_t launch_chunk_bits(const uint64_t* off, uint64_t n, uint64_t N, uint64_t* bits,
-                             const TileFirstJob& tf, hipStream_t stream);
+                             uint64_t* tstarts, const TileFirstJob& tf, hipStream_t stream);
 
 struct UnpackArgs {
   const uint8_t* packed;        // batch of packed bytes
@@ -74,18 +89,17 @@ struct UnpackArgs {
   uint64_t ntiles;
   uint64_t* desc;               // ntiles tile descriptors (cpk_unpack.hip), zeroed
   uint32_t* x0p;                // ntiles chain-0 exits (0x80000000 | exit), zeroed
-  uint32_t* fail_flag;          // per message
-  uint32_t* fail_list;
-  uint32_t* fail_count;
   uint32_t* err;
   unsigned long long* stamps;   // diagnostic build only (env CPK_STAMPS), else NULL
   uint32_t debug_skip;          // diagnostic (env CPK_DEBUG_SKIP): 4 no chain-0 walks, 8 no look-back,
                                 // 16 no record batches, 32 no lists
   const uint64_t* tile_firstpos;  // in_off[tile_first[t]]: the first message start >= tile start
+  uint64_t* hdr_desc;           // the header launch's scan descriptors (zero at rest): cleared
+  uint64_t hdr_nblocks;         // by the tile kernel once the headers are done (0: none)
 };
 
-// Unpack stages (launch_unpack_stage), in launch order.
-constexpr int kUnpackTiles = 0, kUnpackFallback = 1;
+// Unpack stages (launch_unpack_stage), in launch order: the tile kernel is the only one.
+constexpr int kUnpackTiles = 0;
 
 uint32_t debug_skip();
 
@@ -97,9 +111,14 @@ constexpr int kStampRows = 256;
 // Diagnostic stamp buffers (env CPK_STAMPS=1): [1] unpack counters.
 unsigned long long* debug_stamps(int which);
 
+// Headers + their word offsets in one launch (decoupled look-back over header blocks whose
+// descriptors `desc` -- header_scan_blocks(n) u64 -- are zero on entry and cleared again by the
+// tile kernel through UnpackArgs::hdr_desc); word_off gets n + 1 entries.
+uint64_t header_scan_blocks(uint64_t n);
 hipError_t launch_unpack_header(const uint8_t* packed, const uint64_t* in_off, uint64_t n,
-                                uint64_t limit, uint64_t* flat, int32_t* hdr_status,
-                                int32_t* status, const TileFirstJob& tf, hipStream_t stream);
+                                uint64_t limit, uint64_t* word_off, int32_t* hdr_status,
+                                int32_t* status, uint64_t* desc, uint32_t* err,
+                                const TileFirstJob& tf, hipStream_t stream);
 hipError_t launch_unpack_stage(int stage, const UnpackArgs& a, hipStream_t stream);
 hipError_t launch_unpack_init(uint32_t mode, const uint64_t* in_off, const uint64_t* word_off,
                               uint64_t n, int32_t* status, uint64_t* size_out,
@@ -110,6 +129,9 @@ hipError_t launch_unpack_init(uint32_t mode, const uint64_t* in_off, const uint6
 // segment tables from word 0 over the decoded words.
 // Fills nbytes at p (8-byte aligned) with value: the codec's scratch zeroing.
 hipError_t launch_fill(void* p, uint64_t nbytes, uint8_t value, hipStream_t stream);
+// Streaming 16-byte-per-lane copy (diagnostic: the bench's measured copy ceiling).
+hipError_t launch_copy(void* dst, const void* src, uint64_t nbytes, uint32_t blocks,
+                       hipStream_t stream);
 hipError_t launch_set_u64x4(uint64_t* dst, uint64_t v0, uint64_t v1, uint64_t v2, uint64_t v3,
                             hipStream_t stream);
 // The message chain over the decoded words, block-parallel (cpk_stream.hip); scratch holds

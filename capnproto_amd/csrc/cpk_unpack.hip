@@ -20,8 +20,10 @@
 //                           inclusive at once).  Then the records are expanded one lane per
 //                           record, 64 consecutive records at a time (coalesced stores), zero and
 //                           raw runs written by the wave.
-//   4. fallback_kernel      messages flagged by an unsettled fixed point, decoded serially (one
-//                           wave per message).  None of the benchmark configurations needs it.
+//   (The lane fixed point that settles chain 0 converges in at most 64 rounds -- once lanes
+//   0..k-1 hold their true entries lane k's is right -- so no tile is ever left unsettled and
+//   there is no serial fallback decoder; a tile that did hit the cap would raise an internal
+//   error rather than write words.)
 #include <limits.h>
 
 #include "cpk_device.h"
@@ -84,14 +86,11 @@ __device__ int32_t decode_exact(const uint8_t* b, uint64_t& p, uint64_t end, uin
   return kOK;
 }
 
-// 1. Message headers (serialize.c++:202-242).
-__global__ void header_kernel(const uint8_t* __restrict__ packed,
-                              const uint64_t* __restrict__ in_off, uint64_t n, uint64_t limit,
-                              uint64_t* __restrict__ flat, int32_t* __restrict__ hdr_status,
-                              int32_t* __restrict__ status, TileFirstJob tf, uint32_t tf_block) {
-  if (run_tile_first(tf, tf_block)) return;
-  const uint64_t m = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (m >= n) return;
+// 1. Message headers (serialize.c++:202-242): the flat size of message m in words (segment
+// table + segments), 0 when the header fails (its status says why).
+__device__ __forceinline__ uint64_t header_words(const uint8_t* __restrict__ packed,
+                                                 const uint64_t* __restrict__ in_off, uint64_t m,
+                                                 uint64_t limit, int32_t* st_out) {
   uint64_t p = in_off[m];
   const uint64_t end = in_off[m + 1];
   uint64_t first = 0;
@@ -141,9 +140,77 @@ __global__ void header_kernel(const uint8_t* __restrict__ packed,
       }
     }
   }
-  flat[m] = words;
-  hdr_status[m] = st;
-  status[m] = st;
+  *st_out = st;
+  return words;
+}
+
+// One launch for the headers and their word offsets: blocks [0, nsb) each take kHdrBlock
+// messages (4 per thread), decode their headers and scan the flat sizes into word_off with a
+// single-pass decoupled look-back over the blocks (blocks in launch order; a block only waits
+// on lower ones).  The look-back descriptors are zero at rest: the tile kernel of the same call
+// clears them once every header block is done (UnpackArgs::hdr_desc).  Blocks past nsb compute
+// tile_first and zero the tile kernel's scratch (TileFirstJob).
+#ifndef CPK_HDR_PER
+#define CPK_HDR_PER 4
+#endif
+constexpr int kHdrPerThread = CPK_HDR_PER;
+constexpr uint64_t kHdrBlock = 256 * kHdrPerThread;
+__global__ __launch_bounds__(256) void header_kernel(
+    const uint8_t* __restrict__ packed, const uint64_t* __restrict__ in_off, uint64_t n,
+    uint64_t limit, uint64_t* __restrict__ word_off, int32_t* __restrict__ hdr_status,
+    int32_t* __restrict__ status, uint64_t* desc, uint32_t* err, TileFirstJob tf,
+    uint32_t nsb) {
+  if (run_tile_first(tf, nsb)) return;
+  __shared__ uint64_t s_wave[4];
+  __shared__ uint64_t s_excl;
+  const uint64_t b = blockIdx.x;
+  const int l = lane_id();
+  const int wv = (int)(threadIdx.x >> 6);
+  const uint64_t m0 = b * kHdrBlock + (uint64_t)kHdrPerThread * threadIdx.x;
+  uint64_t w[kHdrPerThread];
+  uint64_t sum = 0;
+#pragma unroll
+  for (int k = 0; k < kHdrPerThread; k++) {
+    const uint64_t m = m0 + k;
+    w[k] = 0;
+    if (m < n) {
+      int32_t st;
+      w[k] = header_words(packed, in_off, m, limit, &st);
+      hdr_status[m] = st;
+      status[m] = st;
+    }
+    sum += w[k];
+  }
+  const uint64_t incl = wave_incl_sum64(sum);
+  if (l == 63) s_wave[wv] = incl;
+  __syncthreads();
+  uint64_t before = 0, agg = 0;
+#pragma unroll
+  for (int v = 0; v < 4; v++) {
+    const uint64_t x = s_wave[v];
+    if (v < wv) before += x;
+    agg += x;
+  }
+  if (wv == 0) {
+    uint64_t excl = 0;
+    if (b == 0) {
+      if (l == 0) store_agent(desc, kDescIncl | agg);
+    } else {
+      if (l == 0) store_agent(desc + b, kDescAgg | agg);
+      excl = lookback<8>(desc, b, err);
+      if (l == 0) store_agent(desc + b, kDescIncl | (excl + agg));
+    }
+    if (l == 0) s_excl = excl;
+  }
+  __syncthreads();
+  uint64_t o = s_excl + before + incl - sum;
+#pragma unroll
+  for (int k = 0; k < kHdrPerThread; k++) {
+    const uint64_t m = m0 + k;
+    if (m < n) word_off[m] = o;
+    o += w[k];
+    if (m + 1 == n) word_off[n] = o;
+  }
 }
 
 // Byte length of a record from its tag and its count byte (tag 0x00: + count byte; 0xff: +
@@ -328,22 +395,21 @@ struct MsgInfo {
   bool ok, fits;
 };
 
-// Message m's metadata.  check_flag: a message flagged for the fallback decoder counts as not ok
-// (the tile kernels leave it alone); the fallback itself passes false.
-__device__ __forceinline__ MsgInfo msg_info(const UnpackArgs& a, uint64_t m, bool check_flag) {
+// Message m's metadata.
+__device__ __forceinline__ MsgInfo msg_info(const UnpackArgs& a, uint64_t m) {
   MsgInfo mi;
   if (!a.word_off) {  // size-only mode
     mi.base = 0;
     mi.total = ~0ull >> 2;
     mi.end = a.in_off[m + 1];
-    mi.ok = !(check_flag && a.fail_flag[m]);
+    mi.ok = true;
     mi.fits = false;
     return mi;
   }
   mi.base = a.word_off[m];
   mi.total = a.word_off[m + 1] - mi.base;
   mi.end = a.in_off[m + 1];
-  mi.ok = (a.hdr_status ? a.hdr_status[m] == kOK : true) && !(check_flag && a.fail_flag[m]);
+  mi.ok = a.hdr_status ? a.hdr_status[m] == kOK : true;
   mi.fits = mi.base + mi.total <= a.words_capacity;
   return mi;
 }
@@ -499,17 +565,40 @@ __device__ __forceinline__ void run_jobs(const UnpackArgs& a, const RunJob& job,
   }
 }
 
-// Diagnostic counters (env CPK_STAMPS=1 only; a.stamps is NULL otherwise).
-enum : int { kDbgFlagged = 4 };
-__device__ __forceinline__ void dbg_count(const UnpackArgs& a, int slot) {
-  if (a.stamps) atomicAdd(a.stamps + kStampSlots * (blockIdx.x & (kStampRows - 1)) + slot, 1ull);
-}
-__device__ __forceinline__ void flag_message(const UnpackArgs& a, uint64_t m) {
-  if (atomicExch(a.fail_flag + m, 1u) == 0) {
-    const uint32_t i = atomicAdd(a.fail_count, 1u);
-    a.fail_list[i] = (uint32_t)m;
-    dbg_count(a, kDbgFlagged);
+#ifndef CPK_SHORT_RUN
+#define CPK_SHORT_RUN 4  // runs of at most this many words are written by their own lane
+#endif
+// Runs of a batch: a short run (at most CPK_SHORT_RUN words, zero or raw from the staged tile --
+// most runs of dense data, where a zero or raw stretch rarely lasts) is written by its own lane,
+// all such lanes together, one word per step; longer runs and raw runs outside the staged bytes
+// go through run_jobs (the whole wave per run, coalesced).
+__device__ __forceinline__ void run_jobs_batch(const UnpackArgs& a, RunJob job, const uint8_t* d,
+                                               uint64_t dbase, uint32_t dlen) {
+  if (CPK_SHORT_RUN > 0 && a.words) {
+    const bool in_lds = !job.raw || (job.src >= dbase && job.src - dbase + 8ull * job.n + 4 <= dlen);
+    const bool sh = job.n != 0 && job.n <= (uint32_t)CPK_SHORT_RUN && in_lds;
+    if (ballot(sh)) {
+      const uint32_t n = sh ? job.n : 0u;
+      const uint32_t o0 = (uint32_t)(job.src - dbase);
+      const uint32_t* const d32 = (const uint32_t*)d;
+#pragma unroll
+      for (uint32_t k = 0; k < (uint32_t)CPK_SHORT_RUN; k++) {
+        if (!ballot(k < n)) break;
+        if (k < n) {
+          uint64_t v = 0;
+          if (job.raw) {
+            const uint32_t o = o0 + 8 * k, q = o >> 2, s3 = o & 3;
+            const uint32_t q0 = d32[q], q1 = d32[q + 1], q2 = d32[q + 2];
+            v = ((uint64_t)__builtin_amdgcn_alignbyte(q2, q1, s3) << 32) |
+                __builtin_amdgcn_alignbyte(q1, q0, s3);
+          }
+          a.words[job.dst + k] = v;
+        }
+      }
+      if (sh) job.n = 0;
+    }
   }
+  run_jobs(a, job, d, dbase, dlen);
 }
 
 // Per-tile window of message metadata: lane i describes message mw + i.
@@ -519,7 +608,7 @@ struct MsgWin {
   uint64_t end;      // in_off[m + 1]
   uint64_t base;     // word_off[m]
   uint64_t total;    // word_off[m + 1] - word_off[m]
-  uint32_t ok;       // header accepted and not left to the fallback decoder
+  uint32_t ok;       // header accepted
 };
 
 __device__ __forceinline__ void load_win(const UnpackArgs& a, int64_t mw, MsgWin& w) {
@@ -530,17 +619,16 @@ __device__ __forceinline__ void load_win(const UnpackArgs& a, int64_t mw, MsgWin
   const uint64_t mc = v ? (uint64_t)m : 0;
   const uint64_t mn = mc + 1 <= a.nmsgs ? mc + 1 : a.nmsgs;
   const uint64_t* const wo = a.word_off ? a.word_off : a.in_off;
-  const int32_t* const hs = a.hdr_status ? a.hdr_status : (const int32_t*)a.fail_flag;
+  const int32_t* const hs = a.hdr_status ? a.hdr_status : (const int32_t*)a.in_off;
   const uint64_t s0 = a.in_off[mc], e0 = a.in_off[mn];
   const uint64_t b0 = wo[mc], b1 = wo[mn];
   const int32_t h = hs[mc];
-  const uint32_t ff = a.fail_flag[mc];
   w.mw = mw;
   w.start = v ? s0 : ~0ull;
   w.end = v ? e0 : ~0ull;
   w.base = v && a.word_off ? b0 : 0;
   w.total = !v ? 0 : (a.word_off ? b1 - b0 : ~0ull >> 2);
-  w.ok = v && (a.hdr_status ? h == kOK : true) && ff == 0;
+  w.ok = v && (a.hdr_status ? h == kOK : true);
 }
 
 // Starts only (index_kernel needs no more of the window).
@@ -908,13 +996,6 @@ __device__ uint64_t lookback_tiles(const UnpackArgs& a, uint64_t t, uint32_t* xp
   return acc;
 }
 
-__device__ __forceinline__ void flag_tile_messages(const UnpackArgs& a, uint64_t t) {
-  const uint64_t mf = a.tile_first[t];
-  const uint64_t A = t * kB;
-  if (mf > 0) flag_message(a, mf - 1);
-  for (uint64_t m = mf; m < a.nmsgs && a.in_off[m] < A + kB; m++) flag_message(a, m);
-}
-
 // Expansion of a tile's records given its true record-start masks (lane = sub-tile) and excl,
 // the words of the tile's first message before the tile: one lane per record, 64 consecutive
 // records at a time, coalesced stores; zero and raw runs written by the wave.  Records that end
@@ -928,7 +1009,7 @@ __device__ __forceinline__ void expand_records(const UnpackArgs& a, uint64_t A, 
   const int l = lane_id();
   uint16_t* list = (uint16_t*)aux;
   // Fast expansion when every message touching the tile is in the window, has a valid header,
-  // is not left to the fallback, fits the output, and no two messages start at the same byte.
+  // fits the output, and no two messages start at the same byte.
   bool fast = a.mode == 0 && mlast - (mfirst - 1) <= 63 && a.word_off && a.words;
   if (fast) {
     const int64_t m = win.mw + l;
@@ -1027,7 +1108,7 @@ __device__ __forceinline__ void expand_records(const UnpackArgs& a, uint64_t A, 
       mi.total = shfl64(win.total, wl);
       mi.end = shfl64(win.end, wl);
       mi.ok = shfl32(win.ok, wl) != 0;
-      if (!inwin && act && m >= 0 && (uint64_t)m < a.nmsgs) mi = msg_info(a, (uint64_t)m, true);
+      if (!inwin && act && m >= 0 && (uint64_t)m < a.nmsgs) mi = msg_info(a, (uint64_t)m);
       mi.fits = a.word_off ? (mi.base + mi.total <= a.words_capacity) : false;
       const uint64_t word = expand_word(d, p, rc.tag, lut);
       RunJob job;
@@ -1049,7 +1130,7 @@ __device__ __forceinline__ void expand_records(const UnpackArgs& a, uint64_t A, 
           report_end(a, (uint64_t)m, st, job);
         }
       }
-      run_jobs(a, job, d, A, (uint32_t)(kB + kPad));
+      run_jobs_batch(a, job, d, A, (uint32_t)(kB + kPad));
       base_key = readlane32(km, 63);
       sum += readlane32(inc, 63);
     }
@@ -1108,7 +1189,7 @@ __device__ __forceinline__ void expand_records(const UnpackArgs& a, uint64_t A, 
         job.dst = cbase0 + excl + o + 1;
         job.raw = f;
         job.src = A + (uint32_t)p + 10;
-        run_jobs(a, job, d, A, (uint32_t)(kB + kPad));
+        run_jobs_batch(a, job, d, A, (uint32_t)(kB + kPad));
         sum += readlane32(inc, 63);
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1243,7 +1324,7 @@ __device__ __forceinline__ void expand_records(const UnpackArgs& a, uint64_t A, 
           report_end(a, (uint64_t)m, st, job);
         }
       }
-      run_jobs(a, job, d, A, (uint32_t)(kB + kPad));
+      run_jobs_batch(a, job, d, A, (uint32_t)(kB + kPad));
       base_key = readlane32(km, 63);
       sum += readlane32(inc, 63);
       if (msb) {
@@ -1276,6 +1357,9 @@ unpack_tiles_kernel(UnpackArgs a) {
   __syncthreads();
   const uint64_t t = (uint64_t)blockIdx.x * 4 + wv;
   if (t >= a.ntiles) return;
+  // the header launch is done: its scan descriptors go back to zero for the next call
+  for (uint64_t i = t + a.ntiles * (uint64_t)l; i < a.hdr_nblocks; i += 64 * a.ntiles)
+    a.hdr_desc[i] = 0;
   uint8_t* const d = lds_data[wv];
   uint64_t* const aux = lds_aux[wv];
   const uint64_t P = a.nbytes;
@@ -1303,9 +1387,8 @@ unpack_tiles_kernel(UnpackArgs a) {
   const uint32_t x0 = readlane32((uint32_t)out, 63);
   if (l == 0) store_agent32(a.x0p + t, 0x80000000u | x0);
   if (!settled) {
-    // rare (fixed point at its iteration cap): the messages touching the tile go to the serial
-    // fallback decoder, and this tile writes none of their words
-    if (l == 0) flag_tile_messages(a, t);
+    // unreachable (the fixed point settles in at most 64 rounds): refuse the batch, write nothing
+    if (l == 0) raise_error(a.err, kErrInternal);
     win.ok = 0;
   }
 
@@ -1381,87 +1464,6 @@ unpack_tiles_kernel(UnpackArgs a) {
                  mlast, msw, w_tile);
 }
 
-// 6. Serial re-decode of flagged messages: one wave per message; lane 0 walks the records of a
-// 4 KiB window, then the wave expands them with the same record handler as expand_kernel.
-__global__ __launch_bounds__(64) void fallback_kernel(UnpackArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t d[kB + kPad];
-  __shared__ uint16_t rpos[kB];
-  __shared__ uint64_t rwb[kB];
-  __shared__ int sh_n, sh_adv;
-  const int l = lane_id();
-  const uint32_t lut = deposit_sel((uint32_t)l & 15);
-  const uint32_t nfail = *a.fail_count;
-  for (uint32_t fi = blockIdx.x; fi < nfail; fi += gridDim.x) {
-    const uint64_t m = a.fail_list[fi];
-    const MsgInfo mi = msg_info(a, m, false);
-    if (!mi.ok) continue;
-    uint64_t pos = a.in_off[m];
-    const uint64_t mend = mi.end;
-    uint64_t wb = 0;
-    bool done = false;
-    while (!done && pos < mend) {
-      for (int o = l; o < kB + kPad; o += 64) d[o] = (pos + o < mend) ? a.packed[pos + o] : 0;
-      __syncthreads();
-      if (l == 0) {
-        int p = 0, n = 0;
-        uint64_t w = wb;
-        while (p < kB && pos + p < mend) {
-          rpos[n] = (uint16_t)p;
-          rwb[n] = w;
-          n++;
-          const Rec rc = read_rec(d, p);
-          w += 1 + rc.cnt;
-          p += rc.hb + (rc.run ? 1 : 0) + (rc.tag == 0xff ? 8 * (int)rc.cnt : 0);
-          if (w >= mi.total) break;
-        }
-        sh_n = n;
-        sh_adv = p;
-      }
-      __syncthreads();
-      const int n = sh_n;
-      for (int b0 = 0; b0 < n; b0 += 64) {
-        const int r = b0 + l;
-        RunJob job;
-        job.n = 0;
-        const int pp = r < n ? rpos[r] : 0;
-        const uint64_t word = expand_word(d, pp, d[pp], lut);
-        if (r < n) {
-          const int p = pp;
-          const uint64_t w0 = rwb[r];
-          if (a.mode == 2) {
-            const int32_t s = handle_record(a, d, p, pos + p, w0, mi, &job, word);
-            if (s == kInvalid) {
-              a.status[m] = kInvalid;
-              a.size_out[m] = 0;
-              done = true;
-            } else if (s == kSizeDone) {
-              const Rec rc = read_rec(d, p);
-              a.status[m] = kOK;
-              a.size_out[m] = w0 + 1 + (rc.run ? rc.cnt : 0);
-              done = true;
-            }
-          } else {
-            const int32_t s = handle_record(a, d, p, pos + p, w0, mi, &job, word);
-            if (s >= 0) {
-              a.status[m] = s;
-              report_end(a, m, s, job);
-              done = true;
-            }
-          }
-        }
-        run_jobs(a, job);
-      }
-      done = ballot(done) != 0;
-      if (n > 0) {
-        const Rec rc = read_rec(d, rpos[n - 1]);
-        wb = rwb[n - 1] + 1 + rc.cnt;
-      }
-      pos += (uint64_t)sh_adv;
-      __syncthreads();
-    }
-  }
-}
-
 // Status before any record is seen (buffers with no records keep it): flat-packed chunks read
 // exactly word_off[m+1]-word_off[m] words; size-only buffers start at 0 words.
 __global__ void init_kernel(uint32_t mode, const uint64_t* __restrict__ in_off,
@@ -1493,19 +1495,22 @@ hipError_t launch_unpack_init(uint32_t mode, const uint64_t* in_off, const uint6
   return hipGetLastError();
 }
 
+uint64_t header_scan_blocks(uint64_t n) { return (n + kHdrBlock - 1) / kHdrBlock; }
+
 hipError_t launch_unpack_header(const uint8_t* packed, const uint64_t* in_off, uint64_t n,
-                                uint64_t limit, uint64_t* flat, int32_t* hdr_status,
-                                int32_t* status, const TileFirstJob& tf, hipStream_t stream) {
-  const unsigned nb = (unsigned)((n + 255) / 256);
+                                uint64_t limit, uint64_t* word_off, int32_t* hdr_status,
+                                int32_t* status, uint64_t* desc, uint32_t* err,
+                                const TileFirstJob& tf, hipStream_t stream) {
+  const unsigned nb = (unsigned)header_scan_blocks(n);
   if (nb + tile_first_blocks(tf) == 0) return hipSuccess;
   hipLaunchKernelGGL(header_kernel, dim3(nb + tile_first_blocks(tf)), dim3(256), 0, stream,
-                     packed, in_off, n, limit, flat, hdr_status, status, tf, nb);
+                     packed, in_off, n, limit, word_off, hdr_status, status, desc, err, tf, nb);
   return hipGetLastError();
 }
 
 hipError_t launch_unpack_stage(int stage, const UnpackArgs& a, hipStream_t stream) {
   if (a.ntiles == 0) return hipSuccess;
-  if (stage == kUnpackTiles) {
+  {
     // plain tiles are most tiles when messages span several tiles
     const bool plain = a.word_off && a.nmsgs && a.nbytes / a.nmsgs >= 4 * (uint64_t)kB;
     if (plain)
@@ -1514,11 +1519,8 @@ hipError_t launch_unpack_stage(int stage, const UnpackArgs& a, hipStream_t strea
     else
       hipLaunchKernelGGL(unpack_tiles_kernel<false>, dim3((unsigned)((a.ntiles + 3) / 4)),
                          dim3(256), 0, stream, a);
-  } else {
-    // a small grid: it only loops over the (rare) flagged messages, and an empty launch of
-    // thousands of workgroups costs microseconds
-    hipLaunchKernelGGL(fallback_kernel, dim3(128), dim3(64), 0, stream, a);
   }
+  (void)stage;
   return hipGetLastError();
 }
 

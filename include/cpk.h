@@ -276,10 +276,11 @@ cpk_status cpk_gen_offsets(cpk_ctx* ctx, uint64_t seed, uint64_t first_msg,
 
 /* ------------------------------------------------------------------------------------------
  * Measurement hooks (bench.py).  When enabled, every pack / unpack call brackets its tile
- * kernels with HIP events on the call's stream: timer 0 the pack tile kernels together (count
- * pass, scan, emit pass), timer 1 the unpack tile kernels together (index, resolve, expand,
- * fallback), timers 2..5 each of those four alone, timers 6 and 7 the pack count and emit
- * passes.  cpk_timing_read synchronises the events, returns the summed milliseconds and
+ * kernels with HIP events on the call's stream: timer 0 the pack kernels after the framing
+ * launch (tile kernel, scan of the tile byte counts, placement -- or the direct kernel alone),
+ * timer 1 the unpack kernels after the header launch, timer 2 the unpack tile kernel alone;
+ * timers 3..7 are unused.  cpk_timing_read synchronises the events, returns the summed
+ * milliseconds and
  * launch counts of timers 0 and 1 since the last read, and clears every timer;
  * cpk_timing_read_all does the same for all CPK_TIMERS timers. */
 #define CPK_TIMERS 8

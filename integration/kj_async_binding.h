@@ -9,10 +9,12 @@
 //
 //   tryReadMessage  reads from the stream into a byte buffer, asks the device for one message
 //                   (cpk_read_packed_message_host); CPK_ERR_PREMATURE_EOF means "read more and
-//                   retry".  A stream read may return any amount, so after a failed attempt the
-//                   next one waits until the buffered bytes have doubled (or the stream ends):
-//                   a message costs O(log size) device attempts and O(size) bytes uploaded in
-//                   all, however the socket fragments it.  Bytes past the message stay
+//                   retry".  After a failed attempt the next one waits until the buffered bytes
+//                   have doubled, unless a stream read comes back short (the peer paused: the
+//                   message may be complete, and a request/response peer sends nothing more
+//                   until it is read) or the stream ends.  A message streamed without pauses
+//                   costs O(log size) device attempts and O(size) bytes uploaded, however the
+//                   socket fragments it; each pause of the peer inside a message adds one.  Bytes past the message stay
 //                   buffered for the next call (back-to-back messages, one stream read).  A clean
 //                   end before the first byte is kj::none; an end inside a message is
 //                   DISCONNECTED "Premature EOF." (serialize-async.c++:92, :525).  The flat
@@ -185,8 +187,9 @@ class PackedMessageStream final : public capnp::MessageStream {
   }
 
   kj::Promise<kj::Maybe<capnp::MessageReaderAndFds>> readLoop(capnp::ReaderOptions options,
-                                                               kj::ArrayPtr<capnp::word> scratch) {
-    if (end_ > begin_ && end_ - begin_ >= retryAt_) {
+                                                               kj::ArrayPtr<capnp::word> scratch,
+                                                               bool paused = true) {
+    if (end_ > begin_ && (paused || end_ - begin_ >= retryAt_)) {
       KJ_IF_SOME(r, tryDecode(options, scratch)) {
         retryAt_ = failedAt_ = 0;
         return kj::Maybe<capnp::MessageReaderAndFds>(capnp::MessageReaderAndFds{kj::mv(r), nullptr});
@@ -203,7 +206,7 @@ class PackedMessageStream final : public capnp::MessageStream {
     const size_t want = std::max(readSize_, end_);
     if (buf_.size() < end_ + want) buf_.resize(end_ + want);
     return stream_.tryRead(buf_.data() + end_, 1, want)
-        .then([this, options, scratch](size_t n) mutable -> kj::Promise<kj::Maybe<capnp::MessageReaderAndFds>> {
+        .then([this, options, scratch, want](size_t n) mutable -> kj::Promise<kj::Maybe<capnp::MessageReaderAndFds>> {
           if (n == 0) {
             if (end_ == begin_) return kj::Maybe<capnp::MessageReaderAndFds>(kj::none);
             if (end_ - begin_ != failedAt_) {
@@ -218,7 +221,7 @@ class PackedMessageStream final : public capnp::MessageStream {
             return kj::Maybe<capnp::MessageReaderAndFds>(kj::none);
           }
           end_ += n;
-          return readLoop(options, scratch);
+          return readLoop(options, scratch, n < want);  // a short read: the peer paused
         });
   }
 

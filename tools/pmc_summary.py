@@ -14,7 +14,7 @@ import sys
 from collections import defaultdict
 
 out_dir, tag, cfg = sys.argv[1], sys.argv[2], sys.argv[3]
-KERNELS = {"unpack_tiles_kernel": "unpack_tiles", "fallback_kernel": "unpack_fallback", "header_kernel": "unpack_header",
+KERNELS = {"unpack_tiles_kernel": "unpack_tiles", "header_kernel": "unpack_header",
            "message_bits_kernel": "pack_framing", "chunk_bits_kernel": "pack_framing",
            "scan_kernel": "scan", "fill_kernel": "fill"}
 
