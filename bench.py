@@ -235,11 +235,11 @@ def cpu_baseline(sample_words, sample_off, seconds, threads):
 
 
 def measure_copy(codec, nbytes=1 << 30, reps=10):
-    """Device-to-device copy ceiling in the same run: our streaming copy kernel (16 B per lane,
-    four loads in flight per lane; capnproto_amd/csrc/cpk_stream.hip copy_kernel), best of a
-    small grid sweep, read + write bytes / time, timed with HIP events on the stream it runs
-    on.  The torch copy_ it replaces measured ~4.8 TB/s, below MI355X_MICROARCH.md's 6.29 TB/s
-    for a float4 copy."""
+    """Device-to-device copy ceiling in the same run: our streaming copy kernel (16 B per lane;
+    capnproto_amd/csrc/cpk_stream.hip copy_kernel), best over 4 or 8 loads in flight per lane,
+    default or non-temporal loads and four grid sizes, read + write bytes / time, timed with
+    HIP events on the stream it runs on.  (The torch copy_ it replaces measured ~4.8 TB/s;
+    MI355X_MICROARCH.md quotes 6.29 TB/s for a float4 copy.)"""
     import ctypes as C
 
     torch = codec.torch
@@ -249,7 +249,10 @@ def measure_copy(codec, nbytes=1 << 30, reps=10):
     s = torch.cuda.current_stream(codec.device)
     best = 0.0
     sweep = {}
-    for blocks in (2048, 4096, 8192, 16384):
+    for form in range(4):
+      for g in (4096, 8192, 16384, 32768):
+        blocks = (form << 24) | g
+
         def run():
             st = codec.lib.cpk_debug_copy(C.c_void_p(b.data_ptr()), C.c_void_p(a.data_ptr()),
                                           nbytes, blocks, C.c_void_p(s.cuda_stream))
@@ -264,7 +267,7 @@ def measure_copy(codec, nbytes=1 << 30, reps=10):
         e1.record(s)
         torch.cuda.synchronize()
         gbps = 2 * nbytes / (e0.elapsed_time(e1) / reps * 1e-3) / 1e9
-        sweep[blocks] = round(gbps, 1)
+        sweep[f"{('x4', 'x8', 'x4nt', 'x8nt')[form]}/{g}"] = round(gbps, 1)
         best = max(best, gbps)
     ok = torch.equal(a, b)
     del a, b
@@ -465,7 +468,8 @@ def summarize(res, world, copy_gbps):
             "read_only_frac": round(rd / HBM_PEAK_GBS, 4),
             "measured_copy_GBps": round(copy_gbps, 1) if copy_gbps else None,
             "measured_copy_kernel": "copy_kernel (cpk_stream.hip): 16 B/lane streaming copy, "
-                                    "best of a grid sweep, read + write bytes",
+                                    "best of a sweep over loads in flight (4, 8), cache policy "
+                                    "and grid size, read + write bytes, 1 GiB each way",
             "frac_of_measured_copy": round(rt / copy_gbps, 4) if copy_gbps else None,
             "dominant_kernel": {
                 "kernel": dom,

@@ -250,12 +250,16 @@ cpk_status pack_common(cpk_ctx* ctx, const uint64_t* d_words, uint64_t N, const 
   if (order_streams(ctx, stream) != CPK_OK) return CPK_ERR_HIP;
   const uint64_t T = cpk::kPackTileWords;
   const uint64_t ntiles = (N + T - 1) / T;
-  cpk_status st = ensure(&ctx->scratch, &ctx->scratch_size, pack_scratch_bytes(N, ntiles));
+  // a batch of one tile (a single small message) takes the direct kernel: its offset is 0, so
+  // no scan and no placement launch (two launches per call in all)
+  const bool direct = CPK_PACK_DIRECT || ntiles == 1;
+  cpk_status st = ensure(&ctx->scratch, &ctx->scratch_size,
+                         carve_pack(nullptr, N, ntiles, direct).total + 64);
   if (st != CPK_OK) return st;
-  PackScratch s = carve_pack(ctx->scratch, N, ntiles, CPK_PACK_DIRECT);
+  PackScratch s = carve_pack(ctx->scratch, N, ntiles, direct);
   if ((st = ensure_pack_bits(ctx, N, ntiles)) != CPK_OK) return st;
   uint64_t* const bits = ctx->pack_bits;
-  uint64_t* const tstarts = bits + (N + 63) / 64 + 1;
+  uint8_t* const tstarts = (uint8_t*)(bits + (N + 63) / 64 + 1);
   cpk::TileFirstJob tf;  // tile_first for the requested output positions, in the same launch
   tf.pos = d_off;
   tf.npos = n;
@@ -313,7 +317,7 @@ cpk_status pack_common(cpk_ctx* ctx, const uint64_t* d_words, uint64_t N, const 
   a.gword = s.gword;
   a.gincl = s.gincl;
   TimedLaunch tl(ctx, 0, stream);
-  if (CPK_PACK_DIRECT) {
+  if (direct) {
     e = cpk::launch_pack_direct(a, stream);
     tl.done();
     if (e != hipSuccess) clear_bits();
@@ -348,7 +352,7 @@ cpk_status ensure_hdr_desc(cpk_ctx* ctx, uint64_t n) {
 }
 
 // Zero-at-rest chunk-start bitmap of a pack of N words (+ one bit per tile).
-size_t pack_bits_words(uint64_t N, uint64_t ntiles) { return (N + 63) / 64 + 1 + (ntiles + 64) / 64 + 1; }
+size_t pack_bits_words(uint64_t N, uint64_t ntiles) { return (N + 63) / 64 + 1 + (ntiles + 16) / 8; }
 cpk_status ensure_pack_bits(cpk_ctx* ctx, uint64_t N, uint64_t ntiles) {
   const size_t need = pack_bits_words(N, ntiles);
   if (need <= ctx->pack_bits_n) return CPK_OK;

@@ -10,14 +10,12 @@
 namespace cpk {
 namespace {
 
-// Marks word p as a chunk start (and, at a pack tile start, the tile's bit).
-__device__ __forceinline__ void mark(unsigned long long* bits, unsigned long long* tstarts,
-                                     uint64_t p) {
+// Marks word p as a chunk start (and, at a pack tile start, the tile's byte: plain byte stores,
+// no atomics -- a word shared by 64 tiles, OR-ed and AND-ed by atomics, cost the tile kernel
+// half its speed in contention).
+__device__ __forceinline__ void mark(unsigned long long* bits, uint8_t* tstarts, uint64_t p) {
   atomicOr(bits + (p >> 6), 1ull << (p & 63));
-  if (p % kPackTileWords == 0 && p) {  // (tile 0 has no predecessor to read its bit)
-    const uint64_t t = p / kPackTileWords;
-    atomicOr(tstarts + (t >> 6), 1ull << (t & 63));
-  }
+  if (p % kPackTileWords == 0 && p) tstarts[p / kPackTileWords] = 1;  // (tile 0: no predecessor)
 }
 
 // Chunk-start bitmap + per-message framing status for a batch of flat messages.
@@ -26,7 +24,7 @@ __device__ __forceinline__ void mark(unsigned long long* bits, unsigned long lon
 __global__ void message_bits_kernel(const uint64_t* __restrict__ words,
                                     const uint64_t* __restrict__ off, uint64_t n,
                                     unsigned long long* __restrict__ bits,
-                                    unsigned long long* __restrict__ tstarts,
+                                    uint8_t* __restrict__ tstarts,
                                     int32_t* __restrict__ status, TileFirstJob tf,
                                     uint32_t tf_block) {
   if (run_tile_first(tf, tf_block)) return;
@@ -64,7 +62,7 @@ __global__ void message_bits_kernel(const uint64_t* __restrict__ words,
 
 __global__ void chunk_bits_kernel(const uint64_t* __restrict__ off, uint64_t n, uint64_t N,
                                   unsigned long long* __restrict__ bits,
-                                  unsigned long long* __restrict__ tstarts, TileFirstJob tf,
+                                  uint8_t* __restrict__ tstarts, TileFirstJob tf,
                                   uint32_t tf_block) {
   if (run_tile_first(tf, tf_block)) return;
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -77,22 +75,22 @@ __global__ void chunk_bits_kernel(const uint64_t* __restrict__ off, uint64_t n, 
 }  // namespace
 
 hipError_t launch_message_bits(const uint64_t* words, const uint64_t* off, uint64_t n,
-                               uint64_t* bits, uint64_t* tstarts, int32_t* status,
+                               uint64_t* bits, uint8_t* tstarts, int32_t* status,
                                const TileFirstJob& tf, hipStream_t stream) {
   const unsigned nb = (unsigned)((n + 255) / 256);
   if (nb + tile_first_blocks(tf) == 0) return hipSuccess;
   hipLaunchKernelGGL(message_bits_kernel, dim3(nb + tile_first_blocks(tf)), dim3(256), 0, stream,
-                     words, off, n, (unsigned long long*)bits, (unsigned long long*)tstarts,
+                     words, off, n, (unsigned long long*)bits, tstarts,
                      status, tf, nb);
   return hipGetLastError();
 }
 
 hipError_t launch_chunk_bits(const uint64_t* off, uint64_t n, uint64_t N, uint64_t* bits,
-                             uint64_t* tstarts, const TileFirstJob& tf, hipStream_t stream) {
+                             uint8_t* tstarts, const TileFirstJob& tf, hipStream_t stream) {
   const unsigned nb = (n == 0 && N == 0) ? 0u : (unsigned)((n + 256) / 256);
   if (nb + tile_first_blocks(tf) == 0) return hipSuccess;
   hipLaunchKernelGGL(chunk_bits_kernel, dim3(nb + tile_first_blocks(tf)), dim3(256), 0, stream,
-                     off, n, N, (unsigned long long*)bits, (unsigned long long*)tstarts, tf, nb);
+                     off, n, N, (unsigned long long*)bits, tstarts, tf, nb);
   return hipGetLastError();
 }
 

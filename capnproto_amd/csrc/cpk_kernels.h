@@ -16,7 +16,7 @@ struct PackTileArgs {
   uint64_t nwords;
   uint64_t* chunk_bits;        // bit i set <=> word i starts a chunk (word 0 always); zero at
                                // rest: each tile clears the words of its own 2048 words
-  uint64_t* tile_starts;       // bit t set <=> tile t's first word starts a chunk (read and
+  uint8_t* tile_starts;        // byte t set <=> tile t's first word starts a chunk (read and
                                // cleared by tile t - 1)
   uint64_t ntiles;
   uint8_t* out;
@@ -66,10 +66,10 @@ struct TileFirstJob {
 // pack tile of kPackTileWords words), tile_first and the zeroing of TileFirstJob::zero in one
 // launch.
 hipError_t launch_message_bits(const uint64_t* words, const uint64_t* off, uint64_t n,
-                               uint64_t* bits, uint64_t* tstarts, int32_t* status,
+                               uint64_t* bits, uint8_t* tstarts, int32_t* status,
                                const TileFirstJob& tf, hipStream_t stream);
 hipError_t launch_chunk_bits(const uint64_t* off, uint64_t n, uint64_t N, uint64_t* bits,
-                             uint64_t* tstarts, const TileFirstJob& tf, hipStream_t stream);
+                             uint8_t* tstarts, const TileFirstJob& tf, hipStream_t stream);
 
 struct UnpackArgs {
   const uint8_t* packed;        // batch of packed bytes
@@ -92,7 +92,8 @@ struct UnpackArgs {
   uint32_t* err;
   unsigned long long* stamps;   // diagnostic build only (env CPK_STAMPS), else NULL
   uint32_t debug_skip;          // diagnostic (env CPK_DEBUG_SKIP): 4 no chain-0 walks, 8 no look-back,
-                                // 16 no record batches, 32 no lists
+                                // 16 no record batches, 32 no lists; return after 64 staging and
+                                // message window, 128 chain 0, 256 entry and look-back
   const uint64_t* tile_firstpos;  // in_off[tile_first[t]]: the first message start >= tile start
   uint64_t* hdr_desc;           // the header launch's scan descriptors (zero at rest): cleared
   uint64_t hdr_nblocks;         // by the tile kernel once the headers are done (0: none)

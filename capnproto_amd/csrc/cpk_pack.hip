@@ -232,7 +232,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void p
   // decides whether this tile's open run may go on in the next tile)
   const uint64_t xi = l == 0 ? (wbase > 0 ? wbase - 1 : 0) : (tend < N ? tend : N - 1);
   const uint64_t xw0 = a.words[xi < N ? xi : N - 1];
-  const uint64_t nbi = ((T + 1) >> 6) + (uint64_t)opaque_zero();  // the next tile's bit
+  const uint64_t nbi = T + 1 + (uint64_t)opaque_zero();  // the next tile's start byte
   const uint64_t nb0 = a.tile_starts[nbi];
   typedef const __attribute__((address_space(4))) uint64_t cu64;
   const uint64_t pidx = a.pos ? *((cu64*)a.tile_first + T) : 0;  // scalar load
@@ -308,7 +308,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void p
   if (w == kWv - 1) {
     const uint32_t ntag = tag_of((uint32_t)xw0, (uint32_t)(xw0 >> 32));
     const uint32_t nnz = __popc(ntag);
-    const bool nC = (nb0 >> ((T + 1) & 63)) & 1;
+    const bool nC = nb0 != 0;
     const uint32_t lastZ = readlane32(Zm >> 7, 63) & 1u, lastR = readlane32(Rm >> 7, 63) & 1u;
     const bool nZ = ntag == 0, nR = nnz >= 7;
     const bool ns = nC || (!nZ && !nR) || (nZ && !lastZ) || (nR && !lastR);
@@ -318,8 +318,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void p
   // the chunk-start bits are zero at rest: this tile clears what only it reads (its bitmap words;
   // the bit of its successor's first word, read here and nowhere else)
   if ((l & 7) == 0 && cbi < nbitw && cbw != 0) a.chunk_bits[cbi] = 0;
-  if (w == kWv - 1 && l == 0 && ((nb0 >> ((T + 1) & 63)) & 1))
-    atomicAnd((unsigned long long*)a.tile_starts + nbi, ~(1ull << ((T + 1) & 63)));
+  if (w == kWv - 1 && l == 0 && nb0) a.tile_starts[nbi] = 0;
 
   uint32_t sm[kWv];
 #pragma unroll
@@ -796,7 +795,7 @@ pack_direct_kernel(PackTileArgs args) {
     const uint64_t cb0 = A_.chunk_bits[cbi < nbitw ? cbi : nbitw - 1];
     const uint64_t xi = l == 0 ? (wbase > 0 ? wbase - 1 : 0) : (tend < N ? tend : N - 1);
     const uint64_t xw0 = A_.words[xi < N ? xi : N - 1];
-    const uint64_t nbi = ((T + 1) >> 6) + (uint64_t)opaque_zero();  // the next tile's bit
+    const uint64_t nbi = T + 1 + (uint64_t)opaque_zero();  // the next tile's start byte
     const uint64_t nb0 = A_.tile_starts[nbi];
     const uint64_t pidx = A_.pos ? A_.tile_first[T] : 0;
     const uint64_t pi = pidx + l;
@@ -862,7 +861,7 @@ pack_direct_kernel(PackTileArgs args) {
     if (w == kWv - 1) {
       const uint32_t ntag = tag_of((uint32_t)xw0, (uint32_t)(xw0 >> 32));
       const uint32_t nnz = __popc(ntag);
-      const bool nC = (nb0 >> ((T + 1) & 63)) & 1;
+      const bool nC = nb0 != 0;
       const uint32_t lastZ = readlane32(Zm >> 7, 63) & 1u, lastR = readlane32(Rm >> 7, 63) & 1u;
       const bool nZ = ntag == 0, nR = nnz >= 7;
       const bool ns = nC || (!nZ && !nR) || (nZ && !lastZ) || (nR && !lastR);
@@ -870,8 +869,7 @@ pack_direct_kernel(PackTileArgs args) {
     }
     __syncthreads();  // ---- A: wave summaries -------------------------------------------
     if ((l & 7) == 0 && cbi < nbitw && cbw != 0) A_.chunk_bits[cbi] = 0;  // zero at rest
-    if (w == kWv - 1 && l == 0 && ((nb0 >> ((T + 1) & 63)) & 1))
-      atomicAnd((unsigned long long*)A_.tile_starts + nbi, ~(1ull << ((T + 1) & 63)));
+    if (w == kWv - 1 && l == 0 && nb0) A_.tile_starts[nbi] = 0;
 
     uint32_t sm[kWv];
 #pragma unroll

@@ -43,23 +43,22 @@ __global__ void fill_kernel(uint8_t* __restrict__ p, uint64_t n, uint8_t value) 
   if (blockIdx.x == 0 && threadIdx.x < n - 8 * nw) p[8 * nw + threadIdx.x] = value;
 }
 
-// Streaming device-to-device copy, 16 bytes per lane with four loads in flight per lane before
-// their stores: the measured HBM ceiling bench.py quotes beside the 8 TB/s spec
-// (MI355X_MICROARCH.md: 6.29 TB/s for a float4 copy).  Diagnostic, not on the codec path.
+// Streaming device-to-device copy, 16 bytes per lane with U loads in flight per lane before their
+// stores: the measured HBM ceiling bench.py quotes beside the 8 TB/s spec (MI355X_MICROARCH.md:
+// 6.29 TB/s for a float4 copy).  Diagnostic, not on the codec path.
 typedef uint32_t cu32x4 __attribute__((ext_vector_type(4)));
+template <int U, bool NT>
 __global__ __launch_bounds__(256) void copy_kernel(const cu32x4* __restrict__ src,
                                                    cu32x4* __restrict__ dst, uint64_t n16) {
   const uint64_t stride = (uint64_t)gridDim.x * 256;
   uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  for (; i + 3 * stride < n16; i += 4 * stride) {
-    const cu32x4 a = __builtin_nontemporal_load(src + i);
-    const cu32x4 b = __builtin_nontemporal_load(src + i + stride);
-    const cu32x4 c = __builtin_nontemporal_load(src + i + 2 * stride);
-    const cu32x4 d = __builtin_nontemporal_load(src + i + 3 * stride);
-    dst[i] = a;
-    dst[i + stride] = b;
-    dst[i + 2 * stride] = c;
-    dst[i + 3 * stride] = d;
+  for (; i + (U - 1) * stride < n16; i += U * stride) {
+    cu32x4 v[U];
+#pragma unroll
+    for (int k = 0; k < U; k++)
+      v[k] = NT ? __builtin_nontemporal_load(src + i + k * stride) : src[i + k * stride];
+#pragma unroll
+    for (int k = 0; k < U; k++) dst[i + k * stride] = v[k];
   }
   for (; i < n16; i += stride) dst[i] = src[i];
 }
@@ -504,8 +503,17 @@ hipError_t launch_copy(void* dst, const void* src, uint64_t nbytes, uint32_t blo
                        hipStream_t stream) {
   if (nbytes == 0) return hipSuccess;
   if (((uintptr_t)dst | (uintptr_t)src | nbytes) & 15) return hipErrorInvalidValue;
-  copy_kernel<<<blocks ? blocks : 4096, 256, 0, stream>>>((const cu32x4*)src, (cu32x4*)dst,
-                                                          nbytes / 16);
+  // blocks: low 24 bits the grid, bits 24-25 the form (0: 4 loads in flight per lane, 1: 8,
+  // 2: 4 non-temporal, 3: 8 non-temporal)
+  const unsigned g = (blocks & 0xffffffu) ? (blocks & 0xffffffu) : 4096u;
+  const auto* s16 = (const cu32x4*)src;
+  auto* d16 = (cu32x4*)dst;
+  switch ((blocks >> 24) & 3u) {
+    case 0: copy_kernel<4, false><<<g, 256, 0, stream>>>(s16, d16, nbytes / 16); break;
+    case 1: copy_kernel<8, false><<<g, 256, 0, stream>>>(s16, d16, nbytes / 16); break;
+    case 2: copy_kernel<4, true><<<g, 256, 0, stream>>>(s16, d16, nbytes / 16); break;
+    default: copy_kernel<8, true><<<g, 256, 0, stream>>>(s16, d16, nbytes / 16); break;
+  }
   return hipGetLastError();
 }
 

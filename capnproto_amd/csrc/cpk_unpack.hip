@@ -33,6 +33,18 @@ namespace cpk {
 
 namespace {
 
+// The kernel's arguments re-read from the kernarg segment (an opaque copy of its address): the
+// rare per-record paths (a record that ends or breaks its message) use these, so the many
+// pointers they touch are not hoisted into SGPRs for the whole tile (the kernel spilled SGPRs
+// to VGPR lanes and reloaded them with v_readlane inside the record loops).  Every kernel of this
+// file takes UnpackArgs as its only argument.
+typedef const __attribute__((address_space(4))) UnpackArgs KUnpackArgs;
+__device__ __forceinline__ const UnpackArgs& kua() {
+  KUnpackArgs* p = (KUnpackArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return *(const UnpackArgs*)p;  // (the compiler infers the constant address space back)
+}
+
 constexpr int kB = (int)kUnpackTileBytes;  // 4096
 constexpr int kPad = 16;
 constexpr int kDead = 1 << 24;  // chain ran into the end of the batch
@@ -428,8 +440,10 @@ struct RunJob {
 // The terminal record of message m: its end (stream readers), and, for the prefix reads of
 // PackedInputStream (size_out given in mode 1), where a failing read stops too -- the start of
 // the record that ends the input early or overshoots -- with the words decoded up to there.
-__device__ __forceinline__ void report_end(const UnpackArgs& a, uint64_t m, int32_t st,
+__device__ __forceinline__ void report_end(const UnpackArgs& a_unused, uint64_t m, int32_t st,
                                            const RunJob& job) {
+  (void)a_unused;
+  const UnpackArgs& a = kua();
   if (!a.in_end) return;
   const bool prefix = a.mode == 1 && a.size_out;
   if (st == kOK || st == kTrailing || st == kCap || (prefix && (st == kEOF || st == kOvershoot)))
@@ -437,9 +451,11 @@ __device__ __forceinline__ void report_end(const UnpackArgs& a, uint64_t m, int3
   if (prefix) a.size_out[m] = job.bw;
 }
 
-__device__ __forceinline__ int32_t handle_record(const UnpackArgs& a, const uint8_t* d, int p,
-                                                 uint64_t pabs, uint64_t wb, const MsgInfo& mi,
-                                                 RunJob* job, uint64_t word) {
+__device__ __forceinline__ int32_t handle_record(const UnpackArgs& a_unused, const uint8_t* d,
+                                                 int p, uint64_t pabs, uint64_t wb,
+                                                 const MsgInfo& mi, RunJob* job, uint64_t word) {
+  (void)a_unused;
+  const UnpackArgs& a = kua();
   job->n = 0;
   job->dst = job->src = 0;
   job->raw = false;
@@ -1320,7 +1336,7 @@ __device__ __forceinline__ void expand_records(const UnpackArgs& a, uint64_t A, 
         mi.fits = true;
         const int32_t st = handle_record(a, d, p, pabs, wb, mi, &job, word);
         if (st >= 0) {
-          a.status[m] = st;
+          kua().status[m] = st;
           report_end(a, (uint64_t)m, st, job);
         }
       }
@@ -1374,6 +1390,10 @@ unpack_tiles_kernel(UnpackArgs a) {
   const uint64_t msw = aux[l];
   lane_handoff();
   const SubTile st = make_subtile(A, P, msw, nms_tile_after);
+  if (a.debug_skip & 64) {  // diagnostic: staging + message window only
+    if (l == 0 && st.msw == 0) a.x0p[t] = 0x80000000u | (uint32_t)ballot(st.msw != 0);
+    return;
+  }
 
   // ---- chain 0 (entered at the tile's first byte): speculative walks, then the lane fixed point
   uint64_t chain = 0, runm = 0;
@@ -1386,6 +1406,7 @@ unpack_tiles_kernel(UnpackArgs a) {
       (a.debug_skip & 4) ? true : settle(d, st, chain, sx, 0, e, tm0, out, runm);
   const uint32_t x0 = readlane32((uint32_t)out, 63);
   if (l == 0) store_agent32(a.x0p + t, 0x80000000u | x0);
+  if (a.debug_skip & 128) return;  // diagnostic: + chain-0 walks and settle
   if (!settled) {
     // unreachable (the fixed point settles in at most 64 rounds): refuse the batch, write nothing
     if (l == 0) raise_error(a.err, kErrInternal);
@@ -1460,6 +1481,7 @@ unpack_tiles_kernel(UnpackArgs a) {
   }
 
   // ---- expansion -------------------------------------------------------------------------
+  if (a.debug_skip & 256) return;  // diagnostic: + the entry and the look-back
   expand_records<PLAIN>(a, A, d, aux, dep_tab, deposit_sel((uint32_t)l & 15), tm, excl, win, mfirst,
                  mlast, msw, w_tile);
 }
