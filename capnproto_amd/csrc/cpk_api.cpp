@@ -109,6 +109,70 @@ cpk_status ensure_pinned(void** p, size_t* size, size_t need) {
 // Host entry points stage through one pinned buffer and one device buffer when the whole call
 // fits in this many bytes each way (larger batches keep the per-buffer copies).
 constexpr size_t kHostIoMax = 64ull << 20;
+// Inputs up to this size are read by the kernels straight from the pinned buffer (no upload).
+constexpr size_t kZeroCopyMax = 256 << 10;
+
+// Staging of one host call.  Device buffer: [error word, 16 B][results][inputs (uploaded)]; the
+// error word is zero at rest and stands in for the context's for the call, so one download
+// brings back the error and the results together.  Pinned buffer: [inputs][error][results].
+struct HostIo {
+  uint8_t* hin;   // pinned inputs
+  uint8_t* din;   // the kernels' view of the inputs (the pinned buffer itself when small)
+  uint8_t* dres;  // device results
+  uint8_t* hres;  // pinned results
+  uint32_t* derr;
+  const uint32_t* herr;
+  bool upload;
+};
+
+cpk_status host_io(cpk_ctx* ctx, size_t in_bytes, size_t out_bytes, HostIo* io) {
+  cpk_status st;
+  if ((st = ensure_pinned(&ctx->hio, &ctx->hio_size, in_bytes + 16 + out_bytes)) != CPK_OK)
+    return st;
+  void* const before = ctx->dio;
+  if ((st = ensure(&ctx->dio, &ctx->dio_size, 16 + out_bytes + in_bytes)) != CPK_OK) return st;
+  if (ctx->dio != before && (hipMemset(ctx->dio, 0, 16) != hipSuccess ||
+                             hipDeviceSynchronize() != hipSuccess))
+    return CPK_ERR_HIP;
+  uint8_t* const hb = (uint8_t*)ctx->hio;
+  uint8_t* const db = (uint8_t*)ctx->dio;
+  io->hin = hb;
+  io->upload = in_bytes > kZeroCopyMax;
+  io->din = db + 16 + out_bytes;
+  if (!io->upload && hipHostGetDevicePointer((void**)&io->din, hb, 0) != hipSuccess)
+    return CPK_ERR_HIP;
+  io->derr = (uint32_t*)db;
+  io->dres = db + 16;
+  io->herr = (const uint32_t*)(hb + in_bytes);
+  io->hres = hb + in_bytes + 16;
+  return CPK_OK;
+}
+
+// Runs fn (the device entry point) on the staged inputs with the call's error word, then brings
+// back error and results (out_bytes) with one download and one synchronisation.
+template <class F>
+cpk_status host_io_run(cpk_ctx* ctx, const HostIo& io, size_t in_bytes, size_t out_bytes,
+                       bool* downloaded, F fn) {
+  hipStream_t s = nullptr;
+  *downloaded = false;
+  if (io.upload && hipMemcpyAsync(io.din, io.hin, in_bytes, hipMemcpyHostToDevice, s) != hipSuccess)
+    return CPK_ERR_HIP;
+  uint32_t* const saved = ctx->err;
+  ctx->err = io.derr;
+  cpk_status st = fn(s);
+  ctx->err = saved;
+  if (st != CPK_OK) return st;
+  if (hipMemcpyAsync((void*)io.herr, io.derr, 16 + out_bytes, hipMemcpyDeviceToHost, s) !=
+          hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return CPK_ERR_HIP;
+  *downloaded = true;
+  if (*io.herr) {
+    st = (cpk_status)*io.herr;
+    return hipMemset(io.derr, 0, 4) != hipSuccess ? CPK_ERR_HIP : st;
+  }
+  return CPK_OK;
+}
 
 // Carves aligned sub-buffers out of the context scratch.
 struct Carve {
@@ -213,7 +277,7 @@ PackScratch carve_pack(void* base, uint64_t N, uint64_t ntiles, bool direct) {
   s.scan_counter = c.take<uint32_t>(4);
   s.scan_desc = c.take<uint64_t>(direct ? 0 : cpk::scan_tiles(ntiles + 1));
   s.ticket = c.take<uint32_t>(4);
-  s.desc = c.take<uint64_t>(direct ? ntiles : 0);
+  s.desc = c.take<uint64_t>(ntiles);  // tile descriptors (direct kernel; tiles resolved in time)
   s.gword = c.take<uint64_t>(direct ? ntiles / 64 + 1 : 0);
   s.gincl = c.take<uint64_t>(direct ? ntiles / 64 + 1 : 0);
   s.zero_bytes = c.off;
@@ -656,42 +720,31 @@ cpk_status cpk_pack_messages_host(cpk_ctx* ctx, const uint64_t* h_words, uint64_
   const size_t in_bytes = align16(wbytes) + align16(obytes);
   const size_t out_bytes = align16(obytes) + align16(4 * nmsgs) + align16(out_capacity);
   if (in_bytes + out_bytes <= kHostIoMax) {
-    // one upload (words, offsets), the kernels, one download (offsets, statuses, packed bytes,
-    // error word), one synchronisation
-    if ((st = ensure_pinned(&ctx->hio, &ctx->hio_size, in_bytes + out_bytes + 16)) != CPK_OK ||
-        (st = ensure(&ctx->dio, &ctx->dio_size, in_bytes + out_bytes + 16)) != CPK_OK)
-      return st;
-    uint8_t* const hb = (uint8_t*)ctx->hio;
-    uint8_t* const db = (uint8_t*)ctx->dio;
-    if (wbytes) memcpy(hb, h_words, wbytes);
-    memcpy(hb + align16(wbytes), h_msg_word_off, obytes);
-    uint64_t* d_words = (uint64_t*)db;
-    uint64_t* d_off = (uint64_t*)(db + align16(wbytes));
-    uint8_t* const r = db + in_bytes;  // results: out_off | status | packed bytes
-    uint64_t* d_out_off = (uint64_t*)r;
-    int32_t* d_status = (int32_t*)(r + align16(obytes));
-    uint8_t* d_out = r + align16(obytes) + align16(4 * nmsgs);
-    hipStream_t s = nullptr;
-    if (hipMemcpyAsync(db, hb, in_bytes, hipMemcpyHostToDevice, s) != hipSuccess)
-      return CPK_ERR_HIP;
-    st = cpk_pack_messages(ctx, d_words, total_words, d_off, nmsgs, d_out, out_capacity,
-                           d_out_off, d_status, s);
-    if (st != CPK_OK) return st;
-    uint32_t* const herr = (uint32_t*)(hb + in_bytes + out_bytes);
-    if (hipMemcpyAsync(hb + in_bytes, r, out_bytes, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipMemcpyAsync(herr, ctx->err, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipStreamSynchronize(s) != hipSuccess)
-      return CPK_ERR_HIP;
-    const uint64_t* ho = (const uint64_t*)(hb + in_bytes);
-    const uint64_t total = ho[nmsgs];
-    if (h_msg_out_off) memcpy(h_msg_out_off, ho, obytes);
-    if (h_status && nmsgs) memcpy(h_status, hb + in_bytes + align16(obytes), 4 * nmsgs);
-    if (*herr) {
-      st = (cpk_status)*herr;
-      return hipMemset(ctx->err, 0, 4) != hipSuccess ? CPK_ERR_HIP : st;
+    // inputs read in place (or one upload), the kernels, one download (error word, offsets,
+    // statuses, packed bytes), one synchronisation
+    HostIo io;
+    if ((st = host_io(ctx, in_bytes, out_bytes, &io)) != CPK_OK) return st;
+    if (wbytes) memcpy(io.hin, h_words, wbytes);
+    memcpy(io.hin + align16(wbytes), h_msg_word_off, obytes);
+    const uint64_t* d_words = (const uint64_t*)io.din;
+    const uint64_t* d_off = (const uint64_t*)(io.din + align16(wbytes));
+    uint64_t* d_out_off = (uint64_t*)io.dres;  // results: out_off | status | packed bytes
+    int32_t* d_status = (int32_t*)(io.dres + align16(obytes));
+    uint8_t* d_out = io.dres + align16(obytes) + align16(4 * nmsgs);
+    bool got = false;
+    st = host_io_run(ctx, io, in_bytes, out_bytes, &got, [&](hipStream_t s) {
+      return cpk_pack_messages(ctx, d_words, total_words, d_off, nmsgs, d_out, out_capacity,
+                               d_out_off, d_status, s);
+    });
+    const uint64_t* ho = (const uint64_t*)io.hres;
+    if (got) {
+      if (h_msg_out_off) memcpy(h_msg_out_off, ho, obytes);
+      if (h_status && nmsgs) memcpy(h_status, io.hres + align16(obytes), 4 * nmsgs);
     }
+    if (st != CPK_OK) return st;
+    const uint64_t total = ho[nmsgs];
     if (total > out_capacity) return CPK_ERR_CAPACITY;
-    if (total) memcpy(h_out, hb + in_bytes + align16(obytes) + align16(4 * nmsgs), total);
+    if (total) memcpy(h_out, io.hres + align16(obytes) + align16(4 * nmsgs), total);
     return CPK_OK;
   }
   if ((st = ensure(&ctx->stage[0], &ctx->stage_size[0], wbytes + 16)) != CPK_OK) return st;
@@ -816,42 +869,31 @@ cpk_status cpk_unpack_messages_host(cpk_ctx* ctx, const uint8_t* h_packed, uint6
   const size_t in_bytes = align16(total_bytes) + align16(obytes);
   const size_t out_bytes = align16(obytes) + align16(4 * nmsgs) + align16(words_capacity * 8);
   if (in_bytes + out_bytes <= kHostIoMax) {
-    // one upload (packed bytes, offsets), the kernels, one download (word offsets, statuses,
-    // words, error word), one synchronisation
-    if ((st = ensure_pinned(&ctx->hio, &ctx->hio_size, in_bytes + out_bytes + 16)) != CPK_OK ||
-        (st = ensure(&ctx->dio, &ctx->dio_size, in_bytes + out_bytes + 16)) != CPK_OK)
-      return st;
-    uint8_t* const hb = (uint8_t*)ctx->hio;
-    uint8_t* const db = (uint8_t*)ctx->dio;
-    if (total_bytes) memcpy(hb, h_packed, total_bytes);
-    memcpy(hb + align16(total_bytes), h_msg_in_off, obytes);
-    const uint8_t* d_packed = db;
-    const uint64_t* d_in_off = (const uint64_t*)(db + align16(total_bytes));
-    uint8_t* const r = db + in_bytes;  // results: word offsets | status | words
-    uint64_t* d_word_off = (uint64_t*)r;
-    int32_t* d_status = (int32_t*)(r + align16(obytes));
-    uint64_t* d_words = (uint64_t*)(r + align16(obytes) + align16(4 * nmsgs));
-    hipStream_t s = nullptr;
-    if (hipMemcpyAsync(db, hb, in_bytes, hipMemcpyHostToDevice, s) != hipSuccess)
-      return CPK_ERR_HIP;
-    st = cpk_unpack_messages(ctx, d_packed, total_bytes, d_in_off, nmsgs, d_words,
-                             words_capacity, d_word_off, d_status, limits, s);
-    if (st != CPK_OK) return st;
-    uint32_t* const herr = (uint32_t*)(hb + in_bytes + out_bytes);
-    if (hipMemcpyAsync(hb + in_bytes, r, out_bytes, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipMemcpyAsync(herr, ctx->err, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipStreamSynchronize(s) != hipSuccess)
-      return CPK_ERR_HIP;
-    const uint64_t* hw = (const uint64_t*)(hb + in_bytes);
-    if (h_msg_word_off) memcpy(h_msg_word_off, hw, obytes);
-    if (h_status && nmsgs) memcpy(h_status, hb + in_bytes + align16(obytes), 4 * nmsgs);
-    if (*herr) {
-      st = (cpk_status)*herr;
-      return hipMemset(ctx->err, 0, 4) != hipSuccess ? CPK_ERR_HIP : st;
+    // inputs read in place (or one upload), the kernels, one download (error word, word
+    // offsets, statuses, words), one synchronisation
+    HostIo io;
+    if ((st = host_io(ctx, in_bytes, out_bytes, &io)) != CPK_OK) return st;
+    if (total_bytes) memcpy(io.hin, h_packed, total_bytes);
+    memcpy(io.hin + align16(total_bytes), h_msg_in_off, obytes);
+    const uint8_t* d_packed = io.din;
+    const uint64_t* d_in_off = (const uint64_t*)(io.din + align16(total_bytes));
+    uint64_t* d_word_off = (uint64_t*)io.dres;  // results: word offsets | status | words
+    int32_t* d_status = (int32_t*)(io.dres + align16(obytes));
+    uint64_t* d_words = (uint64_t*)(io.dres + align16(obytes) + align16(4 * nmsgs));
+    bool got = false;
+    st = host_io_run(ctx, io, in_bytes, out_bytes, &got, [&](hipStream_t s) {
+      return cpk_unpack_messages(ctx, d_packed, total_bytes, d_in_off, nmsgs, d_words,
+                                 words_capacity, d_word_off, d_status, limits, s);
+    });
+    const uint64_t* hw = (const uint64_t*)io.hres;
+    if (got) {
+      if (h_msg_word_off) memcpy(h_msg_word_off, hw, obytes);
+      if (h_status && nmsgs) memcpy(h_status, io.hres + align16(obytes), 4 * nmsgs);
     }
+    if (st != CPK_OK) return st;
     const uint64_t total = hw[nmsgs];
     const uint64_t n = total < words_capacity ? total : words_capacity;
-    if (n) memcpy(h_words, hb + in_bytes + align16(obytes) + align16(4 * nmsgs), n * 8);
+    if (n) memcpy(h_words, io.hres + align16(obytes) + align16(4 * nmsgs), n * 8);
     return CPK_OK;
   }
   if ((st = ensure(&ctx->stage[0], &ctx->stage_size[0], words_capacity * 8 + 16)) != CPK_OK)

@@ -174,6 +174,84 @@ __device__ __forceinline__ bool sum_simple(uint32_t s) { return (s >> 1) & 1u; }
 __device__ __forceinline__ uint32_t sum_fsw(uint32_t s) { return (s >> 2) & 0x3ffu; }
 __device__ __forceinline__ uint32_t sum_exit(uint32_t s) { return (s >> 16) & 0xffu; }
 
+#ifndef CPK_PACK_OPP
+#define CPK_PACK_OPP 1  // 0: every tile goes through its scratch slot and the placement launch
+#endif
+
+// Non-blocking look-back for tile t (one wave): the exclusive byte prefix from the descriptors
+// of up to 512 predecessors, or false when one before the nearest inclusive prefix has not
+// published its byte count yet.
+__device__ __forceinline__ bool try_lookback(const uint64_t* desc, uint64_t t, uint64_t* out) {
+  constexpr int K = 4;
+  const int l = lane_id() + (int)opaque_zero();  // (addresses not hoisted out of the caller's loop)
+  uint64_t excl = 0;
+  int64_t j = (int64_t)t - 1;
+  for (int round = 0; round < 2; round++) {
+    uint64_t d[K];
+#pragma unroll
+    for (int i = 0; i < K; i++) {
+      const int64_t idx = j - (64 * i + l);
+      d[i] = idx >= 0 ? load_agent(desc + idx) : kDescIncl;
+    }
+    int stop_at = 64 * K, blocked = 64 * K;
+#pragma unroll
+    for (int i = K - 1; i >= 0; i--) {
+      const uint64_t f = d[i] & kDescFlags;
+      const uint64_t sb = ballot(f == kDescIncl), nb = ballot(f == 0);
+      if (sb) stop_at = 64 * i + lowest_bit(sb);
+      if (nb) blocked = 64 * i + lowest_bit(nb);
+    }
+    if (blocked < stop_at) return false;
+    uint64_t contrib = 0;
+#pragma unroll
+    for (int i = 0; i < K; i++)
+      if (64 * i + l <= stop_at) contrib += d[i] & kDescValue;
+    excl += wave_sum64(contrib);
+    if (stop_at < 64 * K) {
+      *out = excl;
+      return true;
+    }
+    j -= 64 * K;
+  }
+  return false;
+}
+
+// The staged tile (tile byte j at stg byte kPadF + j, n bytes) to o0 (any alignment), all
+// threads of the workgroup: 16-byte stores in the body, byte stores at both ends and in the one
+// 16-byte block holding `hole` (a count byte the next tile writes; ~0: none), which is skipped.
+__device__ __forceinline__ void copy_out_final(const uint32_t* stg, uint32_t n, uint8_t* o0,
+                                               uint32_t hole, int tid) {
+  const uint8_t* const sb = (const uint8_t*)stg + kPadF;
+  const uint64_t A0 = (uint64_t)(uintptr_t)o0;
+  const uint64_t A1 = A0 + n;
+  const uint64_t al = (A0 + 15) & ~15ull;
+  const uint32_t head = (uint32_t)((al < A1 ? al : A1) - A0);
+  if ((uint32_t)tid < head && (uint32_t)tid != hole) o0[tid] = sb[tid];
+  if (A1 <= al) return;
+  const uint32_t body = (uint32_t)((A1 & ~15ull) - A0);
+  const uint32_t nblk = (body - head) >> 4;
+  const uint32_t sbyte = kPadF + head;
+  const uint32_t rr = sbyte & 3u;
+  u32x4* const ob = (u32x4*)(o0 + head);
+  for (uint32_t i = tid; i < nblk; i += 64 * kWv) {
+    const uint32_t b0 = head + 16 * i;
+    if (hole - b0 < 16u) {
+      for (uint32_t q = 0; q < 16; q++)
+        if (b0 + q != hole) o0[b0 + q] = sb[b0 + q];
+      continue;
+    }
+    const uint32_t d = (sbyte >> 2) + 4 * i;
+    const uint32_t v0 = stg[d], v1 = stg[d + 1], v2 = stg[d + 2], v3 = stg[d + 3], v4 = stg[d + 4];
+    u32x4 v;
+    v.x = __builtin_amdgcn_alignbyte(v1, v0, rr);
+    v.y = __builtin_amdgcn_alignbyte(v2, v1, rr);
+    v.z = __builtin_amdgcn_alignbyte(v3, v2, rr);
+    v.w = __builtin_amdgcn_alignbyte(v4, v3, rr);
+    ob[i] = v;
+  }
+  if (body + (uint32_t)tid < n && body + (uint32_t)tid != hole) o0[body + tid] = sb[body + tid];
+}
+
 // ---------------------------------------------------------------------------------------------
 // 1. Tile kernel: one workgroup per 2048-word tile, in blockIdx order.  The tile's packed bytes
 //    go to its own scratch slot (scr + T * kScr, 16-byte aligned), with its byte count, the
@@ -190,6 +268,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void p
   __shared__ uint32_t s_sum[kWv];    // wave summaries (sum_pack)
   __shared__ uint32_t s_bytes[kWv];  // wave byte counts
   __shared__ uint32_t s_sexit[kWv];  // serial mode: exit of each wave
+  __shared__ uint32_t s_hole;        // byte of the tile's provisional count (~0: none)
+  __shared__ uint64_t s_dst;         // the tile's output offset when resolved in time (~0: not)
+  __shared__ uint32_t s_patch;       // previous tile's count byte | its distance before ours << 8
 
   const int tid = (int)threadIdx.x;
   const int l = lane_id();
@@ -418,13 +499,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void p
       // its count byte (written here as if the batch ended at the tile end) is final only
       // once the next tile has seen where the run stops.
       const uint32_t b = t_exit & 0xffu;
-      a.thole[T] = (b != 0 && !next_sync) ? agg - 1u - ((t_exit & 0x100u) ? 8u * (255u - b) : 0u)
-                                           : 0xffffffffu;
+      const uint32_t hole = (b != 0 && !next_sync)
+                                ? agg - 1u - ((t_exit & 0x100u) ? 8u * (255u - b) : 0u)
+                                : 0xffffffffu;
+      a.thole[T] = hole;
+      s_hole = hole;
     }
     if (w == 0) {
-      // the previous tile's open run ends in this tile: its count byte
+      // the previous tile's open run ends in this tile: its count byte, and how far before this
+      // tile's first byte it lies
       const uint32_t b = bT & 0xffu;
-      a.tpatch[T] = b != 0 ? 0x100u | (255u - b + (s0 < b ? s0 : b)) : 0u;
+      const uint32_t tpv = b != 0 ? 0x100u | (255u - b + (s0 < b ? s0 : b)) : 0u;
+      a.tpatch[T] = tpv;
+#if CPK_PACK_OPP
+      s_patch = tpv ? (tpv & 0xffu) | ((1u + ((bT & 0x100u) ? 8u * (255u - b) : 0u)) << 8) : 0u;
+      // the tile's byte count, for the look-back of the tiles after it (tile 0: its prefix too)
+      store_agent(a.desc + T, (T == 0 ? kDescIncl : kDescAgg) | agg);
+#endif
     }
   }
 
@@ -513,6 +604,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void p
       __builtin_amdgcn_sched_barrier(0);
     }
     __syncthreads();  // ---- C: staged ------------------------------------------------------
+#if CPK_PACK_OPP
+    if (!windowed) {
+      // The tile's offset, if the tiles before it have all published their byte counts by now
+      // (no waiting): then its bytes go straight to the output and the placement launch skips it.
+      if (w == 0) {
+        uint64_t ex = 0;
+        bool ok = T == 0 || try_lookback(a.desc, T, &ex);
+        ok = ok && ex + agg <= a.out_capacity;
+        if (l == 0) {
+          if (ok && T != 0) store_agent(a.desc + T, kDescIncl | (ex + agg));
+          s_dst = ok ? ex : ~0ull;
+        }
+      }
+      __syncthreads();  // ---- D: offset ----------------------------------------------------
+      const uint64_t ex = uniform64(s_dst);
+      if (ex != ~0ull) {
+        copy_out_final(stg, agg, a.out + ex, uniform32(s_hole), tid);
+        // the previous tile's provisional count byte, now final (its tile left it out)
+        const uint32_t pt = uniform32(s_patch);
+        if (tid == 0 && pt != 0) a.out[ex - (pt >> 8)] = (uint8_t)pt;
+        return;
+      }
+    }
+#endif
     // the window's bytes to the tile's scratch slot: aligned 16-byte copies
     const uint32_t n16 = ((whi < agg ? whi : agg) - wlo + 15u) >> 4;
     for (uint32_t i = tid; i < n16; i += 64 * kWv) dst[(wlo >> 4) + i] = ((const u32x4*)stg)[1 + i];
@@ -1137,9 +1252,18 @@ __global__ __launch_bounds__(256) void pack_place_kernel(PackTileArgs a) {
   const uint64_t off = a.tile_off[T];
   const uint32_t n = (uint32_t)(a.tile_off[T + 1] - off);
   const uint64_t total = a.tile_off[a.ntiles];
+  // (a tile whose offset was known in time wrote its bytes itself: INCL descriptor, one staging
+  // window; tile 0 publishes INCL before it knows)
+  const bool placed = CPK_PACK_OPP && (a.desc[T] & kDescFlags) == kDescIncl && n <= kCap;
   if (total > a.out_capacity) {
     if (T == 0 && l == 0) raise_error(a.err, kErrCapacity);
-  } else if (n) {
+  } else if (!placed && n) {
+    // the previous tile's count byte that this tile finishes (the previous tile may have left it
+    // out, having written its bytes itself)
+    if (CPK_PACK_OPP && T > 0 && l == 0) {
+      const uint32_t ph = a.thole[T - 1], pp = a.tpatch[T];
+      if (ph != 0xffffffffu && pp) a.out[a.tile_off[T - 1] + ph] = (uint8_t)pp;
+    }
     // count byte patched by the next tile (position, value) -- wave-uniform
     const uint32_t hole = T + 1 < a.ntiles ? a.thole[T] : 0xffffffffu;
     const uint32_t pv = hole != 0xffffffffu ? a.tpatch[T + 1] : 0u;

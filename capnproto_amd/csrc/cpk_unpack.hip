@@ -31,6 +31,11 @@
 
 namespace cpk {
 
+#ifdef CPK_DIAG
+// diagnostic build only (-DCPK_DIAG): per-phase step counters, read by cpk_debug_diag
+__device__ unsigned long long g_diag[16];
+#endif
+
 namespace {
 
 // The kernel's arguments re-read from the kernarg segment (an opaque copy of its address): the
@@ -48,6 +53,22 @@ __device__ __forceinline__ const UnpackArgs& kua() {
 constexpr int kB = (int)kUnpackTileBytes;  // 4096
 constexpr int kPad = 16;
 constexpr int kDead = 1 << 24;  // chain ran into the end of the batch
+
+#ifdef CPK_DIAG
+__device__ __forceinline__ void diag_add(int k, uint64_t v) {
+  if (lane_id() == 0) atomicAdd(&g_diag[k], (unsigned long long)v);
+}
+// wave-level trip count (max over lanes) and lane-step total of a per-lane count n
+__device__ __forceinline__ void diag_trips(int k, int n) {
+  const uint32_t mx = readlane32(wave_incl_max32((uint32_t)n), 63);
+  const uint32_t sm = readlane32(wave_incl_sum32((uint32_t)n), 63);
+  diag_add(k, mx);
+  diag_add(k + 1, sm);
+}
+#define CPK_DIAG_ONLY(x) x
+#else
+#define CPK_DIAG_ONLY(x)
+#endif
 constexpr int kMergeCap = 48;               // entry-walk records before the jump walk
 
 // status codes (include/cpk.h)
@@ -228,7 +249,9 @@ __global__ __launch_bounds__(256) void header_kernel(
 // Byte length of a record from its tag and its count byte (tag 0x00: + count byte; 0xff: +
 // count byte + 8*count raw bytes).
 __device__ __forceinline__ int rec_len(uint32_t tag, uint32_t cnt) {
-  return 1 + __popc(tag) + ((tag == 0 || tag == 0xff) ? 1 : 0) + (tag == 0xff ? 8 * (int)cnt : 0);
+  // (tag - 1 >= 0xfe: tag 0x00 or 0xff, in 32-bit arithmetic -- no 16-bit byte compares)
+  const uint32_t run = tag - 1u >= 0xfeu ? 2u : 1u;
+  return (int)(__popc(tag) + run + ((tag == 0xffu ? cnt : 0u) << 3));
 }
 
 // Staged tile bytes: tile byte p at d[p], zero past the batch end, kPad bytes past the tile, so
@@ -266,16 +289,19 @@ __device__ __forceinline__ int step_len(uint32_t t, uint32_t c9) { return rec_le
 // only moves when the chain reaches it (rare), so the step itself carries no message logic.
 // Returns the position reached.  (Sub-tiles are 64-byte aligned in the tile: bit p & 63.)
 __device__ __forceinline__ int walk(const uint8_t* d, const SubTile& st, int p, uint64_t stop,
-                                    uint64_t* marks, uint64_t* runs = nullptr) {
+                                    uint64_t* marks, uint64_t* runs = nullptr, int* nstep = nullptr) {
   uint64_t m = 0, rm = 0;
   if (st.no_starts) {
     // no message start in the tile: the only clip is the first start after the sub-tile, where
     // the walk ends anyway (most tiles of large messages)
     while (p < st.vend) {
-      const uint32_t e = d[p], c9 = d[p + 9];
+      if (nstep) ++*nstep;
+      uint32_t e = d[p];
+      const uint32_t c9 = d[p + 9];
+      asm("" : "+v"(e));  // a plain 32-bit value: 32-bit compares, no 16-bit byte arithmetic
       const uint64_t bit = 1ull << (p & 63);
       m |= bit;
-      if (e == 0 || e == 0xff) rm |= bit;
+      if (e - 1u >= 0xfeu) rm |= bit;
       const int np = p + step_len(e, c9);
       p = np < st.nms_after ? np : st.nms_after;
       if (p < st.vend && ((stop >> (p & 63)) & 1)) break;
@@ -286,10 +312,13 @@ __device__ __forceinline__ int walk(const uint8_t* d, const SubTile& st, int p, 
   }
   int nm = next_start_after(st, p);
   while (p < st.vend) {
-    const uint32_t e = d[p], c9 = d[p + 9];
+    if (nstep) ++*nstep;
+    uint32_t e = d[p];
+    const uint32_t c9 = d[p + 9];
+    asm("" : "+v"(e));
     const uint64_t bit = 1ull << (p & 63);
     m |= bit;
-    if (e == 0 || e == 0xff) rm |= bit;
+    if (e - 1u >= 0xfeu) rm |= bit;
     int np = p + step_len(e, c9);
     if (np >= nm) {
       np = nm;
@@ -319,7 +348,10 @@ __device__ __forceinline__ bool settle(const uint8_t* d, const SubTile& st, uint
   out = pass ? (e >= st.pend ? kDead : e) : sx;
   tm = pass ? 0ull : chain;
   for (int iter = 0; iter < 96; iter++) {
-    if (iters) *iters = iter + 1;
+    if (iters) iters[0] = iter + 1;
+#ifdef CPK_DIAG
+    if (iter) diag_trips(3, iters[1] - iters[2]), iters[2] = iters[1];
+#endif
     // the largest exit of the earlier lanes (wave_shr:1 of the inclusive max: no LDS trip)
     const uint32_t incl = wave_incl_max32(pass ? 0u : (uint32_t)out);
     const int prev = (int)wave_shr1_32(incl);
@@ -336,7 +368,13 @@ __device__ __forceinline__ bool settle(const uint8_t* d, const SubTile& st, uint
       tm = chain & ~mask_lt(e - st.s);
     } else {
       uint64_t wm, wr;
+#ifdef CPK_DIAG
+      int ns = 0;
+      const int p = walk(d, st, e, chain, &wm, &wr, &ns);
+      if (iters) iters[1] += ns;
+#else
       const int p = walk(d, st, e, chain, &wm, &wr);
+#endif
       runm |= wr;
       if (p != kDead && p < st.vend) {
         out = sx;
@@ -880,6 +918,7 @@ __device__ uint64_t enter_chain(const uint8_t* d, uint64_t* aux, const SubTile& 
     }
     done = steps < kMergeCap;
   }
+  CPK_DIAG_ONLY(diag_add(6, 1); diag_add(7, readlane32((uint32_t)steps, 0)); diag_add(8, !readlane32(done, 0)));
   if (!readlane32(done, 0)) {
     p = (int)readlane32((uint32_t)p, 0);
     cur = (int)readlane32((uint32_t)cur, 0);
@@ -1398,12 +1437,22 @@ unpack_tiles_kernel(UnpackArgs a) {
   // ---- chain 0 (entered at the tile's first byte): speculative walks, then the lane fixed point
   uint64_t chain = 0, runm = 0;
   int sx = kDead;
+#ifdef CPK_DIAG
+  int dn = 0, dit[3] = {0, 0, 0};
+  if (st.s < st.pend && !(a.debug_skip & 4)) sx = walk(d, st, st.s, 0, &chain, &runm, &dn);
+  diag_add(0, 1);
+  diag_trips(1, dn);
+  int* const diag_it = dit;
+#else
   if (st.s < st.pend && !(a.debug_skip & 4)) sx = walk(d, st, st.s, 0, &chain, &runm);
+  int* const diag_it = nullptr;
+#endif
   int e = st.s;
   uint64_t tm0 = 0;
   int out = st.end;
   const bool settled =
-      (a.debug_skip & 4) ? true : settle(d, st, chain, sx, 0, e, tm0, out, runm);
+      (a.debug_skip & 4) ? true : settle(d, st, chain, sx, 0, e, tm0, out, runm, diag_it);
+  CPK_DIAG_ONLY(diag_add(5, dit[0]));
   const uint32_t x0 = readlane32((uint32_t)out, 63);
   if (l == 0) store_agent32(a.x0p + t, 0x80000000u | x0);
   if (a.debug_skip & 128) return;  // diagnostic: + chain-0 walks and settle
@@ -1422,6 +1471,7 @@ unpack_tiles_kernel(UnpackArgs a) {
   const int lastms = highest_bit(msin);
   const uint64_t hm = ballot(lastms >= 0);
   const bool has_start = hm != 0;
+  CPK_DIAG_ONLY(diag_add(11, has_start));
   if (has_start) {
     const int lm = highest_bit(hm);
     const uint64_t from = l > lm ? ~0ull : (l == lm ? ~mask_lt(lastms) : 0ull);
@@ -1456,6 +1506,7 @@ unpack_tiles_kernel(UnpackArgs a) {
     uint32_t xprev = xp;
     if (!(a.debug_skip & 8)) excl = lookback_tiles(a, t, &xprev);
     const uint32_t E = entry_from_exit(xprev, fms);
+    CPK_DIAG_ONLY(diag_add(9, E != Eopt); diag_add(10, Eopt > 0 && Eopt < fms));
     if (E != Eopt) {
       // the predecessor's chain did not lead where its chain 0 does
       runs = runm;
@@ -1547,3 +1598,19 @@ hipError_t launch_unpack_stage(int stage, const UnpackArgs& a, hipStream_t strea
 }
 
 }  // namespace cpk
+
+#ifdef CPK_DIAG
+// diagnostic build only: copies out (and optionally zeroes) the unpack step counters
+//  0 tiles  1/2 chain-0 walk trips (wave max / lane sum)  3/4 settle re-walk trips (max / sum)
+//  5 settle rounds  6 enter_chain calls  7 lane-0 merge steps  8 merges past the cap
+//  9 entries that differed from the optimistic one  10 optimistic entries walked  11 tiles with a start
+extern "C" int cpk_debug_diag(uint64_t* out, int reset) {
+  if (hipDeviceSynchronize() != hipSuccess) return 10;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(cpk::g_diag), 16 * sizeof(uint64_t)) != hipSuccess) return 10;
+  if (reset) {
+    const uint64_t z[16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(cpk::g_diag), z, sizeof z) != hipSuccess) return 10;
+  }
+  return 0;
+}
+#endif
