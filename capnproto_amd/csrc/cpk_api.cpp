@@ -248,8 +248,6 @@ cpk_status order_streams(cpk_ctx* ctx, hipStream_t s) {
 struct PackScratch {
   uint32_t* state;
   uint64_t* bits;
-  uint32_t* scan_counter;
-  uint64_t* scan_desc;
   uint32_t* ticket;
   uint64_t* desc;
   uint64_t* gword;
@@ -264,9 +262,9 @@ struct PackScratch {
   size_t total;
 };
 
-// Pack scratch: the zeroed part (exit budgets polled by the next tile, the scan's descriptors;
-// zeroed by the framing launch), then per tile the first requested position, byte count,
-// offset, count-byte patch, and the tile's slot for its packed bytes.  (The chunk-start bitmap
+// Pack scratch: the zeroed part (exit budgets polled by the next tile, the tiles' look-back
+// descriptors; zeroed by the framing launch), then per tile the first requested position, byte
+// count, count-byte patch, and the tile's slot for its packed bytes.  (The chunk-start bitmap
 // is zero at rest in its own buffer, ctx->pack_bits.)
 PackScratch carve_pack(void* base, uint64_t N, uint64_t ntiles, bool direct) {
   (void)N;
@@ -274,8 +272,6 @@ PackScratch carve_pack(void* base, uint64_t N, uint64_t ntiles, bool direct) {
   PackScratch s;
   s.bits = nullptr;
   s.state = c.take<uint32_t>(ntiles);
-  s.scan_counter = c.take<uint32_t>(4);
-  s.scan_desc = c.take<uint64_t>(direct ? 0 : cpk::scan_tiles(ntiles + 1));
   s.ticket = c.take<uint32_t>(4);
   s.desc = c.take<uint64_t>(ntiles);  // tile descriptors (direct kernel; tiles resolved in time)
   s.gword = c.take<uint64_t>(direct ? ntiles / 64 + 1 : 0);
@@ -291,7 +287,7 @@ PackScratch carve_pack(void* base, uint64_t N, uint64_t ntiles, bool direct) {
   }
   s.tile_first = c.take<uint64_t>(ntiles);
   s.tile_bytes = c.take<uint64_t>(ntiles);
-  s.tile_off = c.take<uint64_t>(ntiles + 1);
+  s.tile_off = nullptr;
   s.thole = c.take<uint32_t>(ntiles);
   s.tpatch = c.take<uint32_t>(ntiles);
   s.scr = c.take<uint8_t>(ntiles * cpk::kPackScratchBytes + 16);
@@ -387,12 +383,10 @@ cpk_status pack_common(cpk_ctx* ctx, const uint64_t* d_words, uint64_t N, const 
     if (e != hipSuccess) clear_bits();
     return hip_status(e);
   }
-  // tiles -> scratch slots, scan of the tile byte counts, scratch -> output
+  // tiles -> output (offset known in time) or scratch slots; the rest placed by the look-back
+  // of the placement launch
   e = cpk::launch_pack_tiles(a, stream);
   if (e != hipSuccess) clear_bits();
-  if (e == hipSuccess)
-    e = cpk::launch_exclusive_scan(s.tile_bytes, ntiles, s.tile_off, s.scan_counter, s.scan_desc,
-                                   ctx->err, stream);
   if (e == hipSuccess) e = cpk::launch_pack_place(a, stream);
   tl.done();
   return hip_status(e);

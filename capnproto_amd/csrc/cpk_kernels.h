@@ -30,21 +30,22 @@ struct PackTileArgs {
   // scratch
   uint32_t* state;             // ntiles exit budgets (0x80000000 | raw << 8 | budget), zeroed
   uint64_t* tile_bytes;        // ntiles packed bytes per tile
-  uint64_t* tile_off;          // ntiles + 1: their exclusive scan
+  uint64_t* tile_off;          // (unused: offsets come from the descriptors' look-back)
   uint8_t* scr;                // per-tile slots (ntiles * kPackScratchBytes + 16)
   uint32_t* thole;             // byte of a tile's provisional count (~0: none)
   uint32_t* tpatch;            // the next tile's final value for it (0x100 | v; 0: none)
   uint32_t* err;
-  // direct pack (pack_direct_kernel), all zeroed: tile tickets, tile AGG descriptors, per
-  // 64-tile group (count << 48) + bytes, per group the inclusive byte prefix
+  // zeroed: tile tickets (direct kernel), tile descriptors (AGG | bytes, INCL | inclusive prefix;
+  // both kernels), per 64-tile group (count << 48) + bytes and the groups' inclusive byte prefix
+  // (direct kernel)
   uint32_t* ticket;
   uint64_t* desc;
   uint64_t* gword;
   uint64_t* gincl;
 };
 
-// tiles -> scratch slots (tile_bytes, thole, tpatch), then (after the scan of tile_bytes into
-// tile_off) scratch -> out
+// tiles -> out when the tile's offset is known in time, else its scratch slot (tile_bytes, thole,
+// tpatch, desc); then placement: offsets by look-back over desc, scratch -> out
 hipError_t launch_pack_tiles(const PackTileArgs& a, hipStream_t stream);
 hipError_t launch_pack_place(const PackTileArgs& a, hipStream_t stream);
 // tiles -> out directly (persistent, ticketed, two-level look-back resolved one tile late): no

@@ -511,11 +511,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void p
       const uint32_t b = bT & 0xffu;
       const uint32_t tpv = b != 0 ? 0x100u | (255u - b + (s0 < b ? s0 : b)) : 0u;
       a.tpatch[T] = tpv;
-#if CPK_PACK_OPP
       s_patch = tpv ? (tpv & 0xffu) | ((1u + ((bT & 0x100u) ? 8u * (255u - b) : 0u)) << 8) : 0u;
       // the tile's byte count, for the look-back of the tiles after it (tile 0: its prefix too)
       store_agent(a.desc + T, (T == 0 ? kDescIncl : kDescAgg) | agg);
-#endif
     }
   }
 
@@ -1241,28 +1239,38 @@ pack_direct_kernel(PackTileArgs args) {
 
 // ---------------------------------------------------------------------------------------------
 // 2. Placement: one wave per tile moves the tile's bytes from its scratch slot to their final
-//    place (out + tile_off[T], from the scan of the tile byte counts), writing the final count
-//    byte of a run the next tile closed, and turns the tile's requested positions into output
-//    offsets.  (A tile's bytes are a few KiB at most: a whole workgroup per tile spent more on
+//    place, writing the final count byte of a run the next tile closed, and turns the tile's
+//    requested positions into output offsets.  The tile's offset: its inclusive descriptor when
+//    the tile kernel resolved it (and then wrote the bytes itself), else a decoupled look-back
+//    over the tile kernel's byte counts (AGG) and this launch's inclusive prefixes -- no separate
+//    scan launch.  (A tile's bytes are a few KiB at most: a whole workgroup per tile spent more on
 //    its own start than on the copy.)
 __global__ __launch_bounds__(256) void pack_place_kernel(PackTileArgs a) {
   const int l = lane_id();
   const uint64_t T = (uint64_t)blockIdx.x * 4 + uniform32(threadIdx.x >> 6);
   if (T >= a.ntiles) return;
-  const uint64_t off = a.tile_off[T];
-  const uint32_t n = (uint32_t)(a.tile_off[T + 1] - off);
-  const uint64_t total = a.tile_off[a.ntiles];
+  const uint32_t n = (uint32_t)a.tile_bytes[T];
+  const uint64_t dT = uniform64(load_agent(a.desc + T));
+  const bool incl = (dT & kDescFlags) == kDescIncl;
+  uint64_t off;
+  if (incl) {
+    off = (dT & kDescValue) - n;
+  } else {
+    off = lookback<8>(a.desc, T, a.err);
+    if (l == 0) store_agent(a.desc + T, kDescIncl | (off + n));
+  }
+  const uint64_t total = off + n;  // (the batch total on the last tile)
   // (a tile whose offset was known in time wrote its bytes itself: INCL descriptor, one staging
   // window; tile 0 publishes INCL before it knows)
-  const bool placed = CPK_PACK_OPP && (a.desc[T] & kDescFlags) == kDescIncl && n <= kCap;
-  if (total > a.out_capacity) {
-    if (T == 0 && l == 0) raise_error(a.err, kErrCapacity);
+  const bool placed = CPK_PACK_OPP && incl && n <= kCap;
+  if (off + n > a.out_capacity) {
+    if (l == 0) raise_error(a.err, kErrCapacity);
   } else if (!placed && n) {
     // the previous tile's count byte that this tile finishes (the previous tile may have left it
     // out, having written its bytes itself)
     if (CPK_PACK_OPP && T > 0 && l == 0) {
       const uint32_t ph = a.thole[T - 1], pp = a.tpatch[T];
-      if (ph != 0xffffffffu && pp) a.out[a.tile_off[T - 1] + ph] = (uint8_t)pp;
+      if (ph != 0xffffffffu && pp) a.out[off - a.tile_bytes[T - 1] + ph] = (uint8_t)pp;
     }
     // count byte patched by the next tile (position, value) -- wave-uniform
     const uint32_t hole = T + 1 < a.ntiles ? a.thole[T] : 0xffffffffu;
