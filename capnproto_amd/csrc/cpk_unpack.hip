@@ -388,6 +388,24 @@ __device__ __forceinline__ bool settle(const uint8_t* d, const SubTile& st, uint
   return false;
 }
 
+// Positions j of the lane's sub-tile [s, s + 64) with d[s + j] == d[s + j + 9] == 0xff: the head
+// of a raw record of 255 words (or two 0xff bytes 9 apart).
+__device__ __forceinline__ uint64_t ff_heads(const uint8_t* d, int s) {
+  const uint32_t* const w = (const uint32_t*)(d + s);
+  uint64_t m = 0;
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    const uint32_t y = ~w[k];  // 0xff bytes -> zero bytes
+    uint32_t f = ~(((y & 0x7f7f7f7fu) + 0x7f7f7f7fu) | y) & 0x80808080u;
+    while (f) {
+      const int b = __builtin_ctz(f) >> 3;
+      f &= f - 1;
+      if (d[s + 4 * k + b + 9] == 0xff) m |= 1ull << (4 * k + b);
+    }
+  }
+  return m;
+}
+
 struct Rec {
   uint32_t tag;
   int hb;       // tag + data bytes
@@ -1453,7 +1471,31 @@ unpack_tiles_kernel(UnpackArgs a) {
   const bool settled =
       (a.debug_skip & 4) ? true : settle(d, st, chain, sx, 0, e, tm0, out, runm, diag_it);
   CPK_DIAG_ONLY(diag_add(5, dit[0]));
-  const uint32_t x0 = readlane32((uint32_t)out, 63);
+  uint32_t x0 = readlane32((uint32_t)out, 63);
+  // Flat streams (stream split): inside long raw stretches (text) the chain from the tile's first
+  // byte parses raw bytes as records and rarely finds the true chain within the tile, so its exit
+  // -- the next tile's optimistic entry -- is wrong tile after tile and the entries resolve one
+  // tile per look-back hop.  There, a raw record head with a full count (0xff, 8 bytes, 0xff) off
+  // that chain is a better guess: when the chain through it never meets chain 0, it stands in for
+  // chain 0 (any chain of the tile serves as the base the entry's chain is traced onto; its exit
+  // is only ever a guess the look-back checks).
+  int q0 = 0;  // where the tile's base chain starts
+  if (a.rec_pos && st.no_starts && t > 0 && settled && !(a.debug_skip & 4)) {
+    const uint64_t ffm = ff_heads(d, st.s) & ~tm0;
+    const uint64_t fl = ballot(ffm != 0);
+    if (fl) {
+      const int ql = lowest_bit(fl);
+      const int q = 64 * ql + lowest_bit(readlane64(ffm, ql));
+      int eF = st.s, outF = st.end;
+      uint64_t tmF = 0, runF = runm;
+      if (settle(d, st, chain, sx, q, eF, tmF, outF, runF) && ballot((tmF & tm0) != 0) == 0) {
+        tm0 = tmF;
+        runm = runF;
+        x0 = readlane32((uint32_t)outF, 63);
+        q0 = q;
+      }
+    }
+  }
   if (l == 0) store_agent32(a.x0p + t, 0x80000000u | x0);
   if (a.debug_skip & 128) return;  // diagnostic: + chain-0 walks and settle
   if (!settled) {
@@ -1494,7 +1536,7 @@ unpack_tiles_kernel(UnpackArgs a) {
     const uint32_t Eopt = entry_from_exit(xp, fms);
     uint32_t xE = x0;
     uint64_t runs = runm;
-    if (Eopt > 0 && Eopt < fms)
+    if (Eopt != (uint32_t)q0 && Eopt < fms)
       tm = enter_chain(d, aux, st, tm0, (int)Eopt, (int)fms, x0, &xE, &runs);
     else if (Eopt >= fms)
       tm = clip_below(tm0, fms, st.s, &xE);
@@ -1511,7 +1553,7 @@ unpack_tiles_kernel(UnpackArgs a) {
       // the predecessor's chain did not lead where its chain 0 does
       runs = runm;
       xE = x0;
-      if (E > 0 && E < fms)
+      if (E != (uint32_t)q0 && E < fms)
         tm = enter_chain(d, aux, st, tm0, (int)E, (int)fms, x0, &xE, &runs);
       else if (E >= fms)
         tm = clip_below(tm0, fms, st.s, &xE);
