@@ -259,12 +259,16 @@ struct PackScratch {
   uint32_t* thole;
   uint32_t* tpatch;
   uint8_t* scr;
+  uint32_t* tslot;
+  uint32_t nslots;
   size_t total;
 };
 
-// Pack scratch: the zeroed part (exit budgets polled by the next tile, the tiles' look-back
-// descriptors; zeroed by the framing launch), then per tile the first requested position, byte
-// count, count-byte patch, and the tile's slot for its packed bytes.  (The chunk-start bitmap
+// Pack scratch: the zeroed part (exit budgets polled by the next tile, the count of pool slots
+// taken, the tiles' look-back descriptors; zeroed by the framing launch), then per tile the first
+// requested position, byte count, count-byte patch and pool slot, then the slot pool (at most
+// kPackSlots slots of kPackScratchBytes: ~40 MiB whatever the batch size) for the bytes of tiles
+// whose offset was not known in time.  (The chunk-start bitmap
 // is zero at rest in its own buffer, ctx->pack_bits.)
 PackScratch carve_pack(void* base, uint64_t N, uint64_t ntiles, bool direct) {
   (void)N;
@@ -272,7 +276,7 @@ PackScratch carve_pack(void* base, uint64_t N, uint64_t ntiles, bool direct) {
   PackScratch s;
   s.bits = nullptr;
   s.state = c.take<uint32_t>(ntiles);
-  s.ticket = c.take<uint32_t>(4);
+  s.ticket = c.take<uint32_t>(4);  // (direct kernel: tile tickets; tile kernel: slots taken)
   s.desc = c.take<uint64_t>(ntiles);  // tile descriptors (direct kernel; tiles resolved in time)
   s.gword = c.take<uint64_t>(direct ? ntiles / 64 + 1 : 0);
   s.gincl = c.take<uint64_t>(direct ? ntiles / 64 + 1 : 0);
@@ -280,7 +284,8 @@ PackScratch carve_pack(void* base, uint64_t N, uint64_t ntiles, bool direct) {
   if (direct) {  // the direct kernel writes straight to the output: no slots, counts, offsets
     s.tile_first = c.take<uint64_t>(ntiles);
     s.tile_bytes = s.tile_off = nullptr;
-    s.thole = s.tpatch = nullptr;
+    s.thole = s.tpatch = s.tslot = nullptr;
+    s.nslots = 0;
     s.scr = nullptr;
     s.total = c.off;
     return s;
@@ -290,7 +295,9 @@ PackScratch carve_pack(void* base, uint64_t N, uint64_t ntiles, bool direct) {
   s.tile_off = nullptr;
   s.thole = c.take<uint32_t>(ntiles);
   s.tpatch = c.take<uint32_t>(ntiles);
-  s.scr = c.take<uint8_t>(ntiles * cpk::kPackScratchBytes + 16);
+  s.tslot = c.take<uint32_t>(ntiles);
+  s.nslots = (uint32_t)(ntiles < cpk::kPackSlots ? ntiles : cpk::kPackSlots);
+  s.scr = c.take<uint8_t>(s.nslots * cpk::kPackScratchBytes + 16);
   s.total = c.off;
   return s;
 }
@@ -369,6 +376,9 @@ cpk_status pack_common(cpk_ctx* ctx, const uint64_t* d_words, uint64_t N, const 
   a.tile_bytes = s.tile_bytes;
   a.tile_off = s.tile_off;
   a.scr = s.scr;
+  a.tslot = s.tslot;
+  a.slot_next = s.ticket;
+  a.nslots = s.nslots;
   a.thole = s.thole;
   a.tpatch = s.tpatch;
   a.err = ctx->err;

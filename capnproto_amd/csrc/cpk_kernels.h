@@ -9,6 +9,7 @@ namespace cpk {
 
 constexpr uint64_t kPackTileWords = 2048;       // words per workgroup tile (cpk_pack.hip)
 constexpr uint64_t kPackScratchBytes = 10 * kPackTileWords;  // a tile's packed bytes, worst case
+constexpr uint64_t kPackSlots = 2048;  // slot pool: a tile finding none waits for its offset
 constexpr uint64_t kUnpackTileBytes = 4096;     // packed bytes per unpack tile (>= 2050)
 
 struct PackTileArgs {
@@ -31,7 +32,11 @@ struct PackTileArgs {
   uint32_t* state;             // ntiles exit budgets (0x80000000 | raw << 8 | budget), zeroed
   uint64_t* tile_bytes;        // ntiles packed bytes per tile
   uint64_t* tile_off;          // (unused: offsets come from the descriptors' look-back)
-  uint8_t* scr;                // per-tile slots (ntiles * kPackScratchBytes + 16)
+  uint8_t* scr;                // slot pool (nslots * kPackScratchBytes + 16) for the tiles whose
+                               // offset is not known in time
+  uint32_t* tslot;             // per tile: its slot (written only by tiles that take one)
+  uint32_t* slot_next;         // slots taken so far (zeroed)
+  uint32_t nslots;
   uint32_t* thole;             // byte of a tile's provisional count (~0: none)
   uint32_t* tpatch;            // the next tile's final value for it (0x100 | v; 0: none)
   uint32_t* err;

@@ -174,19 +174,17 @@ __device__ __forceinline__ bool sum_simple(uint32_t s) { return (s >> 1) & 1u; }
 __device__ __forceinline__ uint32_t sum_fsw(uint32_t s) { return (s >> 2) & 0x3ffu; }
 __device__ __forceinline__ uint32_t sum_exit(uint32_t s) { return (s >> 16) & 0xffu; }
 
-#ifndef CPK_PACK_OPP
-#define CPK_PACK_OPP 1  // 0: every tile goes through its scratch slot and the placement launch
-#endif
-
-// Non-blocking look-back for tile t (one wave): the exclusive byte prefix from the descriptors
-// of up to 512 predecessors, or false when one before the nearest inclusive prefix has not
-// published its byte count yet.
-__device__ __forceinline__ bool try_lookback(const uint64_t* desc, uint64_t t, uint64_t* out) {
+// Look-back for tile t (one wave): the exclusive byte prefix from the descriptors of its
+// predecessors, 256 per round trip.  wait == false: gives up (false) when one before the nearest
+// inclusive prefix has not published its byte count yet, or after 512 predecessors.
+__device__ __forceinline__ bool pack_lookback(const uint64_t* desc, uint64_t t, uint64_t* out,
+                                              bool wait, uint32_t* err) {
   constexpr int K = 4;
   const int l = lane_id() + (int)opaque_zero();  // (addresses not hoisted out of the caller's loop)
   uint64_t excl = 0;
   int64_t j = (int64_t)t - 1;
-  for (int round = 0; round < 2; round++) {
+  uint32_t spins = 0;
+  for (int round = 0;;) {
     uint64_t d[K];
 #pragma unroll
     for (int i = 0; i < K; i++) {
@@ -201,7 +199,16 @@ __device__ __forceinline__ bool try_lookback(const uint64_t* desc, uint64_t t, u
       if (sb) stop_at = 64 * i + lowest_bit(sb);
       if (nb) blocked = 64 * i + lowest_bit(nb);
     }
-    if (blocked < stop_at) return false;
+    if (blocked < stop_at) {
+      if (!wait) return false;
+      if (++spins >= kSpinLimit) {
+        if (l == 0) raise_error(err, kErrInternal);
+        *out = excl;
+        return true;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      continue;  // the same window again
+    }
     uint64_t contrib = 0;
 #pragma unroll
     for (int i = 0; i < K; i++)
@@ -212,15 +219,16 @@ __device__ __forceinline__ bool try_lookback(const uint64_t* desc, uint64_t t, u
       return true;
     }
     j -= 64 * K;
+    if (!wait && ++round == 2) return false;
   }
-  return false;
 }
 
 // The staged tile (tile byte j at stg byte kPadF + j, n bytes) to o0 (any alignment), all
 // threads of the workgroup: 16-byte stores in the body, byte stores at both ends and in the one
 // 16-byte block holding `hole` (a count byte the next tile writes; ~0: none), which is skipped.
 __device__ __forceinline__ void copy_out_final(const uint32_t* stg, uint32_t n, uint8_t* o0,
-                                               uint32_t hole, int tid) {
+                                               uint32_t hole, int tid_) {
+  const int tid = tid_ + (int)opaque_zero();  // (addresses not hoisted out of the caller's loop)
   const uint8_t* const sb = (const uint8_t*)stg + kPadF;
   const uint64_t A0 = (uint64_t)(uintptr_t)o0;
   const uint64_t A1 = A0 + n;
@@ -253,13 +261,18 @@ __device__ __forceinline__ void copy_out_final(const uint32_t* stg, uint32_t n, 
 }
 
 // ---------------------------------------------------------------------------------------------
-// 1. Tile kernel: one workgroup per 2048-word tile, in blockIdx order.  The tile's packed bytes
-//    go to its own scratch slot (scr + T * kScr, 16-byte aligned), with its byte count, the
-//    position of its provisional count byte (if the next tile may change it) and, for the
-//    previous tile, the final value of that byte.  The only wait is for the previous tile's
-//    exit budget, and only when this tile's first word goes on with the stretch the previous
-//    tile ended in; the previous tile publishes it right after its classes when it holds a
-//    sync point.  (A tile only waits on a lower one, dispatched before it.)
+// 1. Tile kernel: one workgroup per 2048-word tile, in blockIdx order.  The tile publishes its
+//    byte count (desc[T] = AGG | bytes) as soon as it is known, stages its packed bytes in LDS,
+//    and then looks back over its predecessors' descriptors without waiting: when they are all
+//    there it writes its bytes straight to their final offset (desc[T] = INCL | prefix); else it
+//    copies them to a slot of a bounded pool (kPackSlots slots, 16-byte aligned) for the
+//    placement launch, and with the pool used up it waits for its offset.  Beside that: its
+//    byte count, the position of its provisional count byte (if the next tile may change it)
+//    and, for the previous tile, the final value of that byte (written by this tile when it
+//    writes its own bytes).  The other wait is for the previous tile's exit budget, and only
+//    when this tile's first word goes on with the stretch the previous tile ended in; the
+//    previous tile publishes it right after its classes when it holds a sync point.  (A tile
+//    only waits on lower ones, dispatched before it.)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void pack_tile_kernel(
     PackTileArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t stg[kSlotDw];
@@ -271,6 +284,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void p
   __shared__ uint32_t s_hole;        // byte of the tile's provisional count (~0: none)
   __shared__ uint64_t s_dst;         // the tile's output offset when resolved in time (~0: not)
   __shared__ uint32_t s_patch;       // previous tile's count byte | its distance before ours << 8
+  __shared__ uint32_t s_slot;        // the tile's slot of the pool (~0: none)
 
   const int tid = (int)threadIdx.x;
   const int l = lane_id();
@@ -545,7 +559,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void p
   // ---- emission: records OR-ed into the staging slot at their own byte offsets ------------
   const uint32_t nwin = agg <= kCap ? 1u : (agg + kCap - 1) / kCap;
   uint32_t* const wtr = trash[w] + l;
-  u32x4* const dst = (u32x4*)(a.scr + T * (uint64_t)kScr);
   for (uint32_t win = 0; win < nwin; win++) {
     const uint32_t wlo = win * kCap;
     const uint32_t whi = wlo + kCap;
@@ -602,33 +615,53 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void p
       __builtin_amdgcn_sched_barrier(0);
     }
     __syncthreads();  // ---- C: staged ------------------------------------------------------
-#if CPK_PACK_OPP
-    if (!windowed) {
+    if (win == 0) {
       // The tile's offset, if the tiles before it have all published their byte counts by now
-      // (no waiting): then its bytes go straight to the output and the placement launch skips it.
+      // (no waiting): then its bytes go straight to the output and the placement launch skips
+      // it.  Otherwise a slot of the pool holds them for the placement launch; with the pool
+      // used up (or more bytes than one staging window), the tile waits for its offset after all
+      // (only ever on lower tiles, which publish their byte counts before anything they could
+      // wait for).
       if (w == 0) {
         uint64_t ex = 0;
-        bool ok = T == 0 || try_lookback(a.desc, T, &ex);
-        ok = ok && ex + agg <= a.out_capacity;
+        bool ok = T == 0, wait = windowed;
+        uint32_t slot = ~0u;
+        while (!ok) {
+          ok = pack_lookback(a.desc, T, &ex, wait, a.err);
+          if (ok || wait) break;
+          if (l == 0) slot = atomicAdd(a.slot_next, 1u);
+          slot = readlane32(slot, 0);
+          if (slot < a.nslots) break;
+          slot = ~0u;
+          wait = true;
+        }
+        ok = ok && ex + agg <= a.out_capacity;  // (too small an output: placement raises it)
         if (l == 0) {
           if (ok && T != 0) store_agent(a.desc + T, kDescIncl | (ex + agg));
+          if (slot != ~0u) a.tslot[T] = slot;
           s_dst = ok ? ex : ~0ull;
+          s_slot = slot;
         }
       }
-      __syncthreads();  // ---- D: offset ----------------------------------------------------
-      const uint64_t ex = uniform64(s_dst);
-      if (ex != ~0ull) {
-        copy_out_final(stg, agg, a.out + ex, uniform32(s_hole), tid);
-        // the previous tile's provisional count byte, now final (its tile left it out)
-        const uint32_t pt = uniform32(s_patch);
-        if (tid == 0 && pt != 0) a.out[ex - (pt >> 8)] = (uint8_t)pt;
-        return;
+      __syncthreads();  // ---- D: offset or slot ---------------------------------------------
+    }
+    const uint64_t ex = uniform64(s_dst);
+    if (ex != ~0ull) {
+      const uint32_t nw = (whi < agg ? whi : agg) - wlo;
+      copy_out_final(stg, nw, a.out + ex + wlo, uniform32(s_hole) - wlo, tid);
+      // the previous tile's provisional count byte, now final (its tile left it out)
+      const uint32_t pt = uniform32(s_patch);
+      if (win == 0 && tid == 0 && pt != 0) a.out[ex - (pt >> 8)] = (uint8_t)pt;
+    } else if (!windowed) {
+      const uint32_t slot = uniform32(s_slot);
+      if (slot != ~0u) {
+        // the tile's bytes to its slot: aligned 16-byte copies
+        u32x4* const dst = (u32x4*)(a.scr + slot * (uint64_t)kScr);
+        const uint32_t n16 = (agg + 15u) >> 4;
+        for (uint32_t i = tid + opaque_zero(); i < n16; i += 64 * kWv)
+          dst[i] = ((const u32x4*)stg)[1 + i];
       }
     }
-#endif
-    // the window's bytes to the tile's scratch slot: aligned 16-byte copies
-    const uint32_t n16 = ((whi < agg ? whi : agg) - wlo + 15u) >> 4;
-    for (uint32_t i = tid; i < n16; i += 64 * kWv) dst[(wlo >> 4) + i] = ((const u32x4*)stg)[1 + i];
     if (windowed) {
       __syncthreads();
       for (int i = tid; i < kSlotDw / 4; i += 64 * kWv) ((u32x4*)stg)[i] = (u32x4){0, 0, 0, 0};
@@ -1260,22 +1293,21 @@ __global__ __launch_bounds__(256) void pack_place_kernel(PackTileArgs a) {
     if (l == 0) store_agent(a.desc + T, kDescIncl | (off + n));
   }
   const uint64_t total = off + n;  // (the batch total on the last tile)
-  // (a tile whose offset was known in time wrote its bytes itself: INCL descriptor, one staging
-  // window; tile 0 publishes INCL before it knows)
-  const bool placed = CPK_PACK_OPP && incl && n <= kCap;
+  // (a tile whose offset was known in time wrote its bytes itself: INCL descriptor; the others
+  // are in their slots)
   if (off + n > a.out_capacity) {
     if (l == 0) raise_error(a.err, kErrCapacity);
-  } else if (!placed && n) {
+  } else if (!incl && n) {
     // the previous tile's count byte that this tile finishes (the previous tile may have left it
     // out, having written its bytes itself)
-    if (CPK_PACK_OPP && T > 0 && l == 0) {
+    if (T > 0 && l == 0) {
       const uint32_t ph = a.thole[T - 1], pp = a.tpatch[T];
       if (ph != 0xffffffffu && pp) a.out[off - a.tile_bytes[T - 1] + ph] = (uint8_t)pp;
     }
     // count byte patched by the next tile (position, value) -- wave-uniform
     const uint32_t hole = T + 1 < a.ntiles ? a.thole[T] : 0xffffffffu;
     const uint32_t pv = hole != 0xffffffffu ? a.tpatch[T + 1] : 0u;
-    const uint8_t* const src = a.scr + T * (uint64_t)kScr;
+    const uint8_t* const src = a.scr + a.tslot[T] * (uint64_t)kScr;
     uint8_t* const o0 = a.out + off;
     const uint64_t A0 = (uint64_t)(uintptr_t)o0;
     const uint64_t A1 = A0 + n;

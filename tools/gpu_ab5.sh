@@ -1,10 +1,24 @@
 #!/bin/bash
 # tests + default bench + per-kernel A/B of VARIANTS on CFGS + unpack step counters (var_diag.so)
 set -o pipefail
-cd ${GRAFT_REPO_ROOT:-$(pwd)}; mkdir -p gpurun_out
+cd ${GRAFT_REPO_ROOT:-$(pwd)}; mkdir -p gpurun_out; PWD_R=$(pwd)
 TAG=${1:-r04f}
+# (variants that are not built are skipped; SPLIT defaults on)
+V=""; for v in ${VARIANTS:-base}; do if [ $v = base ] || [ -f capnproto_amd/var_$v.so ]; then V="$V $v"; fi; done
+export VARIANTS="$V"; SPLIT=${SPLIT-1}
 bash tools/gpu_ab3.sh $TAG || exit 1
 if [ -f capnproto_amd/var_diag.so ]; then
   timeout -k 10 300 python3 tools/diag_unpack.py capnproto_amd/var_diag.so ${DIAG_CFGS:-c2 c3 c4} > gpurun_out/${TAG}_diag.log 2>&1
   rc=$?; cat gpurun_out/${TAG}_diag.log | tail -5; [ $rc = 0 ] || exit 1
+fi
+if [ -n "$SPLIT" ]; then
+  (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD_R/gpurun_out/${TAG}_split" -o run \
+    -- python3 "$PWD_R/tools/split_prof.py" > "$PWD_R/gpurun_out/${TAG}_split.log" 2>&1) || { echo "split prof failed"; tail -5 gpurun_out/${TAG}_split.log; exit 1; }
+  tail -3 gpurun_out/${TAG}_split.log
+  python3 - gpurun_out/${TAG}_split <<'PY'
+import csv, glob, sys
+f = glob.glob(sys.argv[1] + "/*kernel_stats.csv")[0]
+for r in sorted(csv.DictReader(open(f)), key=lambda r: -float(r["TotalDurationNs"]))[:8]:
+    print(r["Name"].split("(")[0][-40:], r["Calls"], round(float(r["AverageNs"]) / 1e3, 1), "us")
+PY
 fi
