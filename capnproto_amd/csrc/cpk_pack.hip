@@ -175,30 +175,25 @@ __device__ __forceinline__ uint32_t sum_fsw(uint32_t s) { return (s >> 2) & 0x3f
 __device__ __forceinline__ uint32_t sum_exit(uint32_t s) { return (s >> 16) & 0xffu; }
 
 // Look-back for tile t (one wave): the exclusive byte prefix from the descriptors of its
-// predecessors, 256 per round trip.  wait == false: gives up (false) when one before the nearest
-// inclusive prefix has not published its byte count yet, or after 512 predecessors.
+// predecessors -- a first window of 16 (one 128-byte line: these agent-scope reads go past the L2,
+// and the nearest inclusive prefix is usually a few tiles back), then 64 per round trip.
+// wait == false: gives up (false) when one before the nearest inclusive prefix has not
+// published its byte count yet, or after 272 predecessors.
 __device__ __forceinline__ bool pack_lookback(const uint64_t* desc, uint64_t t, uint64_t* out,
                                               bool wait, uint32_t* err) {
-  constexpr int K = 4;
   const int l = lane_id() + (int)opaque_zero();  // (addresses not hoisted out of the caller's loop)
   uint64_t excl = 0;
   int64_t j = (int64_t)t - 1;
   uint32_t spins = 0;
+  int width = 16;
   for (int round = 0;;) {
-    uint64_t d[K];
-#pragma unroll
-    for (int i = 0; i < K; i++) {
-      const int64_t idx = j - (64 * i + l);
-      d[i] = idx >= 0 ? load_agent(desc + idx) : kDescIncl;
-    }
-    int stop_at = 64 * K, blocked = 64 * K;
-#pragma unroll
-    for (int i = K - 1; i >= 0; i--) {
-      const uint64_t f = d[i] & kDescFlags;
-      const uint64_t sb = ballot(f == kDescIncl), nb = ballot(f == 0);
-      if (sb) stop_at = 64 * i + lowest_bit(sb);
-      if (nb) blocked = 64 * i + lowest_bit(nb);
-    }
+    const int64_t idx = j - l;
+    const bool in = l < width;
+    const uint64_t d = !in ? 0ull : (idx >= 0 ? load_agent(desc + idx) : kDescIncl);
+    const uint64_t f = d & kDescFlags;
+    const uint64_t sb = ballot(in && f == kDescIncl), nb = ballot(in && f == 0);
+    const int stop_at = sb ? lowest_bit(sb) : 64;
+    const int blocked = nb ? lowest_bit(nb) : 64;
     if (blocked < stop_at) {
       if (!wait) return false;
       if (++spins >= kSpinLimit) {
@@ -209,17 +204,14 @@ __device__ __forceinline__ bool pack_lookback(const uint64_t* desc, uint64_t t, 
       __builtin_amdgcn_s_sleep(1);
       continue;  // the same window again
     }
-    uint64_t contrib = 0;
-#pragma unroll
-    for (int i = 0; i < K; i++)
-      if (64 * i + l <= stop_at) contrib += d[i] & kDescValue;
-    excl += wave_sum64(contrib);
-    if (stop_at < 64 * K) {
+    excl += wave_sum64(l <= stop_at && in ? (d & kDescValue) : 0ull);
+    if (stop_at < 64) {
       *out = excl;
       return true;
     }
-    j -= 64 * K;
-    if (!wait && ++round == 2) return false;
+    j -= width;
+    width = 64;
+    if (!wait && ++round == 5) return false;
   }
 }
 
@@ -1289,7 +1281,7 @@ __global__ __launch_bounds__(256) void pack_place_kernel(PackTileArgs a) {
   if (incl) {
     off = (dT & kDescValue) - n;
   } else {
-    off = lookback<8>(a.desc, T, a.err);
+    pack_lookback(a.desc, T, &off, true, a.err);
     if (l == 0) store_agent(a.desc + T, kDescIncl | (off + n));
   }
   const uint64_t total = off + n;  // (the batch total on the last tile)

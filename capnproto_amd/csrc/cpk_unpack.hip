@@ -1011,27 +1011,31 @@ __device__ __forceinline__ uint64_t clip_below(uint64_t tm0, uint32_t fms, int s
 // exit (as published, and itself right) has the ok bit; the farthest tile without it makes every
 // nearer one wrong, so the wave then waits for the tile right after it to publish INCL (it
 // resolves its own entry the same way) and starts over.  Waits are only ever for lower tiles.
+// The first window of each pass is 16 tiles (one 128-byte line of descriptors: the nearest INCL
+// is usually a few tiles back, and these agent-scope reads go past the L2), later ones 64.
 __device__ uint64_t lookback_tiles(const UnpackArgs& a, uint64_t t, uint32_t* xprev) {
   const int l = lane_id();
   int64_t base = (int64_t)t - 1;  // nearest tile of the window
   uint64_t acc = 0;
   uint32_t xfirst = (uint32_t)kB;
   uint32_t spins = 0;
+  int width = 16;
   for (;;) {
     const int64_t idx = base - l;
+    const bool in = l < width;
     // before tile 0: an inclusive zero whose exit enters tile 0 at byte 0
-    const uint64_t dv = idx >= 0 ? load_agent(a.desc + idx) : (kDescIncl | kOkBit);
+    const uint64_t dv = !in ? 0ull : (idx >= 0 ? load_agent(a.desc + idx) : (kDescIncl | kOkBit));
     const uint64_t stt = dv & kDescFlags;
-    const uint64_t sb = ballot(stt == kDescIncl);
+    const uint64_t sb = ballot(in && stt == kDescIncl);
     const int k = sb ? lowest_bit(sb) : 64;
-    const uint64_t nb = ballot(stt == 0);
+    const uint64_t nb = ballot(in && stt == 0);
     const int nl = nb ? lowest_bit(nb) : 64;
     const uint64_t* wait_on = nullptr;
     bool want_incl = false;
     if (nl < k) {
       wait_on = a.desc + (base - nl);
     } else {
-      const int kk = k < 64 ? k : 63;
+      const int kk = k < width ? k : width - 1;
       const bool first = base == (int64_t)t - 1;
       const uint64_t fb = ballot(l <= kk && (l >= 1 || !first) && !(dv & kOkBit));
       if (fb) {
@@ -1040,8 +1044,9 @@ __device__ uint64_t lookback_tiles(const UnpackArgs& a, uint64_t t, uint32_t* xp
       } else {
         if (first) xfirst = desc_exit(readlane64(dv, 0));
         acc += wave_sum64(l <= kk ? (dv & kWordsMask) : 0ull);
-        if (k < 64) break;
-        base -= 64;
+        if (k < width) break;
+        base -= width;
+        width = 64;
         continue;
       }
     }
@@ -1063,6 +1068,7 @@ __device__ uint64_t lookback_tiles(const UnpackArgs& a, uint64_t t, uint32_t* xp
     if (want_incl) {
       base = (int64_t)t - 1;
       acc = 0;
+      width = 16;
     }
   }
   *xprev = xfirst;
