@@ -141,6 +141,15 @@ __device__ __forceinline__ uint64_t compact_nonzero(uint64_t x) {
 // (it reasons per lane and may otherwise reorder a lane's access past another lane's).
 __device__ __forceinline__ void lane_handoff() { asm volatile("" ::: "memory"); }
 
+// Workgroup barrier ordering LDS only: __syncthreads also releases global memory at workgroup
+// scope, which waits for every outstanding vector memory operation -- stores, and loads issued
+// ahead for later use.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // A zero the compiler cannot see through: added to a uniform index, it keeps a load in a VGPR
 // (a uniform load is otherwise moved to SGPRs with v_readfirstlane right behind it, i.e. waited
 // for at once).

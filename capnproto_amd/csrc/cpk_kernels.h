@@ -44,6 +44,7 @@ struct PackTileArgs {
   // both kernels), per 64-tile group (count << 48) + bytes and the groups' inclusive byte prefix
   // (direct kernel)
   uint32_t* ticket;
+  uint32_t* tile_ticket;       // tile kernel built with CPK_PACK_TICKET: tiles taken (zeroed)
   uint64_t* desc;
   uint64_t* gword;
   uint64_t* gincl;

@@ -265,8 +265,63 @@ __device__ __forceinline__ void copy_out_final(const uint32_t* stg, uint32_t n, 
 //    when this tile's first word goes on with the stretch the previous tile ended in; the
 //    previous tile publishes it right after its classes when it holds a sync point.  (A tile
 //    only waits on lower ones, dispatched before it.)
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void pack_tile_kernel(
-    PackTileArgs a) {
+#ifndef CPK_PACK_TICKET
+#define CPK_PACK_TICKET 0  // 1: persistent workgroups take tiles by ticket, next tile's loads early
+#endif
+#if CPK_PACK_TICKET
+#define CPK_PACK_TILE_WPE 4  // two tiles' words live per lane
+#else
+#define CPK_PACK_TILE_WPE 7
+#endif
+
+// A tile's global loads (one lane's 8 words, its chunk-start bitmap byte, the word before the
+// wave / after the tile, the next tile's start flag, the lane's first requested position).
+struct TileLoads {
+  uint32_t xlo[kK], xhi[kK];
+  uint64_t cb0, xw0, nb0, p00;
+};
+
+// All issued before any is waited for (vector loads retire in order; the compiler waits for all
+// of them right behind a load whose value it moves to an SGPR or at the join behind a load under
+// a branch, so uniform values come through scalar loads and lane-varying guards are clamped
+// addresses).
+__device__ __forceinline__ void tile_loads(const PackTileArgs& a, uint64_t T, int w, int l,
+                                           TileLoads& L) {
+  const uint64_t N = a.nwords;
+  const uint64_t nbitw = (N + 63) >> 6;
+  const uint64_t tbase = T * kTW;
+  const uint64_t tend = tbase + kTW < N ? tbase + kTW : N;
+  const uint64_t wbase = tbase + (uint64_t)kWW * w;
+  const uint64_t w0 = wbase + (uint64_t)kK * l;  // the lane's first word
+  // word pairs from clamped indices (no branch: a load under a branch gets its own wait at the
+  // join), words past the batch then read as zero (the tile kernel runs for N > 2048 words: one
+  // tile goes to the direct kernel)
+#pragma unroll
+  for (int i = 0; i < kK / 2; i++) {
+    const uint64_t j = w0 + 2 * i;
+    const u32x4 v = *(const u32x4*)(a.words + (j + 2 <= N ? j : N - 2));
+    const bool k0 = j < N, k1 = j + 1 < N, sh = j + 2 > N;  // sh: the pair ending at word N - 1
+    L.xlo[2 * i] = k0 ? (sh ? v.z : v.x) : 0u;
+    L.xhi[2 * i] = k0 ? (sh ? v.w : v.y) : 0u;
+    L.xlo[2 * i + 1] = k1 ? v.z : 0u;
+    L.xhi[2 * i + 1] = k1 ? v.w : 0u;
+  }
+  const uint64_t cbi = (wbase >> 6) + (uint64_t)(l >> 3);
+  L.cb0 = a.chunk_bits[cbi < nbitw ? cbi : nbitw - 1];
+  // lane 0: the word before the wave; the other lanes: the word after the tile (its class
+  // decides whether this tile's open run may go on in the next tile)
+  const uint64_t xi = l == 0 ? (wbase > 0 ? wbase - 1 : 0) : (tend < N ? tend : N - 1);
+  L.xw0 = a.words[xi < N ? xi : N - 1];
+  const uint64_t nbi = T + 1 + (uint64_t)opaque_zero();  // the next tile's start byte
+  L.nb0 = a.tile_starts[nbi];
+  typedef const __attribute__((address_space(4))) uint64_t cu64;
+  const uint64_t pidx = a.pos ? *((cu64*)a.tile_first + T) : 0;  // scalar load
+  const uint64_t pi = pidx + l;
+  L.p00 = (a.pos ? a.pos : a.words)[a.pos && pi <= a.npos ? pi : 0];
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CPK_PACK_TILE_WPE))) void
+pack_tile_kernel(PackTileArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t stg[kSlotDw];
   __shared__ __attribute__((aligned(16))) uint32_t trash[kWv][kTrashDw];
   __shared__ uint64_t sel_tab[256];
@@ -279,58 +334,59 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void p
   __shared__ uint32_t s_slot;        // the tile's slot of the pool (~0: none)
 
   const int tid = (int)threadIdx.x;
-  const int l = lane_id();
   const int w = (int)uniform32(threadIdx.x >> 6);
   const uint64_t N = a.nwords;
   const uint64_t nbitw = (N + 63) >> 6;
+  sel_tab[tid] = make_sel((uint32_t)tid);
+#if CPK_PACK_TICKET
+  // Tiles in ticket order: a tile only waits on tiles whose workgroups took their tickets
+  // earlier and are running (whatever number is resident).  A workgroup issues the next tile's
+  // loads before it works on the current one, so its loads are in flight during the whole tile.
+  __shared__ uint32_t s_tk;
+  if (tid == 0) s_tk = atomicAdd(a.tile_ticket, 1u);
+  lds_barrier();
+  uint64_t T = uniform32(s_tk);
+  if (T >= a.ntiles) return;
+  TileLoads cur;
+  tile_loads(a, T, w, lane_id(), cur);
+  for (;;) {
+  lds_barrier();  // the previous tile is done with the LDS and the ticket
+  if (tid == 0) s_tk = atomicAdd(a.tile_ticket, 1u);
+  for (int i = tid; i < kSlotDw / 4; i += 64 * kWv) ((u32x4*)stg)[i] = (u32x4){0, 0, 0, 0};
+  lds_barrier();
+  const uint64_t Tn = uniform32(s_tk);
+  TileLoads nxt;
+  tile_loads(a, Tn < a.ntiles ? Tn : a.ntiles - 1, w, lane_id(), nxt);
+  // (lane masks recomputed per tile, not held -- and spilled -- across the loop: a spill reload
+  // is a vector memory read, retired in order behind the next tile's loads)
+  const int l = lane_id() + (int)opaque_zero();
+#else
   const uint64_t T = blockIdx.x;
+  const int l = lane_id();
+  TileLoads cur;
+  tile_loads(a, T, w, l, cur);
+  for (int i = tid; i < kSlotDw / 4; i += 64 * kWv) ((u32x4*)stg)[i] = (u32x4){0, 0, 0, 0};
+#endif
   const uint64_t tbase = T * kTW;
   const uint64_t tend = tbase + kTW < N ? tbase + kTW : N;
   const uint64_t wbase = tbase + (uint64_t)kWW * w;
   const int nvw = wbase >= N ? 0 : (int)((N - wbase) < (uint64_t)kWW ? (N - wbase) : kWW);
-  const uint64_t w0 = wbase + (uint64_t)kK * l;  // the lane's first word
-
-  // ---- loads: all issued before any is waited for --------------------------------------
-  // (vector loads retire in order; the compiler waits for all of them right behind a load whose
-  // value it moves to an SGPR or at the join behind a load under a branch, so uniform values
-  // come through scalar loads and lane-varying guards are clamped addresses)
   uint32_t xlo[kK], xhi[kK];
-  if (nvw == kWW) {
-    const u32x4* src = (const u32x4*)(a.words + w0);
 #pragma unroll
-    for (int i = 0; i < kK / 2; i++) {
-      const u32x4 v = src[i];
-      xlo[2 * i] = v.x;
-      xhi[2 * i] = v.y;
-      xlo[2 * i + 1] = v.z;
-      xhi[2 * i + 1] = v.w;
-    }
-  } else {
-#pragma unroll
-    for (int k = 0; k < kK; k++) {
-      const uint64_t x = w0 + k < N ? a.words[w0 + k] : 0;
-      xlo[k] = (uint32_t)x;
-      xhi[k] = (uint32_t)(x >> 32);
-    }
+  for (int k = 0; k < kK; k++) {
+    xlo[k] = cur.xlo[k];
+    xhi[k] = cur.xhi[k];
   }
   const uint64_t cbi = (wbase >> 6) + (uint64_t)(l >> 3);
-  const uint64_t cb0 = a.chunk_bits[cbi < nbitw ? cbi : nbitw - 1];
-  // lane 0: the word before the wave; the other lanes: the word after the tile (its class
-  // decides whether this tile's open run may go on in the next tile)
-  const uint64_t xi = l == 0 ? (wbase > 0 ? wbase - 1 : 0) : (tend < N ? tend : N - 1);
-  const uint64_t xw0 = a.words[xi < N ? xi : N - 1];
+  const uint64_t xw0 = cur.xw0, nb0 = cur.nb0;
   const uint64_t nbi = T + 1 + (uint64_t)opaque_zero();  // the next tile's start byte
-  const uint64_t nb0 = a.tile_starts[nbi];
   typedef const __attribute__((address_space(4))) uint64_t cu64;
   const uint64_t pidx = a.pos ? *((cu64*)a.tile_first + T) : 0;  // scalar load
   const uint64_t pi = pidx + l;
   const bool pv = a.pos && pi <= a.npos;
-  const uint64_t p00 = (a.pos ? a.pos : a.words)[pv ? pi : 0];
-  sel_tab[tid] = make_sel((uint32_t)tid);
-  for (int i = tid; i < kSlotDw / 4; i += 64 * kWv) ((u32x4*)stg)[i] = (u32x4){0, 0, 0, 0};
-  const uint64_t cbw = cbi < nbitw ? cb0 : 0;
+  const uint64_t cbw = cbi < nbitw ? cur.cb0 : 0;
   const uint64_t xw = (wbase > 0 || l != 0) ? xw0 : 0;
-  const uint64_t p0 = pv ? p00 : ~0ull;
+  const uint64_t p0 = pv ? cur.p00 : ~0ull;
 
   // ---- classes -------------------------------------------------------------------------
   uint32_t Zm = 0, Rm = 0, Fm = 0, nzA = 0;
@@ -401,10 +457,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void p
     const bool ns = nC || (!nZ && !nR) || (nZ && !lastZ) || (nR && !lastR);
     next_sync = tend >= N || readlane32(ns ? 1u : 0u, 63) != 0;
   }
-  __syncthreads();  // ---- A: wave summaries ---------------------------------------------
+  lds_barrier();  // ---- A: wave summaries ---------------------------------------------
   // the chunk-start bits are zero at rest: this tile clears what only it reads (its bitmap words;
   // the bit of its successor's first word, read here and nowhere else)
-  if ((l & 7) == 0 && cbi < nbitw && cbw != 0) a.chunk_bits[cbi] = 0;
+  if ((l & 7) == 0 && cbi < nbitw && cbw != 0) a.chunk_bits[cbi] = (uint64_t)opaque_zero();
   if (w == kWv - 1 && l == 0 && nb0) a.tile_starts[nbi] = 0;
 
   uint32_t sm[kWv];
@@ -461,7 +517,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void p
         if (l == 0) s_sexit[v] = ex;
         if (v == kWv - 1 && !last_sync) publish_state(ex);
       }
-      __syncthreads();
+      lds_barrier();
     }
   }
   // wave 0 finishes the previous tile's open run: it needs the entry
@@ -478,7 +534,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void p
   const uint32_t incl = wave_incl_sum32(bytes);
   const uint32_t loff = incl - bytes;
   if (l == 63) s_bytes[w] = incl;
-  __syncthreads();  // ---- B: wave byte counts -------------------------------------------
+  lds_barrier();  // ---- B: wave byte counts -------------------------------------------
 
   uint32_t woff = 0, agg = 0, s0 = (uint32_t)kTW;
 #pragma unroll
@@ -606,7 +662,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void p
       o += L;
       __builtin_amdgcn_sched_barrier(0);
     }
-    __syncthreads();  // ---- C: staged ------------------------------------------------------
+    lds_barrier();  // ---- C: staged ------------------------------------------------------
     if (win == 0) {
       // The tile's offset, if the tiles before it have all published their byte counts by now
       // (no waiting): then its bytes go straight to the output and the placement launch skips
@@ -635,7 +691,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void p
           s_slot = slot;
         }
       }
-      __syncthreads();  // ---- D: offset or slot ---------------------------------------------
+      lds_barrier();  // ---- D: offset or slot ---------------------------------------------
     }
     const uint64_t ex = uniform64(s_dst);
     if (ex != ~0ull) {
@@ -655,11 +711,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void p
       }
     }
     if (windowed) {
-      __syncthreads();
+      lds_barrier();
       for (int i = tid; i < kSlotDw / 4; i += 64 * kWv) ((u32x4*)stg)[i] = (u32x4){0, 0, 0, 0};
-      __syncthreads();
+      lds_barrier();
     }
   }
+#if CPK_PACK_TICKET
+  if (Tn >= a.ntiles) break;
+  T = Tn;
+  cur = nxt;
+  }
+#endif
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1356,17 +1418,7 @@ __global__ __launch_bounds__(256) void pack_place_kernel(PackTileArgs a) {
 
 }  // namespace
 
-hipError_t launch_pack_tiles(const PackTileArgs& a, hipStream_t stream) {
-  if (a.ntiles == 0) return hipSuccess;
-  if (a.ntiles >= (1ull << 31)) return hipErrorInvalidValue;
-  pack_tile_kernel<<<(unsigned)a.ntiles, 256, 0, stream>>>(a);
-  return hipGetLastError();
-}
-
-hipError_t launch_pack_direct(const PackTileArgs& a, hipStream_t stream) {
-  if (a.ntiles == 0) return hipSuccess;
-  if (a.ntiles >= (1ull << 31)) return hipErrorInvalidValue;
-  // persistent workgroups take tiles by ticket until none is left: as many as fit on the device
+static int cu_count() {
   static int ncu = 0;
   if (ncu == 0) {
     int dev = 0, v = 0;
@@ -1374,7 +1426,27 @@ hipError_t launch_pack_direct(const PackTileArgs& a, hipStream_t stream) {
            hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
            v > 0) ? v : 256;
   }
-  const uint64_t grid = (uint64_t)ncu * CPK_PACKD_WPE;
+  return ncu;
+}
+
+hipError_t launch_pack_tiles(const PackTileArgs& a, hipStream_t stream) {
+  if (a.ntiles == 0) return hipSuccess;
+  if (a.ntiles >= (1ull << 31)) return hipErrorInvalidValue;
+#if CPK_PACK_TICKET
+  // persistent workgroups taking tiles by ticket: as many as fit on the device
+  const uint64_t grid = (uint64_t)cu_count() * CPK_PACK_TILE_WPE;
+  pack_tile_kernel<<<(unsigned)(a.ntiles < grid ? a.ntiles : grid), 256, 0, stream>>>(a);
+#else
+  pack_tile_kernel<<<(unsigned)a.ntiles, 256, 0, stream>>>(a);
+#endif
+  return hipGetLastError();
+}
+
+hipError_t launch_pack_direct(const PackTileArgs& a, hipStream_t stream) {
+  if (a.ntiles == 0) return hipSuccess;
+  if (a.ntiles >= (1ull << 31)) return hipErrorInvalidValue;
+  // persistent workgroups take tiles by ticket until none is left: as many as fit on the device
+  const uint64_t grid = (uint64_t)cu_count() * CPK_PACKD_WPE;
   pack_direct_kernel<<<(unsigned)(a.ntiles < grid ? a.ntiles : grid), 256, 0, stream>>>(a);
   return hipGetLastError();
 }

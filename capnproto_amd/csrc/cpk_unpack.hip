@@ -1417,6 +1417,9 @@ __device__ __forceinline__ void expand_records(const UnpackArgs& a, uint64_t A, 
   }
 }
 
+#ifndef CPK_PREWALK
+#define CPK_PREWALK 0  // bytes of unmarked walk before each sub-tile (0: none; at most 64)
+#endif
 #ifndef CPK_UNPACK_WPE
 #define CPK_UNPACK_WPE 7  // 72 VGPRs: 7 waves per SIMD (LDS allows 7); 6 at the unconstrained 80
 #endif
@@ -1461,17 +1464,36 @@ unpack_tiles_kernel(UnpackArgs a) {
   // ---- chain 0 (entered at the tile's first byte): speculative walks, then the lane fixed point
   uint64_t chain = 0, runm = 0;
   int sx = kDead;
+  // Each lane's speculative chain starts CPK_PREWALK bytes before its sub-tile (at the last
+  // message start there, if any) and walks unmarked up to it: chains synchronise within a few
+  // records, so the chain then usually enters the sub-tile where the true one does, and the
+  // fixed point below has little left to re-walk.
+  int e0 = st.s;
+#if CPK_PREWALK > 0
+  {
+    const uint64_t pm = shfl64(st.msw, l > 0 ? l - 1 : 0);
+    if (l > 0 && st.s < st.pend && !(a.debug_skip & 4)) {
+      const uint64_t wn = pm & ~mask_lt(64 - CPK_PREWALK);
+      int q = wn ? st.s - 64 + highest_bit(wn) : st.s - CPK_PREWALK;
+      while (q < st.s) q += step_len(d[q], d[q + 9]);
+      // (a message start in the sub-tile before the landing point restarts the chain there)
+      const int fm = st.msw ? st.s + lowest_bit(st.msw) : 0x7fffffff;
+      e0 = q < fm ? q : fm;
+    }
+  }
+#endif
 #ifdef CPK_DIAG
   int dn = 0, dit[3] = {0, 0, 0};
-  if (st.s < st.pend && !(a.debug_skip & 4)) sx = walk(d, st, st.s, 0, &chain, &runm, &dn);
+  if (e0 < st.pend && !(a.debug_skip & 4)) sx = walk(d, st, e0, 0, &chain, &runm, &dn);
   diag_add(0, 1);
   diag_trips(1, dn);
   int* const diag_it = dit;
 #else
-  if (st.s < st.pend && !(a.debug_skip & 4)) sx = walk(d, st, st.s, 0, &chain, &runm);
+  if (e0 < st.pend && !(a.debug_skip & 4)) sx = walk(d, st, e0, 0, &chain, &runm);
   int* const diag_it = nullptr;
 #endif
-  int e = st.s;
+  if (e0 >= st.pend) sx = kDead;
+  int e = e0;
   uint64_t tm0 = 0;
   int out = st.end;
   const bool settled =
@@ -1492,7 +1514,7 @@ unpack_tiles_kernel(UnpackArgs a) {
     if (fl) {
       const int ql = lowest_bit(fl);
       const int q = 64 * ql + lowest_bit(readlane64(ffm, ql));
-      int eF = st.s, outF = st.end;
+      int eF = e0, outF = st.end;
       uint64_t tmF = 0, runF = runm;
       if (settle(d, st, chain, sx, q, eF, tmF, outF, runF) && ballot((tmF & tm0) != 0) == 0) {
         tm0 = tmF;

@@ -7,10 +7,21 @@ TAG=${1:-r04f}
 V=""; for v in ${VARIANTS:-base}; do if [ $v = base ] || [ -f capnproto_amd/var_$v.so ]; then V="$V $v"; fi; done
 export VARIANTS="$V"; SPLIT=${SPLIT-1}
 bash tools/gpu_ab3.sh $TAG || exit 1
-if [ -f capnproto_amd/var_diag.so ]; then
-  timeout -k 10 300 python3 tools/diag_unpack.py capnproto_amd/var_diag.so ${DIAG_CFGS:-c2 c3 c4} > gpurun_out/${TAG}_diag.log 2>&1
-  rc=$?; cat gpurun_out/${TAG}_diag.log | tail -5; [ $rc = 0 ] || exit 1
-fi
+# GPU tests with each variant library in TESTVARS swapped in
+cp capnproto_amd/libcpk_hip.so /tmp/cpk_main.so
+for v in $TESTVARS; do
+  cp capnproto_amd/var_$v.so capnproto_amd/libcpk_hip.so
+  timeout -k 10 400 python -u -m pytest tests -m "gpu and not slow" -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/${TAG}_tests_$v.log 2>&1
+  rc=$?; echo "== tests $v"; tail -2 gpurun_out/${TAG}_tests_$v.log
+  cp /tmp/cpk_main.so capnproto_amd/libcpk_hip.so
+  [ $rc = 0 ] || [ $rc = 1 ] || exit 1
+done
+for f in capnproto_amd/var_diag*.so; do
+  [ -f $f ] || continue
+  n=$(basename $f .so)
+  timeout -k 10 300 python3 tools/diag_unpack.py $f ${DIAG_CFGS:-c2 c3 c4} > gpurun_out/${TAG}_$n.log 2>&1
+  rc=$?; echo "== $n"; grep -v amdgpu.ids gpurun_out/${TAG}_$n.log | tail -4; [ $rc = 0 ] || exit 1
+done
 if [ -n "$SPLIT" ]; then
   (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD_R/gpurun_out/${TAG}_split" -o run \
     -- python3 "$PWD_R/tools/split_prof.py" > "$PWD_R/gpurun_out/${TAG}_split.log" 2>&1) || { echo "split prof failed"; tail -5 gpurun_out/${TAG}_split.log; exit 1; }

@@ -15,6 +15,7 @@ for v in ${VARIANTS:-base}; do
     (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/${TAG}_${v}_${c}" -o run \
       -- python3 "$R/bench.py" --config $c --sub none --steps ${STEPS:-10} --warmup 2 --no-cpu-baseline --no-host --no-split \
       > "$R/gpurun_out/${TAG}_${v}_${c}.log" 2>&1) || { echo "rocprof $v $c failed"; tail -20 "$R/gpurun_out/${TAG}_${v}_${c}.log"; exit 1; }
+    grep -q "check failed\|differ from the reference" "$R/gpurun_out/${TAG}_${v}_${c}.log" && echo "!! $v $c: WRONG OUTPUT"
     f=$(find "$R/gpurun_out/${TAG}_${v}_${c}" -name '*kernel_stats.csv' | head -1)
     python3 - "$f" "$v $c" <<'PY'
 import csv, sys
