@@ -1516,7 +1516,9 @@ unpack_tiles_kernel(UnpackArgs a) {
       const int q = 64 * ql + lowest_bit(readlane64(ffm, ql));
       int eF = e0, outF = st.end;
       uint64_t tmF = 0, runF = runm;
+      CPK_DIAG_ONLY(diag_add(12, 1));
       if (settle(d, st, chain, sx, q, eF, tmF, outF, runF) && ballot((tmF & tm0) != 0) == 0) {
+        CPK_DIAG_ONLY(diag_add(13, 1));
         tm0 = tmF;
         runm = runF;
         x0 = readlane32((uint32_t)outF, 63);
@@ -1572,6 +1574,7 @@ unpack_tiles_kernel(UnpackArgs a) {
     if (!has_start) {
       w = readlane32(wave_incl_sum32(mask_words(d, st.s, tm, runs)), 63);
       if (l == 0) store_agent(a.desc + t, make_desc(kDescAgg, xE, x0, w));
+      CPK_DIAG_ONLY(diag_add(14, xE != x0));
     }
     uint32_t xprev = xp;
     if (!(a.debug_skip & 8)) excl = lookback_tiles(a, t, &xprev);
@@ -1674,6 +1677,8 @@ hipError_t launch_unpack_stage(int stage, const UnpackArgs& a, hipStream_t strea
 //  0 tiles  1/2 chain-0 walk trips (wave max / lane sum)  3/4 settle re-walk trips (max / sum)
 //  5 settle rounds  6 enter_chain calls  7 lane-0 merge steps  8 merges past the cap
 //  9 entries that differed from the optimistic one  10 optimistic entries walked  11 tiles with a start
+//  12 flat stream: tiles with a raw-head candidate  13 ... whose chain replaced chain 0
+//  14 tiles whose optimistic entry's exit is not their chain-0 exit (no ok bit)
 extern "C" int cpk_debug_diag(uint64_t* out, int reset) {
   if (hipDeviceSynchronize() != hipSuccess) return 10;
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(cpk::g_diag), 16 * sizeof(uint64_t)) != hipSuccess) return 10;

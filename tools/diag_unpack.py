@@ -20,7 +20,7 @@ from bench import CONFIGS  # noqa: E402
 
 NAMES = ["tiles", "walk0_trips", "walk0_lane_steps", "rewalk_trips", "rewalk_lane_steps",
          "settle_rounds", "enter_calls", "merge_steps", "merge_capped", "entry_mismatch",
-         "opt_walked", "has_start"]
+         "opt_walked", "has_start", "f_cand", "f_used", "not_ok"]
 
 L = capnproto_amd.load_library()
 L.cpk_debug_diag.restype = C.c_int
@@ -28,6 +28,24 @@ L.cpk_debug_diag.argtypes = [C.c_void_p, C.c_int]
 codec = capnproto_amd.Codec(0)
 buf = (C.c_uint64 * 16)()
 for name in sys.argv[2:]:
+    if name == "split":
+        # the bench's stream split: the whole stream decoded as one flat chunk
+        n = 1 << 20
+        off, total = codec.gen_offsets(n, seed=7)
+        words = codec.gen_messages("mixed", off, total, seed=7)
+        packed, poff, st = codec.pack_messages(words, off)
+        codec.sync()
+        nbytes = int(poff[-1].item())
+        L.cpk_debug_diag(buf, 1)
+        res = codec.split_packed_stream(packed, total + 16, n + 1, nbytes=nbytes)
+        codec.sync()
+        assert L.cpk_debug_diag(buf, 1) == 0
+        t = max(buf[0], 1)
+        print(name, "messages", int(res[4].item()), "tiles", buf[0], " ".join(
+            f"{NAMES[k]}={buf[k] / t:.3f}" for k in range(1, len(NAMES))), flush=True)
+        del words, packed, res
+        torch.cuda.empty_cache()
+        continue
     cfg = CONFIGS[name]
     n = cfg["nmsgs"]
     off, total = codec.gen_offsets(n, nseg=cfg["nseg"], seg_words=cfg["seg_words"], seed=1)

@@ -19,7 +19,7 @@ done
 for f in capnproto_amd/var_diag*.so; do
   [ -f $f ] || continue
   n=$(basename $f .so)
-  timeout -k 10 300 python3 tools/diag_unpack.py $f ${DIAG_CFGS:-c2 c3 c4} > gpurun_out/${TAG}_$n.log 2>&1
+  timeout -k 10 300 python3 tools/diag_unpack.py $f ${DIAG_CFGS:-c2 c3 c4 split} > gpurun_out/${TAG}_$n.log 2>&1
   rc=$?; echo "== $n"; grep -v amdgpu.ids gpurun_out/${TAG}_$n.log | tail -4; [ $rc = 0 ] || exit 1
 done
 if [ -n "$SPLIT" ]; then
@@ -31,5 +31,25 @@ import csv, glob, sys
 f = glob.glob(sys.argv[1] + "/*kernel_stats.csv")[0]
 for r in sorted(csv.DictReader(open(f)), key=lambda r: -float(r["TotalDurationNs"]))[:8]:
     print(r["Name"].split("(")[0][-40:], r["Calls"], round(float(r["AverageNs"]) / 1e3, 1), "us")
+PY
+fi
+if [ -n "$SMALL" ]; then
+  (cd /tmp && timeout -k 10 200 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d "$PWD_R/gpurun_out/${TAG}_small" -o run \
+    -- python3 "$PWD_R/tools/small_prof.py" 100 > "$PWD_R/gpurun_out/${TAG}_small.log" 2>&1) || { echo "small prof failed"; tail -5 gpurun_out/${TAG}_small.log; exit 1; }
+  grep "message_bytes" gpurun_out/${TAG}_small.log
+  python3 - gpurun_out/${TAG}_small <<'PY'
+import csv, glob, sys
+ev = []
+for f in glob.glob(sys.argv[1] + "/*kernel_trace.csv") + glob.glob(sys.argv[1] + "/*memory_copy_trace.csv"):
+    for r in csv.DictReader(open(f)):
+        name = r.get("Kernel_Name") or r.get("Direction") or "copy"
+        ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name.split("(")[0][-30:]))
+ev.sort()
+# the last 12 events: durations and gaps
+prev = None
+for s, e, n in ev[-12:]:
+    gap = (s - prev) / 1e3 if prev else 0.0
+    print(f"  {n:32s} dur {(e - s) / 1e3:7.1f} us  gap {gap:7.1f} us")
+    prev = e
 PY
 fi
