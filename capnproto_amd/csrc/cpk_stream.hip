@@ -233,6 +233,10 @@ struct SplitBlock {
   int32_t stop;          // kRunOn, or why the walk from the guess ended inside the block
   uint32_t over;         // more messages than the list holds
   uint64_t entry, kbase, kend;  // resolved: true entry (kNone: none), first / end global index
+  // the block walked from the previous block's guess exit (se; kNone: not done) -- its true
+  // entry whenever the previous block's true chain met its guess: messages, exit, stop
+  uint64_t se, sk, sx, shx;
+  int32_t sst;
 };
 
 __global__ __launch_bounds__(64) void split_spec_kernel(Flat F, const uint64_t* __restrict__ words,
@@ -299,6 +303,9 @@ __global__ __launch_bounds__(64) void split_spec_kernel(Flat F, const uint64_t* 
   if (l == 0) {
     r.entry = kNone;
     r.kbase = r.kend = 0;
+    r.se = kNone;
+    r.sk = r.sx = r.shx = 0;
+    r.sst = kRunOn;
     blocks[b] = r;
   }
 }
@@ -318,6 +325,52 @@ struct Meet2 {
     return readlane32(met ? 1u : 0u, 0) != 0;
   }
 };
+
+// Every block b > 0 walked, in parallel, from where block b - 1's guess chain leaves it until the
+// chain meets block b's guess chain (a few messages): block b's entry whenever block b - 1's true
+// chain met its guess, which the in-order pass below then only has to confirm.
+__global__ __launch_bounds__(64) void split_meet_kernel(Flat F, const uint64_t* __restrict__ words,
+                                                        uint64_t limit, SplitBlock* blocks,
+                                                        const uint64_t* __restrict__ lists,
+                                                        uint64_t nblocks) {
+  F.load();
+  const uint64_t b = (uint64_t)blockIdx.x + 1;
+  if (b >= nblocks) return;
+  const uint64_t pg = blocks[b - 1].g, E = blocks[b - 1].x, hE = blocks[b - 1].hx;
+  const int32_t pst = blocks[b - 1].stop;
+  const uint64_t g = blocks[b].g, gk = blocks[b].k;
+  const uint64_t w1 = (b + 1) * kSplitBlock;
+  uint64_t se = kNone, sk = 0, sx = 0, shx = 0;
+  int32_t sst = kRunOn;
+  if (pg != kNone && pst == kRunOn && E < w1 && E != g) {
+    const bool listed = g != kNone && gk <= kSplitList;
+    uint64_t jl = 0;
+    Meet2 mt{lists + b * kSplitList, listed ? gk : 0, &jl};
+    const WalkEnd we = walk_messages(F, words, E, hE, ~0ull, limit, w1,
+                                     [&](uint64_t, uint64_t, uint64_t) {}, mt);
+    jl = readlane64(jl, 0);
+    se = E;
+    if (we.stop == kMet) {
+      sk = we.k + (gk - jl);
+      sx = blocks[b].x;
+      shx = blocks[b].hx;
+      sst = blocks[b].stop;
+    } else {
+      sk = we.k;
+      sx = we.s;
+      shx = we.hs;
+      sst = we.stop;
+    }
+  }
+  if (lane_id() == 0) {
+    SplitBlock* const B = blocks + b;
+    B->se = se;
+    B->sk = sk;
+    B->sx = sx;
+    B->shx = shx;
+    B->sst = sst;
+  }
+}
 
 // One wave over the blocks in order: each block's true entry, global message range and the
 // stream's stop.  A block whose entry is its guess (or that the chain passes over) costs a load;
@@ -352,6 +405,13 @@ __global__ __launch_bounds__(64) void split_resolve_kernel(Flat F, const uint64_
         hx = readlane64(mine.hx, j);
         k = readlane64(mine.k, j);
         st = (int32_t)readlane32((uint32_t)mine.stop, j);
+      } else if (readlane64(mine.se, j) == E) {
+        // walked in parallel from this very entry (split_meet_kernel)
+        x = readlane64(mine.sx, j);
+        hx = readlane64(mine.shx, j);
+        k = readlane64(mine.sk, j);
+        st = (int32_t)readlane32((uint32_t)mine.sst, j);
+        redo = true;
       } else {
         // the guess was not the entry: walk the block from its true entry until the chain meets
         // the guess's chain (a guess whose chain ran to the block end without failing nearly
@@ -542,6 +602,7 @@ hipError_t launch_split_walk(const uint8_t* packed, uint64_t nbytes, const uint6
   SplitBlock* blocks = (SplitBlock*)scratch;
   uint64_t* lists = (uint64_t*)((char*)scratch + ((nb * sizeof(SplitBlock) + 15) & ~15ull));
   split_spec_kernel<<<(unsigned)nb, 64, 0, stream>>>(F, words, limit, blocks, lists);
+  if (nb > 1) split_meet_kernel<<<(unsigned)(nb - 1), 64, 0, stream>>>(F, words, limit, blocks, lists, nb);
   split_resolve_kernel<<<1, 64, 0, stream>>>(F, words, limit, max_msgs, blocks, lists, nb,
                                              msg_word_off, msg_in_off, status, nmsgs);
   split_write_kernel<<<(unsigned)nb, 64, 0, stream>>>(F, words, limit, blocks, lists,
