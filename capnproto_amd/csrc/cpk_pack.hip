@@ -265,6 +265,14 @@ __device__ __forceinline__ void copy_out_final(const uint32_t* stg, uint32_t n, 
 //    when this tile's first word goes on with the stretch the previous tile ended in; the
 //    previous tile publishes it right after its classes when it holds a sync point.  (A tile
 //    only waits on lower ones, dispatched before it.)
+#ifdef CPK_DIAG
+// diagnostic build only: 0 tiles, 1 offset known in time, 2 slot taken, 3 waited for the offset
+__device__ unsigned long long g_pdiag[4];
+#define CPK_PDIAG(k, v) atomicAdd(&g_pdiag[k], (unsigned long long)(v))
+#else
+#define CPK_PDIAG(k, v)
+#endif
+
 #ifndef CPK_PACK_TICKET
 #define CPK_PACK_TICKET 0  // 1: persistent workgroups take tiles by ticket, next tile's loads early
 #endif
@@ -682,6 +690,10 @@ pack_tile_kernel(PackTileArgs a) {
           if (slot < a.nslots) break;
           slot = ~0u;
           wait = true;
+        }
+        if (l == 0) {
+          CPK_PDIAG(0, 1);
+          CPK_PDIAG(wait ? 3 : (slot != ~0u ? 2 : 1), 1);
         }
         ok = ok && ex + agg <= a.out_capacity;  // (too small an output: placement raises it)
         if (l == 0) {
@@ -1458,3 +1470,15 @@ hipError_t launch_pack_place(const PackTileArgs& a, hipStream_t stream) {
 }
 
 }  // namespace cpk
+
+#ifdef CPK_DIAG
+extern "C" int cpk_debug_pdiag(uint64_t* out, int reset) {
+  if (hipDeviceSynchronize() != hipSuccess) return 10;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(cpk::g_pdiag), 4 * sizeof(uint64_t)) != hipSuccess) return 10;
+  if (reset) {
+    const uint64_t z[4] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(cpk::g_pdiag), z, sizeof z) != hipSuccess) return 10;
+  }
+  return 0;
+}
+#endif

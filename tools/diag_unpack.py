@@ -25,6 +25,9 @@ NAMES = ["tiles", "walk0_trips", "walk0_lane_steps", "rewalk_trips", "rewalk_lan
 L = capnproto_amd.load_library()
 L.cpk_debug_diag.restype = C.c_int
 L.cpk_debug_diag.argtypes = [C.c_void_p, C.c_int]
+L.cpk_debug_pdiag.restype = C.c_int
+L.cpk_debug_pdiag.argtypes = [C.c_void_p, C.c_int]
+pbuf = (C.c_uint64 * 4)()
 codec = capnproto_amd.Codec(0)
 buf = (C.c_uint64 * 16)()
 for name in sys.argv[2:]:
@@ -54,8 +57,13 @@ for name in sys.argv[2:]:
     packed = torch.empty(cap, dtype=torch.uint8, device=codec.device)
     moff = torch.empty(n + 1, dtype=torch.int64, device=codec.device)
     back = torch.empty(total, dtype=torch.int64, device=codec.device)
+    codec.pack_messages(words, off, out=packed, msg_out_off=moff)  # (first call: allocations)
+    codec.sync()
+    L.cpk_debug_pdiag(pbuf, 1)
     codec.pack_messages(words, off, out=packed, msg_out_off=moff)
     codec.sync()
+    assert L.cpk_debug_pdiag(pbuf, 1) == 0
+    print(name, "pack tiles", pbuf[0], "in_time", pbuf[1], "slot", pbuf[2], "waited", pbuf[3], flush=True)
     P = int(moff[-1].item())
     L.cpk_debug_diag(buf, 1)
     codec.unpack_messages(packed, moff, total, nbytes=P, words=back)
