@@ -298,7 +298,7 @@ PackScratch carve_pack(void* base, uint64_t N, uint64_t ntiles, bool direct) {
   s.thole = c.take<uint32_t>(ntiles);
   s.tpatch = c.take<uint32_t>(ntiles);
   s.tslot = c.take<uint32_t>(ntiles);
-  s.nslots = (uint32_t)(ntiles < cpk::kPackSlots ? ntiles : cpk::kPackSlots);
+  s.nslots = (uint32_t)(cpk::kPackSlots == 0 || ntiles < cpk::kPackSlots ? ntiles : cpk::kPackSlots);
   s.scr = c.take<uint8_t>(s.nslots * cpk::kPackScratchBytes + 16);
   s.total = c.off;
   return s;

@@ -9,7 +9,10 @@ namespace cpk {
 
 constexpr uint64_t kPackTileWords = 2048;       // words per workgroup tile (cpk_pack.hip)
 constexpr uint64_t kPackScratchBytes = 10 * kPackTileWords;  // a tile's packed bytes, worst case
-constexpr uint64_t kPackSlots = 2048;  // slot pool: a tile finding none waits for its offset
+#ifndef CPK_PACK_SLOTS
+#define CPK_PACK_SLOTS 2048  // slot pool: a tile finding none waits for its offset (0: one per tile)
+#endif
+constexpr uint64_t kPackSlots = CPK_PACK_SLOTS;
 constexpr uint64_t kUnpackTileBytes = 4096;     // packed bytes per unpack tile (>= 2050)
 
 struct PackTileArgs {

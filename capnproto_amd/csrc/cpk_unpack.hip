@@ -350,7 +350,7 @@ __device__ __forceinline__ bool settle(const uint8_t* d, const SubTile& st, uint
   for (int iter = 0; iter < 96; iter++) {
     if (iters) iters[0] = iter + 1;
 #ifdef CPK_DIAG
-    if (iter) diag_trips(3, iters[1] - iters[2]), iters[2] = iters[1];
+    if (iter && iters) diag_trips(3, iters[1] - iters[2]), iters[2] = iters[1];
 #endif
     // the largest exit of the earlier lanes (wave_shr:1 of the inclusive max: no LDS trip)
     const uint32_t incl = wave_incl_max32(pass ? 0u : (uint32_t)out);
@@ -1418,7 +1418,7 @@ __device__ __forceinline__ void expand_records(const UnpackArgs& a, uint64_t A, 
 }
 
 #ifndef CPK_PREWALK
-#define CPK_PREWALK 0  // bytes of unmarked walk before each sub-tile (0: none; at most 64)
+#define CPK_PREWALK 64  // bytes of unmarked walk before each sub-tile (0: none; at most 64)
 #endif
 #ifndef CPK_UNPACK_WPE
 #define CPK_UNPACK_WPE 7  // 72 VGPRs: 7 waves per SIMD (LDS allows 7); 6 at the unconstrained 80
