@@ -109,8 +109,15 @@ cpk_status ensure_pinned(void** p, size_t* size, size_t need) {
 // Host entry points stage through one pinned buffer and one device buffer when the whole call
 // fits in this many bytes each way (larger batches keep the per-buffer copies).
 constexpr size_t kHostIoMax = 64ull << 20;
-// Inputs up to this size are read by the kernels straight from the pinned buffer (no upload).
-constexpr size_t kZeroCopyMax = 256 << 10;
+// Inputs up to this size are read by the kernels straight from the pinned buffer (no upload);
+// CPK_HOST_ZERO_COPY (bytes) overrides it.
+size_t zero_copy_max() {
+  static const size_t v = [] {
+    const char* e = getenv("CPK_HOST_ZERO_COPY");
+    return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)(256 << 10);
+  }();
+  return v;
+}
 
 // Staging of one host call.  Device buffer: [error word, 16 B][results][inputs (uploaded)]; the
 // error word is zero at rest and stands in for the context's for the call, so one download
@@ -137,7 +144,7 @@ cpk_status host_io(cpk_ctx* ctx, size_t in_bytes, size_t out_bytes, HostIo* io) 
   uint8_t* const hb = (uint8_t*)ctx->hio;
   uint8_t* const db = (uint8_t*)ctx->dio;
   io->hin = hb;
-  io->upload = in_bytes > kZeroCopyMax;
+  io->upload = in_bytes > zero_copy_max();
   io->din = db + 16 + out_bytes;
   if (!io->upload && hipHostGetDevicePointer((void**)&io->din, hb, 0) != hipSuccess)
     return CPK_ERR_HIP;
@@ -319,9 +326,10 @@ cpk_status pack_common(cpk_ctx* ctx, const uint64_t* d_words, uint64_t N, const 
   if (order_streams(ctx, stream) != CPK_OK) return CPK_ERR_HIP;
   const uint64_t T = cpk::kPackTileWords;
   const uint64_t ntiles = (N + T - 1) / T;
-  // a batch of one tile (a single small message) takes the direct kernel: its offset is 0, so
-  // no scan and no placement launch (two launches per call in all)
-  const bool direct = CPK_PACK_DIRECT || ntiles == 1;
+  // a batch of one tile (a single small message): one launch, the tile kernel framing the batch
+  // itself and writing its bytes at offset 0 (no framing or placement launch)
+  const bool direct = CPK_PACK_DIRECT;
+  const bool single = !direct && ntiles == 1;
   cpk_status st = ensure(&ctx->scratch, &ctx->scratch_size,
                          carve_pack(nullptr, N, ntiles, direct).total + 64);
   if (st != CPK_OK) return st;
@@ -348,9 +356,10 @@ cpk_status pack_common(cpk_ctx* ctx, const uint64_t* d_words, uint64_t N, const 
     return CPK_OK;
   }
   if (messages && n == 0) return CPK_ERR_INVALID_ARGUMENT;  // words outside any message
-  hipError_t e = messages ? cpk::launch_message_bits(d_words, d_off, n, bits, tstarts, d_status,
-                                                     tf, stream)
-                          : cpk::launch_chunk_bits(d_off, n, N, bits, tstarts, tf, stream);
+  hipError_t e = hipSuccess;
+  if (!single)
+    e = messages ? cpk::launch_message_bits(d_words, d_off, n, bits, tstarts, d_status, tf, stream)
+                 : cpk::launch_chunk_bits(d_off, n, N, bits, tstarts, tf, stream);
   // the bitmap is zero at rest only if the tile kernel runs and clears it: after any failure
   // from here on it is cleared here
   auto clear_bits = [&]() {
@@ -389,6 +398,10 @@ cpk_status pack_common(cpk_ctx* ctx, const uint64_t* d_words, uint64_t N, const 
   a.desc = s.desc;
   a.gword = s.gword;
   a.gincl = s.gincl;
+  a.frame_mode = single ? (messages ? 1u : 2u) : 0u;
+  a.frame_off = d_off;
+  a.frame_n = n;
+  a.frame_status = d_status;
   TimedLaunch tl(ctx, 0, stream);
   if (direct) {
     e = cpk::launch_pack_direct(a, stream);
@@ -400,7 +413,7 @@ cpk_status pack_common(cpk_ctx* ctx, const uint64_t* d_words, uint64_t N, const 
   // of the placement launch
   e = cpk::launch_pack_tiles(a, stream);
   if (e != hipSuccess) clear_bits();
-  if (e == hipSuccess) e = cpk::launch_pack_place(a, stream);
+  if (e == hipSuccess && !single) e = cpk::launch_pack_place(a, stream);
   tl.done();
   return hip_status(e);
 }

@@ -141,6 +141,54 @@ __device__ __forceinline__ uint64_t compact_nonzero(uint64_t x) {
 // (it reasons per lane and may otherwise reorder a lane's access past another lane's).
 __device__ __forceinline__ void lane_handoff() { asm volatile("" ::: "memory"); }
 
+// Marks word p as a chunk start (and, at a pack tile start, the tile's byte: plain byte stores,
+// no atomics -- a word shared by 64 tiles, OR-ed and AND-ed by atomics, cost the tile kernel
+// half its speed in contention).
+__device__ __forceinline__ void mark_chunk(unsigned long long* bits, uint8_t* tstarts,
+                                           uint64_t p) {
+  atomicOr(bits + (p >> 6), 1ull << (p & 63));
+  if (p % kPackTileWords == 0 && p) tstarts[p / kPackTileWords] = 1;  // (tile 0: no predecessor)
+}
+
+// Chunk starts of message i = words[off[i], off[i+1]) -- segment table (serializeSegmentTable
+// serialize.c++:311-330) then segments; chunk starts = message start, table end, each segment
+// start -- and its framing status (cpk_frame.hip's message_bits_kernel; the pack tile kernel
+// calls it itself for a single-tile batch).
+__device__ __forceinline__ void frame_message(const uint64_t* __restrict__ words,
+                                              const uint64_t* __restrict__ off, uint64_t i,
+                                              unsigned long long* __restrict__ bits,
+                                              uint8_t* __restrict__ tstarts,
+                                              int32_t* __restrict__ status) {
+  const uint64_t w0 = off[i], w1 = off[i + 1];
+  int32_t st = 0;
+  if (w1 <= w0) {
+    if (status) status[i] = 11;  // CPK_ERR_EMPTY_MESSAGE
+    return;
+  }
+  mark_chunk(bits, tstarts, w0);
+  const uint64_t nw = w1 - w0;
+  const uint32_t* t32 = (const uint32_t*)(words + w0);
+  const uint64_t nseg = (uint64_t)t32[0] + 1;
+  const uint64_t tw = nseg / 2 + 1;
+  bool ok = tw <= nw;
+  if (ok) {
+    uint64_t total = tw;
+    for (uint64_t s = 0; s < nseg && total <= nw; s++) total += t32[s + 1];
+    ok = total == nw;
+  }
+  if (!ok) {
+    st = 6;  // CPK_ERR_BAD_FRAMING: packed as one chunk
+  } else {
+    uint64_t p = w0 + tw;
+    if (p < w1) mark_chunk(bits, tstarts, p);
+    for (uint64_t s = 0; s + 1 < nseg; s++) {
+      p += t32[s + 1];
+      if (p < w1) mark_chunk(bits, tstarts, p);
+    }
+  }
+  if (status) status[i] = st;
+}
+
 // Workgroup barrier ordering LDS only: __syncthreads also releases global memory at workgroup
 // scope, which waits for every outstanding vector memory operation -- stores, and loads issued
 // ahead for later use.

@@ -10,14 +10,6 @@
 namespace cpk {
 namespace {
 
-// Marks word p as a chunk start (and, at a pack tile start, the tile's byte: plain byte stores,
-// no atomics -- a word shared by 64 tiles, OR-ed and AND-ed by atomics, cost the tile kernel
-// half its speed in contention).
-__device__ __forceinline__ void mark(unsigned long long* bits, uint8_t* tstarts, uint64_t p) {
-  atomicOr(bits + (p >> 6), 1ull << (p & 63));
-  if (p % kPackTileWords == 0 && p) tstarts[p / kPackTileWords] = 1;  // (tile 0: no predecessor)
-}
-
 // Chunk-start bitmap + per-message framing status for a batch of flat messages.
 // Message i = words[off[i], off[i+1]): segment table (serializeSegmentTable serialize.c++:
 // 311-330) then segments; chunk starts = message start, table end, each segment start.
@@ -30,34 +22,7 @@ __global__ void message_bits_kernel(const uint64_t* __restrict__ words,
   if (run_tile_first(tf, tf_block)) return;
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const uint64_t w0 = off[i], w1 = off[i + 1];
-  int32_t st = 0;
-  if (w1 <= w0) {
-    if (status) status[i] = 11;  // CPK_ERR_EMPTY_MESSAGE
-    return;
-  }
-  mark(bits, tstarts, w0);
-  const uint64_t nw = w1 - w0;
-  const uint32_t* t32 = (const uint32_t*)(words + w0);
-  const uint64_t nseg = (uint64_t)t32[0] + 1;
-  const uint64_t tw = nseg / 2 + 1;
-  bool ok = tw <= nw;
-  if (ok) {
-    uint64_t total = tw;
-    for (uint64_t s = 0; s < nseg && total <= nw; s++) total += t32[s + 1];
-    ok = total == nw;
-  }
-  if (!ok) {
-    st = 6;  // CPK_ERR_BAD_FRAMING: packed as one chunk
-  } else {
-    uint64_t p = w0 + tw;
-    if (p < w1) mark(bits, tstarts, p);
-    for (uint64_t s = 0; s + 1 < nseg; s++) {
-      p += t32[s + 1];
-      if (p < w1) mark(bits, tstarts, p);
-    }
-  }
-  if (status) status[i] = st;
+  frame_message(words, off, i, bits, tstarts, status);
 }
 
 __global__ void chunk_bits_kernel(const uint64_t* __restrict__ off, uint64_t n, uint64_t N,
@@ -66,10 +31,10 @@ __global__ void chunk_bits_kernel(const uint64_t* __restrict__ off, uint64_t n, 
                                   uint32_t tf_block) {
   if (run_tile_first(tf, tf_block)) return;
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i == 0 && N > 0) mark(bits, tstarts, 0);  // word 0 always starts a chunk
+  if (i == 0 && N > 0) mark_chunk(bits, tstarts, 0);  // word 0 always starts a chunk
   if (i >= n) return;
   const uint64_t p = off[i];
-  if (p < N && off[i + 1] > p) mark(bits, tstarts, p);
+  if (p < N && off[i + 1] > p) mark_chunk(bits, tstarts, p);
 }
 
 }  // namespace

@@ -48,6 +48,13 @@ struct PackTileArgs {
   // (direct kernel)
   uint32_t* ticket;
   uint32_t* tile_ticket;       // tile kernel built with CPK_PACK_TICKET: tiles taken (zeroed)
+  // single-tile batches: the framing launch's work done by the tile kernel itself (frame_mode 1:
+  // message batch, frame_off = message word offsets, statuses to frame_status; 2: chunk
+  // offsets; 0: framed by the framing launch)
+  uint32_t frame_mode;
+  const uint64_t* frame_off;
+  uint64_t frame_n;
+  int32_t* frame_status;
   uint64_t* desc;
   uint64_t* gword;
   uint64_t* gincl;

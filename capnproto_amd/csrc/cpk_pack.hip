@@ -273,6 +273,9 @@ __device__ unsigned long long g_pdiag[4];
 #define CPK_PDIAG(k, v)
 #endif
 
+#ifndef CPK_PACK_OPP
+#define CPK_PACK_OPP 1  // 0 (with CPK_PACK_SLOTS=0): no look-back in the tile kernel, a slot per tile
+#endif
 #ifndef CPK_PACK_TICKET
 #define CPK_PACK_TICKET 0  // 1: persistent workgroups take tiles by ticket, next tile's loads early
 #endif
@@ -323,7 +326,7 @@ __device__ __forceinline__ void tile_loads(const PackTileArgs& a, uint64_t T, in
   const uint64_t nbi = T + 1 + (uint64_t)opaque_zero();  // the next tile's start byte
   L.nb0 = a.tile_starts[nbi];
   typedef const __attribute__((address_space(4))) uint64_t cu64;
-  const uint64_t pidx = a.pos ? *((cu64*)a.tile_first + T) : 0;  // scalar load
+  const uint64_t pidx = a.pos && !a.frame_mode ? *((cu64*)a.tile_first + T) : 0;  // scalar load
   const uint64_t pi = pidx + l;
   L.p00 = (a.pos ? a.pos : a.words)[a.pos && pi <= a.npos ? pi : 0];
 }
@@ -371,6 +374,21 @@ pack_tile_kernel(PackTileArgs a) {
 #else
   const uint64_t T = blockIdx.x;
   const int l = lane_id();
+  if (a.frame_mode) {
+    // a single-tile batch: the framing launch's work first (chunk starts, statuses)
+    unsigned long long* const cb = (unsigned long long*)a.chunk_bits;
+    if (a.frame_mode == 1) {
+      for (uint64_t i = tid; i < a.frame_n; i += 64 * kWv)
+        frame_message(a.words, a.frame_off, i, cb, a.tile_starts, a.frame_status);
+    } else {
+      if (tid == 0) mark_chunk(cb, a.tile_starts, 0);  // word 0 always starts a chunk
+      for (uint64_t i = tid; i < a.frame_n; i += 64 * kWv) {
+        const uint64_t p = a.frame_off[i];
+        if (p < N && a.frame_off[i + 1] > p) mark_chunk(cb, a.tile_starts, p);
+      }
+    }
+    __syncthreads();  // (the bitmap's atomics are done at the L2; no wave has read it yet)
+  }
   TileLoads cur;
   tile_loads(a, T, w, l, cur);
   for (int i = tid; i < kSlotDw / 4; i += 64 * kWv) ((u32x4*)stg)[i] = (u32x4){0, 0, 0, 0};
@@ -389,7 +407,7 @@ pack_tile_kernel(PackTileArgs a) {
   const uint64_t xw0 = cur.xw0, nb0 = cur.nb0;
   const uint64_t nbi = T + 1 + (uint64_t)opaque_zero();  // the next tile's start byte
   typedef const __attribute__((address_space(4))) uint64_t cu64;
-  const uint64_t pidx = a.pos ? *((cu64*)a.tile_first + T) : 0;  // scalar load
+  const uint64_t pidx = a.pos && !a.frame_mode ? *((cu64*)a.tile_first + T) : 0;  // scalar load
   const uint64_t pi = pidx + l;
   const bool pv = a.pos && pi <= a.npos;
   const uint64_t cbw = cbi < nbitw ? cur.cb0 : 0;
@@ -682,6 +700,11 @@ pack_tile_kernel(PackTileArgs a) {
         uint64_t ex = 0;
         bool ok = T == 0, wait = windowed;
         uint32_t slot = ~0u;
+#if !CPK_PACK_OPP
+        // (variant: no look-back here -- every tile but oversized ones to its own slot)
+        if (!ok && !wait && T < a.nslots) slot = (uint32_t)T;
+        else
+#endif
         while (!ok) {
           ok = pack_lookback(a.desc, T, &ex, wait, a.err);
           if (ok || wait) break;
@@ -727,6 +750,15 @@ pack_tile_kernel(PackTileArgs a) {
       for (int i = tid; i < kSlotDw / 4; i += 64 * kWv) ((u32x4*)stg)[i] = (u32x4){0, 0, 0, 0};
       lds_barrier();
     }
+  }
+  if (a.frame_mode) {
+    // (a single-tile batch has no placement launch) the total for the positions at the batch
+    // end; a tile the output cannot hold raises the capacity error here
+    if (tid == 0 && uniform64(s_dst) == ~0ull) raise_error(a.err, kErrCapacity);
+    if (a.pos)
+      for (uint64_t i = tid; i <= a.npos; i += 64 * kWv)
+        if (a.pos[i] >= N) a.pos_out[i] = agg;
+    if (a.total_out && tid == 0) *a.total_out = agg;
   }
 #if CPK_PACK_TICKET
   if (Tn >= a.ntiles) break;

@@ -34,10 +34,12 @@ for r in sorted(csv.DictReader(open(f)), key=lambda r: -float(r["TotalDurationNs
 PY
 fi
 if [ -n "$SMALL" ]; then
-  (cd /tmp && timeout -k 10 200 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d "$PWD_R/gpurun_out/${TAG}_small" -o run \
-    -- python3 "$PWD_R/tools/small_prof.py" 100 > "$PWD_R/gpurun_out/${TAG}_small.log" 2>&1) || { echo "small prof failed"; tail -5 gpurun_out/${TAG}_small.log; exit 1; }
-  grep "message_bytes" gpurun_out/${TAG}_small.log
-  python3 - gpurun_out/${TAG}_small <<'PY'
+  for zc in default 0; do
+  if [ $zc = default ]; then unset CPK_HOST_ZERO_COPY; else export CPK_HOST_ZERO_COPY=$zc; fi
+  (cd /tmp && timeout -k 10 200 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d "$PWD_R/gpurun_out/${TAG}_small_$zc" -o run \
+    -- python3 "$PWD_R/tools/small_prof.py" 100 > "$PWD_R/gpurun_out/${TAG}_small_$zc.log" 2>&1) || { echo "small prof failed"; tail -5 gpurun_out/${TAG}_small_$zc.log; exit 1; }
+  echo "== small zero-copy=$zc"; grep "message_bytes" gpurun_out/${TAG}_small_$zc.log
+  python3 - gpurun_out/${TAG}_small_$zc <<'PY'
 import csv, glob, sys
 ev = []
 for f in glob.glob(sys.argv[1] + "/*kernel_trace.csv") + glob.glob(sys.argv[1] + "/*memory_copy_trace.csv"):
@@ -45,11 +47,12 @@ for f in glob.glob(sys.argv[1] + "/*kernel_trace.csv") + glob.glob(sys.argv[1] +
         name = r.get("Kernel_Name") or r.get("Direction") or "copy"
         ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name.split("(")[0][-30:]))
 ev.sort()
-# the last 12 events: durations and gaps
 prev = None
 for s, e, n in ev[-12:]:
     gap = (s - prev) / 1e3 if prev else 0.0
     print(f"  {n:32s} dur {(e - s) / 1e3:7.1f} us  gap {gap:7.1f} us")
     prev = e
 PY
+  done
+  unset CPK_HOST_ZERO_COPY
 fi
