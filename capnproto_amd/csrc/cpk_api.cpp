@@ -504,13 +504,17 @@ cpk_status unpack_common(cpk_ctx* ctx, uint32_t mode, const uint8_t* d_packed, u
   tf.outpos = s.tile_firstpos;
   tf.zero = (uint64_t*)ctx->scratch;  // zeroed in the header / init launch
   tf.zero_words = s.zero_bytes / 8;
+  // a single-tile batch of few messages: one launch, the tile kernel reading the headers itself
+  const bool fuse = mode == 0 && ntiles == 1 && n <= cpk::kUnpackFuseMsgs;
   if (mode == 0) {
     if (!d_word_off_out) return CPK_ERR_INVALID_ARGUMENT;
     if (n == 0) return hip_status(cpk::launch_fill(d_word_off_out, 8, 0, stream));
     if ((st = ensure_hdr_desc(ctx, n)) != CPK_OK) return st;
-    e = cpk::launch_unpack_header(d_packed, d_in_off, n, limit, d_word_off_out, s.hdr_status,
-                                  d_status, ctx->hdr_desc, ctx->err, tf, stream);
-    if (e != hipSuccess) return CPK_ERR_HIP;
+    if (!fuse) {
+      e = cpk::launch_unpack_header(d_packed, d_in_off, n, limit, d_word_off_out, s.hdr_status,
+                                    d_status, ctx->hdr_desc, ctx->err, tf, stream);
+      if (e != hipSuccess) return CPK_ERR_HIP;
+    }
     word_off = d_word_off_out;
     if (ntiles == 0)  // no tile kernel to clear the header launch's descriptors
       return hip_status(cpk::launch_fill(ctx->hdr_desc, 8 * cpk::header_scan_blocks(n), 0, stream));
@@ -544,7 +548,11 @@ cpk_status unpack_common(cpk_ctx* ctx, uint32_t mode, const uint8_t* d_packed, u
   a.stamps = cpk::debug_stamps(1);  // diagnostic counters (CPK_STAMPS=1), else NULL
   a.debug_skip = cpk::debug_skip();
   a.hdr_desc = ctx->hdr_desc;
-  a.hdr_nblocks = mode == 0 ? cpk::header_scan_blocks(n) : 0;
+  a.hdr_nblocks = mode == 0 && !fuse ? cpk::header_scan_blocks(n) : 0;
+  a.hdr_fuse = fuse ? 1u : 0u;
+  a.hdr_limit = limit;
+  a.hdr_word_off = d_word_off_out;
+  a.hdr_status_out = s.hdr_status;
   TimedLaunch tl(ctx, 1, stream);
   for (int stage = cpk::kUnpackTiles; stage <= cpk::kUnpackTiles; stage++) {
     TimedLaunch tk(ctx, 2 + stage, stream);

@@ -114,7 +114,14 @@ struct UnpackArgs {
   const uint64_t* tile_firstpos;  // in_off[tile_first[t]]: the first message start >= tile start
   uint64_t* hdr_desc;           // the header launch's scan descriptors (zero at rest): cleared
   uint64_t hdr_nblocks;         // by the tile kernel once the headers are done (0: none)
+  // a single-tile message batch of at most kUnpackFuseMsgs messages: the header launch's work
+  // (headers, word offsets, statuses) done by the tile kernel itself (0: header launch ran)
+  uint32_t hdr_fuse;
+  uint64_t hdr_limit;
+  uint64_t* hdr_word_off;
+  int32_t* hdr_status_out;
 };
+constexpr uint64_t kUnpackFuseMsgs = 256;
 
 // Unpack stages (launch_unpack_stage), in launch order: the tile kernel is the only one.
 constexpr int kUnpackTiles = 0;

@@ -1436,6 +1436,27 @@ unpack_tiles_kernel(UnpackArgs a) {
   const int l = lane_id();
   const int wv = (int)uniform32(threadIdx.x >> 6);  // wave-uniform (keeps tile math scalar)
   dep_tab[threadIdx.x] = make_dep(threadIdx.x);
+  if (a.hdr_fuse) {
+    // a single-tile batch of few messages: the header launch's work first, one message per
+    // thread (serialize.c++:202-242 via header_words), the word offsets by one block scan
+    __shared__ uint64_t s_hw[4];
+    const uint64_t m = threadIdx.x;
+    uint64_t w = 0;
+    if (m < a.nmsgs) {
+      int32_t hst;
+      w = header_words(a.packed, a.in_off, m, a.hdr_limit, &hst);
+      a.hdr_status_out[m] = hst;
+      a.status[m] = hst;
+    }
+    const uint64_t inc = wave_incl_sum64(w);
+    if (l == 63) s_hw[wv] = inc;
+    __syncthreads();
+    uint64_t before = 0;
+    for (int v = 0; v < wv; v++) before += s_hw[v];
+    const uint64_t o = before + inc - w;
+    if (m < a.nmsgs) a.hdr_word_off[m] = o;
+    if (m + 1 == a.nmsgs) a.hdr_word_off[a.nmsgs] = o + w;
+  }
   __syncthreads();
   const uint64_t t = (uint64_t)blockIdx.x * 4 + wv;
   if (t >= a.ntiles) return;
@@ -1448,7 +1469,7 @@ unpack_tiles_kernel(UnpackArgs a) {
   const uint64_t A = t * kB;
   Staged stg;
   stage_load(a, A, stg);
-  const uint64_t mfirst = uniform64(a.tile_first[t]);
+  const uint64_t mfirst = a.hdr_fuse ? 0 : uniform64(a.tile_first[t]);
   stage_store(stg, d);
   MsgWin win;
   int nms_tile_after;
