@@ -54,6 +54,10 @@ constexpr int kB = (int)kUnpackTileBytes;  // 4096
 constexpr int kPad = 16;
 constexpr int kDead = 1 << 24;  // chain ran into the end of the batch
 
+#ifndef CPK_LIST2
+#define CPK_LIST2 0  // 1: record lists built from both ends of each lane's bits (half the steps)
+#endif
+
 #ifdef CPK_DIAG
 __device__ __forceinline__ void diag_add(int k, uint64_t v) {
   if (lane_id() == 0) atomicAdd(&g_diag[k], (unsigned long long)v);
@@ -1234,11 +1238,25 @@ __device__ __forceinline__ void expand_records(const UnpackArgs& a, uint64_t A, 
       const uint32_t nh = readlane32(Rin, 63);
       uint32_t r = Rin - c;
       const uint32_t pbase = 64u * (uint32_t)src + sh;
+#if CPK_LIST2
+      // from both ends, the lowest and the highest start per step (an odd last step writes its
+      // one start twice, to the same entry)
+      uint32_t rh = Rin - 1;
+      while (bits) {
+        const uint32_t b = (uint32_t)__builtin_ctz(bits);
+        bits &= bits - 1;
+        const uint32_t bh = bits ? 31u - (uint32_t)__builtin_clz(bits) : b;
+        bits &= ~(1u << bh);
+        list[r++] = (uint16_t)(pbase + b);
+        list[rh--] = (uint16_t)(pbase + bh);
+      }
+#else
       while (bits) {
         const uint32_t b = (uint32_t)__builtin_ctz(bits);
         bits &= bits - 1;
         list[r++] = (uint16_t)(pbase + b);
       }
+#endif
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       for (uint32_t b0 = 0; b0 < ((a.debug_skip & 16) ? 0u : nh); b0 += 64) {
         const uint32_t rr = b0 + l;
@@ -1295,11 +1313,23 @@ __device__ __forceinline__ void expand_records(const UnpackArgs& a, uint64_t A, 
     const uint32_t nh = readlane32(Rin, 63);
     uint32_t r = Rin - c;
     const uint32_t pbase = 64u * (uint32_t)src + sh;
+#if CPK_LIST2
+    uint32_t rh = Rin - 1;
+    while (bits) {  // (from both ends, as above)
+      const uint32_t b = (uint32_t)__builtin_ctz(bits);
+      bits &= bits - 1;
+      const uint32_t bh = bits ? 31u - (uint32_t)__builtin_clz(bits) : b;
+      bits &= ~(1u << bh);
+      list[r++] = (uint16_t)((pbase + b) | (((msp >> b) & 1u) << 12));
+      list[rh--] = (uint16_t)((pbase + bh) | (((msp >> bh) & 1u) << 12));
+    }
+#else
     while (bits) {
       const uint32_t b = (uint32_t)__builtin_ctz(bits);
       bits &= bits - 1;
       list[r++] = (uint16_t)((pbase + b) | (((msp >> b) & 1u) << 12));
     }
+#endif
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     for (uint32_t b0 = 0; b0 < ((a.debug_skip & 16) ? 0u : nh); b0 += 64) {
       const uint32_t rr = b0 + l;
