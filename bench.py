@@ -587,7 +587,9 @@ def main():
                                      if cb else ""),
             "roofline": s["roofline"],
             "cpu_baseline": cb,
-            "kernels": {"pack": "pack_tile + scan + pack_place (capnproto_amd/csrc/cpk_pack.hip)",
+            "kernels": {"pack": "framing + pack_tile (tiles whose offset is known in time write "
+                                "straight out, the rest to a bounded slot pool) + pack_place "
+                                "(look-back offsets, slot copies) (capnproto_amd/csrc/cpk_pack.hip)",
                         "unpack": "header (+ word-offset scan, tile_first, scratch zeroing) + "
                                   "unpack_tiles (capnproto_amd/csrc/cpk_unpack.hip)",
                         "knobs": knobs},
