@@ -33,7 +33,7 @@ namespace cpk {
 
 #ifdef CPK_DIAG
 // diagnostic build only (-DCPK_DIAG): per-phase step counters, read by cpk_debug_diag
-__device__ unsigned long long g_diag[16];
+__device__ unsigned long long g_diag[32];
 #endif
 
 namespace {
@@ -1490,6 +1490,7 @@ unpack_tiles_kernel(UnpackArgs a) {
   __syncthreads();
   const uint64_t t = (uint64_t)blockIdx.x * 4 + wv;
   if (t >= a.ntiles) return;
+  CPK_DIAG_ONLY(uint64_t ck[7]; ck[0] = clock64());
   // the header launch is done: its scan descriptors go back to zero for the next call
   for (uint64_t i = t + a.ntiles * (uint64_t)l; i < a.hdr_nblocks; i += 64 * a.ntiles)
     a.hdr_desc[i] = 0;
@@ -1507,6 +1508,7 @@ unpack_tiles_kernel(UnpackArgs a) {
   const uint64_t msw = aux[l];
   lane_handoff();
   const SubTile st = make_subtile(A, P, msw, nms_tile_after);
+  CPK_DIAG_ONLY(ck[1] = clock64());
   if (a.debug_skip & 64) {  // diagnostic: staging + message window only
     if (l == 0 && st.msw == 0) a.x0p[t] = 0x80000000u | (uint32_t)ballot(st.msw != 0);
     return;
@@ -1578,6 +1580,7 @@ unpack_tiles_kernel(UnpackArgs a) {
     }
   }
   if (l == 0) store_agent32(a.x0p + t, 0x80000000u | x0);
+  CPK_DIAG_ONLY(ck[2] = ck[3] = ck[4] = ck[5] = clock64());
   if (a.debug_skip & 128) return;  // diagnostic: + chain-0 walks and settle
   if (!settled) {
     // unreachable (the fixed point settles in at most 64 rounds): refuse the batch, write nothing
@@ -1614,6 +1617,7 @@ unpack_tiles_kernel(UnpackArgs a) {
   } else {
     // optimistic entry: where the predecessor's chain 0 leads
     const uint32_t xp = wait_nonzero32(a.x0p + t - 1, a.err) & 0x7fffffffu;
+    CPK_DIAG_ONLY(ck[3] = ck[4] = ck[5] = clock64());
     const uint32_t Eopt = entry_from_exit(xp, fms);
     uint32_t xE = x0;
     uint64_t runs = runm;
@@ -1628,7 +1632,9 @@ unpack_tiles_kernel(UnpackArgs a) {
       CPK_DIAG_ONLY(diag_add(14, xE != x0));
     }
     uint32_t xprev = xp;
+    CPK_DIAG_ONLY(ck[4] = clock64());
     if (!(a.debug_skip & 8)) excl = lookback_tiles(a, t, &xprev);
+    CPK_DIAG_ONLY(ck[5] = clock64());
     const uint32_t E = entry_from_exit(xprev, fms);
     CPK_DIAG_ONLY(diag_add(9, E != Eopt); diag_add(10, Eopt > 0 && Eopt < fms));
     if (E != Eopt) {
@@ -1659,6 +1665,10 @@ unpack_tiles_kernel(UnpackArgs a) {
   if (a.debug_skip & 256) return;  // diagnostic: + the entry and the look-back
   expand_records<PLAIN>(a, A, d, aux, dep_tab, deposit_sel((uint32_t)l & 15), tm, excl, win, mfirst,
                  mlast, msw, w_tile);
+#ifdef CPK_DIAG
+  ck[6] = clock64();
+  for (int k = 0; k < 6; k++) diag_add(16 + k, ck[k + 1] - ck[k]);
+#endif
 }
 
 // Status before any record is seen (buffers with no records keep it): flat-packed chunks read
@@ -1730,11 +1740,13 @@ hipError_t launch_unpack_stage(int stage, const UnpackArgs& a, hipStream_t strea
 //  9 entries that differed from the optimistic one  10 optimistic entries walked  11 tiles with a start
 //  12 flat stream: tiles with a raw-head candidate  13 ... whose chain replaced chain 0
 //  14 tiles whose optimistic entry's exit is not their chain-0 exit (no ok bit)
+//  16..21 clock cycles (s_memtime) per phase: staging and message window, chain 0, waiting for
+//  the predecessor's chain-0 exit, the optimistic entry, the look-back, the expansion
 extern "C" int cpk_debug_diag(uint64_t* out, int reset) {
   if (hipDeviceSynchronize() != hipSuccess) return 10;
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(cpk::g_diag), 16 * sizeof(uint64_t)) != hipSuccess) return 10;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(cpk::g_diag), 32 * sizeof(uint64_t)) != hipSuccess) return 10;
   if (reset) {
-    const uint64_t z[16] = {};
+    const uint64_t z[32] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(cpk::g_diag), z, sizeof z) != hipSuccess) return 10;
   }
   return 0;

@@ -20,7 +20,8 @@ from bench import CONFIGS  # noqa: E402
 
 NAMES = ["tiles", "walk0_trips", "walk0_lane_steps", "rewalk_trips", "rewalk_lane_steps",
          "settle_rounds", "enter_calls", "merge_steps", "merge_capped", "entry_mismatch",
-         "opt_walked", "has_start", "f_cand", "f_used", "not_ok"]
+         "opt_walked", "has_start", "f_cand", "f_used", "not_ok", "-",
+         "clk_stage", "clk_chain0", "clk_wait_x0p", "clk_entry", "clk_lookback", "clk_expand"]
 
 L = capnproto_amd.load_library()
 L.cpk_debug_diag.restype = C.c_int
@@ -29,7 +30,7 @@ L.cpk_debug_pdiag.restype = C.c_int
 L.cpk_debug_pdiag.argtypes = [C.c_void_p, C.c_int]
 pbuf = (C.c_uint64 * 4)()
 codec = capnproto_amd.Codec(0)
-buf = (C.c_uint64 * 16)()
+buf = (C.c_uint64 * 32)()
 for name in sys.argv[2:]:
     if name == "split":
         # the bench's stream split: the whole stream decoded as one flat chunk
@@ -45,7 +46,7 @@ for name in sys.argv[2:]:
         assert L.cpk_debug_diag(buf, 1) == 0
         t = max(buf[0], 1)
         print(name, "messages", int(res[4].item()), "tiles", buf[0], " ".join(
-            f"{NAMES[k]}={buf[k] / t:.3f}" for k in range(1, len(NAMES))), flush=True)
+            f"{NAMES[k]}={buf[k] / t:.3f}" for k in range(1, len(NAMES)) if NAMES[k] != "-"), flush=True)
         del words, packed, res
         torch.cuda.empty_cache()
         continue
@@ -72,6 +73,6 @@ for name in sys.argv[2:]:
     ok = torch.equal(back[:total], words[:total])
     t = max(buf[0], 1)
     print(name, "round_trip", ok, "tiles", buf[0], " ".join(
-        f"{NAMES[k]}={buf[k] / t:.3f}" for k in range(1, len(NAMES))), flush=True)
+        f"{NAMES[k]}={buf[k] / t:.3f}" for k in range(1, len(NAMES)) if NAMES[k] != "-"), flush=True)
     del words, packed, back, moff, off
     torch.cuda.empty_cache()
