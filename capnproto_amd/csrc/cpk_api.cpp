@@ -454,6 +454,7 @@ cpk_status ensure_pack_bits(cpk_ctx* ctx, uint64_t N, uint64_t ntiles) {
 struct UnpackScratch {
   uint64_t* desc;
   uint32_t* x0p;
+  uint64_t* desc2;
   size_t zero_bytes;
   uint64_t* tile_first;
   uint64_t* tile_firstpos;
@@ -464,11 +465,12 @@ struct UnpackScratch {
 // Unpack scratch: per message 4 B (header status), per 4 KiB tile 28 B (descriptor, chain-0
 // exit, first message and its start).  The tile descriptors and exits are zeroed (in the header /
 // init launch).
-UnpackScratch carve_unpack(void* base, uint64_t ntiles, uint64_t n) {
+UnpackScratch carve_unpack(void* base, uint64_t ntiles, uint64_t n, bool flat = false) {
   Carve c(base);
   UnpackScratch s;
   s.desc = c.take<uint64_t>(ntiles);
   s.x0p = c.take<uint32_t>(ntiles);
+  s.desc2 = flat ? c.take<uint64_t>(ntiles) : nullptr;
   s.zero_bytes = c.off;
   s.tile_first = c.take<uint64_t>(ntiles);
   s.tile_firstpos = c.take<uint64_t>(ntiles);
@@ -489,10 +491,12 @@ cpk_status unpack_common(cpk_ctx* ctx, uint32_t mode, const uint8_t* d_packed, u
   if (order_streams(ctx, stream) != CPK_OK) return CPK_ERR_HIP;
   const uint64_t B = cpk::kUnpackTileBytes;
   const uint64_t ntiles = (P + B - 1) / B;
-  UnpackScratch probe = carve_unpack(nullptr, ntiles, n);
+  // a flat stream decode (the stream split) carries second-candidate tile descriptors
+  const bool flat = d_rec_pos != nullptr;
+  UnpackScratch probe = carve_unpack(nullptr, ntiles, n, flat);
   cpk_status st = ensure(&ctx->scratch, &ctx->scratch_size, probe.total + 64);
   if (st != CPK_OK) return st;
-  UnpackScratch s = carve_unpack(ctx->scratch, ntiles, n);
+  UnpackScratch s = carve_unpack(ctx->scratch, ntiles, n, flat);
   const uint64_t* word_off = d_word_off_in;
   hipError_t e = hipSuccess;
   cpk::TileFirstJob tf;  // each tile's first message, in the same launch as the headers
@@ -549,6 +553,7 @@ cpk_status unpack_common(cpk_ctx* ctx, uint32_t mode, const uint8_t* d_packed, u
   a.debug_skip = cpk::debug_skip();
   a.hdr_desc = ctx->hdr_desc;
   a.hdr_nblocks = mode == 0 && !fuse ? cpk::header_scan_blocks(n) : 0;
+  a.desc2 = s.desc2;
   a.hdr_fuse = fuse ? 1u : 0u;
   a.hdr_limit = limit;
   a.hdr_word_off = d_word_off_out;

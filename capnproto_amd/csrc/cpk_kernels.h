@@ -116,6 +116,8 @@ struct UnpackArgs {
   uint64_t hdr_nblocks;         // by the tile kernel once the headers are done (0: none)
   // a single-tile message batch of at most kUnpackFuseMsgs messages: the header launch's work
   // (headers, word offsets, statuses) done by the tile kernel itself (0: header launch ran)
+  uint64_t* desc2;              // flat stream decode only (else NULL): per tile, zeroed, its
+                                // exit and words for a second candidate entry (cpk_unpack.hip)
   uint32_t hdr_fuse;
   uint64_t hdr_limit;
   uint64_t* hdr_word_off;

@@ -1079,6 +1079,107 @@ __device__ uint64_t lookback_tiles(const UnpackArgs& a, uint64_t t, uint32_t* xp
   return acc;
 }
 
+// Flat stream decode (the stream split): each tile t also publishes desc2[t], its exit and words
+// for a second candidate entry -- the one the predecessor's AGG exit gives, when that is not the
+// optimistic one (a predecessor without the ok bit: its chain-0 exit, which the optimistic entry
+// came from, is then likely not its true exit, and its AGG exit is, when its own entry was
+// right).  desc2: 0 until published; kD2None: no second candidate; else AGG | ok | exit (as
+// desc) | the candidate entry (bits 21-33) | the tile's words (bits 0-20: at most 4096 records
+// of at most 256 words).
+constexpr uint64_t kD2None = 1;
+constexpr int kD2EntryShift = 21;
+constexpr uint64_t kD2WordsMask = (1ull << kD2EntryShift) - 1;
+
+__device__ __forceinline__ uint64_t wait_nonzero64(const uint64_t* p, uint32_t* err) {
+  uint64_t v = 0;
+  if (lane_id() == 0) {
+    for (uint32_t i = 0; i < kSpinLimit; i++) {
+      v = load_agent(p);
+      if (v) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (!v) raise_error(err, kErrInternal);
+  }
+  return readlane64(v, 0);
+}
+
+// The look-back of a flat stream decode: the nearest INCL within 64 tiles, then tile by tile
+// towards t - 1 the true exit -- each tile's AGG when its true entry is its optimistic one (the
+// predecessor's chain-0 exit), its desc2 when it is the second candidate -- and the words.  A
+// tile matching neither is waited for (its INCL); so is a missing descriptor.
+__device__ uint64_t lookback_flat(const UnpackArgs& a, uint64_t t, uint32_t* xprev) {
+  const int l = lane_id();
+  uint32_t spins = 0;
+  for (;;) {
+    const int64_t u = (int64_t)t - 1 - l;  // lane l: tile u, nearest first
+    // before tile 0: an inclusive zero whose exit enters tile 0 at byte 0
+    const uint64_t dv = u >= 0 ? load_agent(a.desc + u) : (kDescIncl | kOkBit);
+    const uint64_t sb = ballot((dv & kDescFlags) == kDescIncl);
+    const int k = sb ? lowest_bit(sb) : 64;
+    const uint64_t nb = ballot(l < k && (dv & kDescFlags) == 0);
+    const uint64_t* wait_on = nullptr;
+    uint64_t want = 0;  // 0: non-zero; kDescIncl: INCL
+    if (nb) {
+      wait_on = a.desc + (t - 1 - lowest_bit(nb));
+    } else if (k == 64) {
+      wait_on = a.desc + (t - 64);
+      want = kDescIncl;
+    } else {
+      const uint64_t d2 = (u >= 1 && l < k) ? load_agent(a.desc2 + u) : 0;
+      const uint32_t xq = (u >= 1 && l < k) ? (load_agent32(a.x0p + u - 1) & 0x7fffffffu) : 0;
+      const uint64_t dk = readlane64(dv, k);
+      uint32_t X = desc_exit(dk);
+      uint64_t acc = dk & kWordsMask;
+      int stuck = -1;
+      bool need2 = false;
+      for (int j = k - 1; j >= 0; j--) {
+        const uint64_t dj = readlane64(dv, j);
+        const uint32_t E = X >= (uint32_t)kDead ? (uint32_t)kB : X - (uint32_t)kB;
+        const uint32_t xqj = readlane32(xq, j);
+        const uint32_t E1 = xqj >= (uint32_t)kDead ? (uint32_t)kB : xqj - (uint32_t)kB;
+        if (E == E1) {
+          X = desc_exit(dj);
+          acc += dj & kWordsMask;
+          continue;
+        }
+        const uint64_t d2j = readlane64(d2, j);
+        if (d2j == 0) {
+          stuck = j;
+          need2 = true;
+          break;
+        }
+        if (d2j != kD2None && E == (uint32_t)((d2j >> kD2EntryShift) & 0x1fffu)) {
+          X = desc_exit(d2j);
+          acc += d2j & kD2WordsMask;
+          continue;
+        }
+        stuck = j;
+        break;
+      }
+      if (stuck < 0) {
+        *xprev = X;
+        return acc;
+      }
+      wait_on = (need2 ? a.desc2 : a.desc) + (t - 1 - stuck);
+      want = need2 ? 0 : kDescIncl;
+    }
+    if (l == 0) {
+      for (;;) {
+        const uint64_t v = load_agent(wait_on);
+        if (want ? (v & kDescFlags) == want : v != 0) break;
+        if (++spins >= kSpinLimit) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    spins = uniform32(spins);
+    if (spins >= kSpinLimit) {
+      raise_error(a.err, kErrInternal);
+      *xprev = (uint32_t)kB;
+      return 0;
+    }
+  }
+}
+
 // Expansion of a tile's records given its true record-start masks (lane = sub-tile) and excl,
 // the words of the tile's first message before the tile: one lane per record, 64 consecutive
 // records at a time, coalesced stores; zero and raw runs written by the wave.  Records that end
@@ -1631,9 +1732,29 @@ unpack_tiles_kernel(UnpackArgs a) {
       if (l == 0) store_agent(a.desc + t, make_desc(kDescAgg, xE, x0, w));
       CPK_DIAG_ONLY(diag_add(14, xE != x0));
     }
+    if (a.desc2 && !has_start) {
+      // flat stream: the exit and words for the entry the predecessor's AGG exit gives
+      const uint64_t dp = wait_nonzero64(a.desc + t - 1, a.err);
+      const uint32_t E2 = entry_from_exit(desc_exit(dp), fms);
+      uint64_t d2 = kD2None;
+      if (E2 != Eopt && E2 <= (uint32_t)kB) {
+        uint64_t runs2 = runm, tm2;
+        uint32_t xE2 = x0;
+        if (E2 != (uint32_t)q0 && E2 < fms)
+          tm2 = enter_chain(d, aux, st, tm0, (int)E2, (int)fms, x0, &xE2, &runs2);
+        else if (E2 >= fms)
+          tm2 = clip_below(tm0, fms, st.s, &xE2);
+        else
+          tm2 = tm0;
+        const uint64_t w2 = readlane32(wave_incl_sum32(mask_words(d, st.s, tm2, runs2)), 63);
+        d2 = (make_desc(kDescAgg, xE2, x0, 0) & ~kWordsMask) | ((uint64_t)E2 << kD2EntryShift) |
+             (w2 & kD2WordsMask);
+      }
+      if (l == 0) store_agent(a.desc2 + t, d2);
+    }
     uint32_t xprev = xp;
     CPK_DIAG_ONLY(ck[4] = clock64());
-    if (!(a.debug_skip & 8)) excl = lookback_tiles(a, t, &xprev);
+    if (!(a.debug_skip & 8)) excl = a.desc2 ? lookback_flat(a, t, &xprev) : lookback_tiles(a, t, &xprev);
     CPK_DIAG_ONLY(ck[5] = clock64());
     const uint32_t E = entry_from_exit(xprev, fms);
     CPK_DIAG_ONLY(diag_add(9, E != Eopt); diag_add(10, Eopt > 0 && Eopt < fms));
