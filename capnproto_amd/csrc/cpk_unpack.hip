@@ -1556,7 +1556,9 @@ __device__ __forceinline__ void expand_records(const UnpackArgs& a, uint64_t A, 
 #endif
 // PLAIN: the plain-tile expansion is compiled in (launched for batches of large messages only:
 // its code costs the kernel a few percent where few tiles are plain).
-template <bool PLAIN>
+// FLAT: the flat stream decode's second-candidate descriptors and look-back are compiled in (a
+// variant of its own: their registers cost the other variants spills).
+template <bool PLAIN, bool FLAT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CPK_UNPACK_WPE))) void
 unpack_tiles_kernel(UnpackArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds_data[4][kB + kPad];
@@ -1732,7 +1734,7 @@ unpack_tiles_kernel(UnpackArgs a) {
       if (l == 0) store_agent(a.desc + t, make_desc(kDescAgg, xE, x0, w));
       CPK_DIAG_ONLY(diag_add(14, xE != x0));
     }
-    if (a.desc2 && !has_start) {
+    if (FLAT && !has_start) {
       // flat stream: the exit and words for the entry the predecessor's AGG exit gives
       const uint64_t dp = wait_nonzero64(a.desc + t - 1, a.err);
       const uint32_t E2 = entry_from_exit(desc_exit(dp), fms);
@@ -1754,7 +1756,10 @@ unpack_tiles_kernel(UnpackArgs a) {
     }
     uint32_t xprev = xp;
     CPK_DIAG_ONLY(ck[4] = clock64());
-    if (!(a.debug_skip & 8)) excl = a.desc2 ? lookback_flat(a, t, &xprev) : lookback_tiles(a, t, &xprev);
+    if (!(a.debug_skip & 8)) {
+      if constexpr (FLAT) excl = lookback_flat(a, t, &xprev);
+      else excl = lookback_tiles(a, t, &xprev);
+    }
     CPK_DIAG_ONLY(ck[5] = clock64());
     const uint32_t E = entry_from_exit(xprev, fms);
     CPK_DIAG_ONLY(diag_add(9, E != Eopt); diag_add(10, Eopt > 0 && Eopt < fms));
@@ -1841,12 +1846,13 @@ hipError_t launch_unpack_stage(int stage, const UnpackArgs& a, hipStream_t strea
   {
     // plain tiles are most tiles when messages span several tiles
     const bool plain = a.word_off && a.nmsgs && a.nbytes / a.nmsgs >= 4 * (uint64_t)kB;
-    if (plain)
-      hipLaunchKernelGGL(unpack_tiles_kernel<true>, dim3((unsigned)((a.ntiles + 3) / 4)),
-                         dim3(256), 0, stream, a);
+    const dim3 grid((unsigned)((a.ntiles + 3) / 4));
+    if (a.desc2)
+      hipLaunchKernelGGL((unpack_tiles_kernel<true, true>), grid, dim3(256), 0, stream, a);
+    else if (plain)
+      hipLaunchKernelGGL((unpack_tiles_kernel<true, false>), grid, dim3(256), 0, stream, a);
     else
-      hipLaunchKernelGGL(unpack_tiles_kernel<false>, dim3((unsigned)((a.ntiles + 3) / 4)),
-                         dim3(256), 0, stream, a);
+      hipLaunchKernelGGL((unpack_tiles_kernel<false, false>), grid, dim3(256), 0, stream, a);
   }
   (void)stage;
   return hipGetLastError();
