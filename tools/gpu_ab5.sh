@@ -4,6 +4,8 @@ set -o pipefail
 cd ${GRAFT_REPO_ROOT:-$(pwd)}; mkdir -p gpurun_out; PWD_R=$(pwd)
 TAG=${1:-r04f}
 # (variants that are not built are skipped; SPLIT defaults on)
+# (tools/ab_variants.txt, if present, adds variants to VARIANTS)
+[ -f tools/ab_variants.txt ] && VARIANTS="${VARIANTS:-base} $(cat tools/ab_variants.txt)"
 V=""; for v in ${VARIANTS:-base}; do if [ $v = base ] || [ -f capnproto_amd/var_$v.so ]; then V="$V $v"; fi; done
 export VARIANTS="$V"; SPLIT=${SPLIT-1}
 bash tools/gpu_ab3.sh $TAG || exit 1
