@@ -63,7 +63,7 @@ for k in sorted(vals):
         traffic[k] = {"read_bytes": round(rd), "write_bytes": round(wr), "bytes": round(rd + wr),
                       "note": "rocprofv3 FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE, per launch"}
         print(f"   HBM traffic per launch: read {rd / 1e6:.1f} MB  write {wr / 1e6:.1f} MB")
-# the pack "launch" the bench times is tile + scan + place; per-step HBM bytes of every kernel
+# the pack "launch" the bench times is tile + place; per-step HBM bytes of every kernel
 pk = [k for k in ("pack_tile", "pack_place") if k in traffic]
 if pk:
     traffic["pack"] = {f: sum(traffic[k][f] for k in pk) for f in ("read_bytes", "write_bytes",
