@@ -256,7 +256,6 @@ struct PackScratch {
   uint32_t* state;
   uint64_t* bits;
   uint32_t* ticket;
-  uint32_t* tile_ticket;
   uint64_t* desc;
   uint64_t* gword;
   uint64_t* gincl;
@@ -285,7 +284,6 @@ PackScratch carve_pack(void* base, uint64_t N, uint64_t ntiles, bool direct) {
   s.bits = nullptr;
   s.state = c.take<uint32_t>(ntiles);
   s.ticket = c.take<uint32_t>(4);  // (direct kernel: tile tickets; tile kernel: slots taken)
-  s.tile_ticket = c.take<uint32_t>(4);
   s.desc = c.take<uint64_t>(ntiles);  // tile descriptors (direct kernel; tiles resolved in time)
   s.gword = c.take<uint64_t>(direct ? ntiles / 64 + 1 : 0);
   s.gincl = c.take<uint64_t>(direct ? ntiles / 64 + 1 : 0);
@@ -394,7 +392,6 @@ cpk_status pack_common(cpk_ctx* ctx, const uint64_t* d_words, uint64_t N, const 
   a.tpatch = s.tpatch;
   a.err = ctx->err;
   a.ticket = s.ticket;
-  a.tile_ticket = s.tile_ticket;
   a.desc = s.desc;
   a.gword = s.gword;
   a.gincl = s.gincl;

@@ -47,7 +47,6 @@ struct PackTileArgs {
   // both kernels), per 64-tile group (count << 48) + bytes and the groups' inclusive byte prefix
   // (direct kernel)
   uint32_t* ticket;
-  uint32_t* tile_ticket;       // tile kernel built with CPK_PACK_TICKET: tiles taken (zeroed)
   // single-tile batches: the framing launch's work done by the tile kernel itself (frame_mode 1:
   // message batch, frame_off = message word offsets, statuses to frame_status; 2: chunk
   // offsets; 0: framed by the framing launch)

@@ -273,17 +273,6 @@ __device__ unsigned long long g_pdiag[4];
 #define CPK_PDIAG(k, v)
 #endif
 
-#ifndef CPK_PACK_OPP
-#define CPK_PACK_OPP 1  // 0 (with CPK_PACK_SLOTS=0): no look-back in the tile kernel, a slot per tile
-#endif
-#ifndef CPK_PACK_TICKET
-#define CPK_PACK_TICKET 0  // 1: persistent workgroups take tiles by ticket, next tile's loads early
-#endif
-#if CPK_PACK_TICKET
-#define CPK_PACK_TILE_WPE 4  // two tiles' words live per lane
-#else
-#define CPK_PACK_TILE_WPE 7
-#endif
 
 // A tile's global loads (one lane's 8 words, its chunk-start bitmap byte, the word before the
 // wave / after the tile, the next tile's start flag, the lane's first requested position).
@@ -331,7 +320,7 @@ __device__ __forceinline__ void tile_loads(const PackTileArgs& a, uint64_t T, in
   L.p00 = (a.pos ? a.pos : a.words)[a.pos && pi <= a.npos ? pi : 0];
 }
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CPK_PACK_TILE_WPE))) void
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void
 pack_tile_kernel(PackTileArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t stg[kSlotDw];
   __shared__ __attribute__((aligned(16))) uint32_t trash[kWv][kTrashDw];
@@ -349,29 +338,6 @@ pack_tile_kernel(PackTileArgs a) {
   const uint64_t N = a.nwords;
   const uint64_t nbitw = (N + 63) >> 6;
   sel_tab[tid] = make_sel((uint32_t)tid);
-#if CPK_PACK_TICKET
-  // Tiles in ticket order: a tile only waits on tiles whose workgroups took their tickets
-  // earlier and are running (whatever number is resident).  A workgroup issues the next tile's
-  // loads before it works on the current one, so its loads are in flight during the whole tile.
-  __shared__ uint32_t s_tk;
-  if (tid == 0) s_tk = atomicAdd(a.tile_ticket, 1u);
-  lds_barrier();
-  uint64_t T = uniform32(s_tk);
-  if (T >= a.ntiles) return;
-  TileLoads cur;
-  tile_loads(a, T, w, lane_id(), cur);
-  for (;;) {
-  lds_barrier();  // the previous tile is done with the LDS and the ticket
-  if (tid == 0) s_tk = atomicAdd(a.tile_ticket, 1u);
-  for (int i = tid; i < kSlotDw / 4; i += 64 * kWv) ((u32x4*)stg)[i] = (u32x4){0, 0, 0, 0};
-  lds_barrier();
-  const uint64_t Tn = uniform32(s_tk);
-  TileLoads nxt;
-  tile_loads(a, Tn < a.ntiles ? Tn : a.ntiles - 1, w, lane_id(), nxt);
-  // (lane masks recomputed per tile, not held -- and spilled -- across the loop: a spill reload
-  // is a vector memory read, retired in order behind the next tile's loads)
-  const int l = lane_id() + (int)opaque_zero();
-#else
   const uint64_t T = blockIdx.x;
   const int l = lane_id();
   if (a.frame_mode) {
@@ -392,7 +358,6 @@ pack_tile_kernel(PackTileArgs a) {
   TileLoads cur;
   tile_loads(a, T, w, l, cur);
   for (int i = tid; i < kSlotDw / 4; i += 64 * kWv) ((u32x4*)stg)[i] = (u32x4){0, 0, 0, 0};
-#endif
   const uint64_t tbase = T * kTW;
   const uint64_t tend = tbase + kTW < N ? tbase + kTW : N;
   const uint64_t wbase = tbase + (uint64_t)kWW * w;
@@ -700,11 +665,6 @@ pack_tile_kernel(PackTileArgs a) {
         uint64_t ex = 0;
         bool ok = T == 0, wait = windowed;
         uint32_t slot = ~0u;
-#if !CPK_PACK_OPP
-        // (variant: no look-back here -- every tile but oversized ones to its own slot)
-        if (!ok && !wait && T < a.nslots) slot = (uint32_t)T;
-        else
-#endif
         while (!ok) {
           ok = pack_lookback(a.desc, T, &ex, wait, a.err);
           if (ok || wait) break;
@@ -760,12 +720,6 @@ pack_tile_kernel(PackTileArgs a) {
         if (a.pos[i] >= N) a.pos_out[i] = agg;
     if (a.total_out && tid == 0) *a.total_out = agg;
   }
-#if CPK_PACK_TICKET
-  if (Tn >= a.ntiles) break;
-  T = Tn;
-  cur = nxt;
-  }
-#endif
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1476,13 +1430,7 @@ static int cu_count() {
 hipError_t launch_pack_tiles(const PackTileArgs& a, hipStream_t stream) {
   if (a.ntiles == 0) return hipSuccess;
   if (a.ntiles >= (1ull << 31)) return hipErrorInvalidValue;
-#if CPK_PACK_TICKET
-  // persistent workgroups taking tiles by ticket: as many as fit on the device
-  const uint64_t grid = (uint64_t)cu_count() * CPK_PACK_TILE_WPE;
-  pack_tile_kernel<<<(unsigned)(a.ntiles < grid ? a.ntiles : grid), 256, 0, stream>>>(a);
-#else
   pack_tile_kernel<<<(unsigned)a.ntiles, 256, 0, stream>>>(a);
-#endif
   return hipGetLastError();
 }
 

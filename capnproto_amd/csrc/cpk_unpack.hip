@@ -54,16 +54,12 @@ constexpr int kB = (int)kUnpackTileBytes;  // 4096
 constexpr int kPad = 16;
 constexpr int kDead = 1 << 24;  // chain ran into the end of the batch
 
-#ifndef CPK_PLAIN2
-#define CPK_PLAIN2 0  // 1: plain-tile batches of two consecutive records per lane
-#endif
-#ifndef CPK_LIST2
-#define CPK_LIST2 0  // 1: record lists built from both ends of each lane's bits (half the steps)
-#endif
 
 #ifdef CPK_DIAG
+// (every 16th workgroup only: a few global atomics per tile from every tile contend enough to
+// distort the timings they measure)
 __device__ __forceinline__ void diag_add(int k, uint64_t v) {
-  if (lane_id() == 0) atomicAdd(&g_diag[k], (unsigned long long)v);
+  if (lane_id() == 0 && (blockIdx.x & 15) == 0) atomicAdd(&g_diag[k], (unsigned long long)v);
 }
 // wave-level trip count (max over lanes) and lane-step total of a per-lane count n
 __device__ __forceinline__ void diag_trips(int k, int n) {
@@ -1342,79 +1338,12 @@ __device__ __forceinline__ void expand_records(const UnpackArgs& a, uint64_t A, 
       const uint32_t nh = readlane32(Rin, 63);
       uint32_t r = Rin - c;
       const uint32_t pbase = 64u * (uint32_t)src + sh;
-#if CPK_LIST2
-      // from both ends, the lowest and the highest start per step (an odd last step writes its
-      // one start twice, to the same entry)
-      uint32_t rh = Rin - 1;
-      while (bits) {
-        const uint32_t b = (uint32_t)__builtin_ctz(bits);
-        bits &= bits - 1;
-        const uint32_t bh = bits ? 31u - (uint32_t)__builtin_clz(bits) : b;
-        bits &= ~(1u << bh);
-        list[r++] = (uint16_t)(pbase + b);
-        list[rh--] = (uint16_t)(pbase + bh);
-      }
-#else
       while (bits) {
         const uint32_t b = (uint32_t)__builtin_ctz(bits);
         bits &= bits - 1;
         list[r++] = (uint16_t)(pbase + b);
       }
-#endif
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#if CPK_PLAIN2
-      // two consecutive records per lane, 128 per batch: one word-offset scan, one list read
-      // and one loop step for both
-      auto rec = [&](int p, uint32_t& cnt, bool& f, uint64_t& word) {
-        const uint32_t* dw = (const uint32_t*)(d + (p & ~3));
-        const uint32_t sh2 = (uint32_t)p & 3;
-        const uint32_t q0 = dw[0], q1 = dw[1], q2 = dw[2], q3 = dw[3];
-        const uint32_t b0w = __builtin_amdgcn_alignbyte(q1, q0, sh2);
-        const uint32_t b1w = __builtin_amdgcn_alignbyte(q2, q1, sh2);
-        const uint32_t b2w = __builtin_amdgcn_alignbyte(q3, q2, sh2);
-        const uint32_t tag = b0w & 0xff;
-        const uint32_t dlo = __builtin_amdgcn_alignbyte(b1w, b0w, 1);
-        const uint32_t dhi = __builtin_amdgcn_alignbyte(b2w, b1w, 1);
-        const bool z = tag == 0;
-        f = tag == 0xff;
-        cnt = z ? (b0w >> 8) & 0xff : 0u;
-        cnt = f ? (b2w >> 8) & 0xff : cnt;
-        const uint64_t sel = dep_tab[tag];
-        word = ((uint64_t)__builtin_amdgcn_perm(dhi, dlo, (uint32_t)(sel >> 32)) << 32) |
-               __builtin_amdgcn_perm(dhi, dlo, (uint32_t)sel);
-      };
-      for (uint32_t b0 = 0; b0 < ((a.debug_skip & 16) ? 0u : nh); b0 += 128) {
-        const uint32_t r0 = b0 + 2u * (uint32_t)l;
-        const bool a0 = r0 < nh, a1 = r0 + 1 < nh;
-        // (inactive lanes read real entries: the LDS reads stay in bounds)
-        const uint32_t rc = a0 ? r0 : ((nh - 1) & ~1u);
-        const uint32_t e01 = *(const uint32_t*)(list + rc);
-        const int p0 = (int)(e01 & 0xffffu);
-        const int p1 = rc + 1 < nh ? (int)(e01 >> 16) : p0;
-        uint32_t c0, c1;
-        bool f0, f1;
-        uint64_t x0w, x1w;
-        rec(p0, c0, f0, x0w);
-        rec(p1, c1, f1, x1w);
-        const uint32_t w0 = a0 ? 1 + c0 : 0, w1 = a1 ? 1 + c1 : 0;
-        const uint32_t inc = wave_incl_sum32(w0 + w1);
-        const uint32_t o0 = sum + inc - (w0 + w1), o1 = o0 + w0;
-        if (a0) wp0[o0] = x0w;
-        if (a1) wp0[o1] = x1w;
-        RunJob job;
-        job.n = a0 ? c0 : 0u;
-        job.dst = cbase0 + excl + o0 + 1;
-        job.raw = f0;
-        job.src = A + (uint32_t)p0 + 10;
-        run_jobs_batch(a, job, d, A, (uint32_t)(kB + kPad));
-        job.n = a1 ? c1 : 0u;
-        job.dst = cbase0 + excl + o1 + 1;
-        job.raw = f1;
-        job.src = A + (uint32_t)p1 + 10;
-        run_jobs_batch(a, job, d, A, (uint32_t)(kB + kPad));
-        sum += readlane32(inc, 63);
-      }
-#else
       for (uint32_t b0 = 0; b0 < ((a.debug_skip & 16) ? 0u : nh); b0 += 64) {
         const uint32_t rr = b0 + l;
         const bool act = rr < nh;
@@ -1446,7 +1375,6 @@ __device__ __forceinline__ void expand_records(const UnpackArgs& a, uint64_t A, 
         run_jobs_batch(a, job, d, A, (uint32_t)(kB + kPad));
         sum += readlane32(inc, 63);
       }
-#endif
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
     return;
@@ -1471,23 +1399,11 @@ __device__ __forceinline__ void expand_records(const UnpackArgs& a, uint64_t A, 
     const uint32_t nh = readlane32(Rin, 63);
     uint32_t r = Rin - c;
     const uint32_t pbase = 64u * (uint32_t)src + sh;
-#if CPK_LIST2
-    uint32_t rh = Rin - 1;
-    while (bits) {  // (from both ends, as above)
-      const uint32_t b = (uint32_t)__builtin_ctz(bits);
-      bits &= bits - 1;
-      const uint32_t bh = bits ? 31u - (uint32_t)__builtin_clz(bits) : b;
-      bits &= ~(1u << bh);
-      list[r++] = (uint16_t)((pbase + b) | (((msp >> b) & 1u) << 12));
-      list[rh--] = (uint16_t)((pbase + bh) | (((msp >> bh) & 1u) << 12));
-    }
-#else
     while (bits) {
       const uint32_t b = (uint32_t)__builtin_ctz(bits);
       bits &= bits - 1;
       list[r++] = (uint16_t)((pbase + b) | (((msp >> b) & 1u) << 12));
     }
-#endif
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     for (uint32_t b0 = 0; b0 < ((a.debug_skip & 16) ? 0u : nh); b0 += 64) {
       const uint32_t rr = b0 + l;
