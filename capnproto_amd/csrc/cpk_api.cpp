@@ -19,6 +19,9 @@ struct cpk_ctx {
   void* scratch = nullptr;       // device scratch (descriptors, bitmaps, tile tables)
   size_t scratch_size = 0;
   uint32_t* err = nullptr;       // device error word (first batch-level error)
+  // (host entry points, small batches) where a single-launch kernel copies the error word at its
+  // end -- a pinned host word, device view -- so that no download is needed; else NULL
+  uint32_t* err_host = nullptr;
   // device staging: [0..2] the *_host entry points, [3] cpk_pack_segments (segment list, flat
   // message, chunk offsets), [4] cpk_split_packed_stream (call state, record-head map)
   void* stage[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -129,6 +132,7 @@ struct HostIo {
   uint8_t* hres;  // pinned results
   uint32_t* derr;
   const uint32_t* herr;
+  uint32_t* dherr;  // device view of herr (small batches), else NULL
   bool upload;
 };
 
@@ -152,6 +156,14 @@ cpk_status host_io(cpk_ctx* ctx, size_t in_bytes, size_t out_bytes, HostIo* io) 
   io->dres = db + 16;
   io->herr = (const uint32_t*)(hb + in_bytes);
   io->hres = hb + in_bytes + 16;
+  io->dherr = nullptr;
+  if (!io->upload) {
+    // small batches: the kernels also write their results straight to the pinned buffer, and a
+    // single-launch kernel its error word (nothing to download then)
+    if (hipHostGetDevicePointer((void**)&io->dres, io->hres, 0) != hipSuccess ||
+        hipHostGetDevicePointer((void**)&io->dherr, (void*)io->herr, 0) != hipSuccess)
+      return CPK_ERR_HIP;
+  }
   return CPK_OK;
 }
 
@@ -164,15 +176,26 @@ cpk_status host_io_run(cpk_ctx* ctx, const HostIo& io, size_t in_bytes, size_t o
   *downloaded = false;
   if (io.upload && hipMemcpyAsync(io.din, io.hin, in_bytes, hipMemcpyHostToDevice, s) != hipSuccess)
     return CPK_ERR_HIP;
+  constexpr uint32_t kUnset = 0xffffffffu;  // (no cpk_status)
+  if (io.dherr) *(volatile uint32_t*)io.herr = kUnset;
   uint32_t* const saved = ctx->err;
   ctx->err = io.derr;
+  ctx->err_host = io.dherr;
   cpk_status st = fn(s);
   ctx->err = saved;
+  ctx->err_host = nullptr;
   if (st != CPK_OK) return st;
-  if (hipMemcpyAsync((void*)io.herr, io.derr, 16 + out_bytes, hipMemcpyDeviceToHost, s) !=
-          hipSuccess ||
-      hipStreamSynchronize(s) != hipSuccess)
+  if (io.dherr) {
+    // results are in place; the error word too when one launch did the call
+    if (hipStreamSynchronize(s) != hipSuccess) return CPK_ERR_HIP;
+    if (*(volatile const uint32_t*)io.herr == kUnset &&
+        hipMemcpy((void*)io.herr, io.derr, 4, hipMemcpyDeviceToHost) != hipSuccess)
+      return CPK_ERR_HIP;
+  } else if (hipMemcpyAsync((void*)io.herr, io.derr, 16 + out_bytes, hipMemcpyDeviceToHost, s) !=
+                 hipSuccess ||
+             hipStreamSynchronize(s) != hipSuccess) {
     return CPK_ERR_HIP;
+  }
   *downloaded = true;
   if (*io.herr) {
     st = (cpk_status)*io.herr;
@@ -395,6 +418,7 @@ cpk_status pack_common(cpk_ctx* ctx, const uint64_t* d_words, uint64_t N, const 
   a.desc = s.desc;
   a.gword = s.gword;
   a.gincl = s.gincl;
+  a.err_host = single ? ctx->err_host : nullptr;
   a.frame_mode = single ? (messages ? 1u : 2u) : 0u;
   a.frame_off = d_off;
   a.frame_n = n;
@@ -552,6 +576,7 @@ cpk_status unpack_common(cpk_ctx* ctx, uint32_t mode, const uint8_t* d_packed, u
   a.hdr_nblocks = mode == 0 && !fuse ? cpk::header_scan_blocks(n) : 0;
   a.desc2 = s.desc2;
   a.hdr_fuse = fuse ? 1u : 0u;
+  a.err_host = fuse ? ctx->err_host : nullptr;
   a.hdr_limit = limit;
   a.hdr_word_off = d_word_off_out;
   a.hdr_status_out = s.hdr_status;

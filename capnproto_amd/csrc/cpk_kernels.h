@@ -51,6 +51,7 @@ struct PackTileArgs {
   // message batch, frame_off = message word offsets, statuses to frame_status; 2: chunk
   // offsets; 0: framed by the framing launch)
   uint32_t frame_mode;
+  uint32_t* err_host;          // single-tile batch: where to copy the error word at the end (or NULL)
   const uint64_t* frame_off;
   uint64_t frame_n;
   int32_t* frame_status;
@@ -118,6 +119,7 @@ struct UnpackArgs {
   uint64_t* desc2;              // flat stream decode only (else NULL): per tile, zeroed, its
                                 // exit and words for a second candidate entry (cpk_unpack.hip)
   uint32_t hdr_fuse;
+  uint32_t* err_host;           // fused batch: where to copy the error word at the end (or NULL)
   uint64_t hdr_limit;
   uint64_t* hdr_word_off;
   int32_t* hdr_status_out;

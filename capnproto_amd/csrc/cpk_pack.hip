@@ -719,6 +719,9 @@ pack_tile_kernel(PackTileArgs a) {
       for (uint64_t i = tid; i <= a.npos; i += 64 * kWv)
         if (a.pos[i] >= N) a.pos_out[i] = agg;
     if (a.total_out && tid == 0) *a.total_out = agg;
+    // the call's error word for the host (this launch is the whole call; tid 0 raised the only
+    // error a single tile can)
+    if (a.err_host && tid == 0) *a.err_host = load_agent32(a.err);
   }
 }
 

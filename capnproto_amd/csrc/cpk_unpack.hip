@@ -1764,6 +1764,8 @@ unpack_tiles_kernel(UnpackArgs a) {
   if (a.debug_skip & 256) return;  // diagnostic: + the entry and the look-back
   expand_records<PLAIN>(a, A, d, aux, dep_tab, deposit_sel((uint32_t)l & 15), tm, excl, win, mfirst,
                  mlast, msw, w_tile);
+  // a fused single-tile batch: this wave is the whole call -- its error word for the host
+  if (a.err_host && l == 0) *a.err_host = load_agent32(a.err);
 #ifdef CPK_DIAG
   ck[6] = clock64();
   for (int k = 0; k < 6; k++) diag_add(16 + k, ck[k + 1] - ck[k]);
