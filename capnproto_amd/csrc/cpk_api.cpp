@@ -289,6 +289,7 @@ struct PackScratch {
   uint32_t* thole;
   uint32_t* tpatch;
   uint8_t* scr;
+  uint8_t* scr_small;
   uint32_t* tslot;
   uint32_t nslots;
   size_t total;
@@ -315,6 +316,7 @@ PackScratch carve_pack(void* base, uint64_t N, uint64_t ntiles, bool direct) {
     s.tile_first = c.take<uint64_t>(ntiles);
     s.tile_bytes = s.tile_off = nullptr;
     s.thole = s.tpatch = s.tslot = nullptr;
+    s.scr_small = nullptr;
     s.nslots = 0;
     s.scr = nullptr;
     s.total = c.off;
@@ -326,6 +328,7 @@ PackScratch carve_pack(void* base, uint64_t N, uint64_t ntiles, bool direct) {
   s.thole = c.take<uint32_t>(ntiles);
   s.tpatch = c.take<uint32_t>(ntiles);
   s.tslot = c.take<uint32_t>(ntiles);
+  s.scr_small = c.take<uint8_t>(ntiles * cpk::kSmallSlot + 16);
   s.nslots = (uint32_t)(cpk::kPackSlots == 0 || ntiles < cpk::kPackSlots ? ntiles : cpk::kPackSlots);
   s.scr = c.take<uint8_t>(s.nslots * cpk::kPackScratchBytes + 16);
   s.total = c.off;
@@ -409,6 +412,7 @@ cpk_status pack_common(cpk_ctx* ctx, const uint64_t* d_words, uint64_t N, const 
   a.tile_off = s.tile_off;
   a.scr = s.scr;
   a.tslot = s.tslot;
+  a.scr_small = s.scr_small;
   a.slot_next = s.ticket;
   a.nslots = s.nslots;
   a.thole = s.thole;

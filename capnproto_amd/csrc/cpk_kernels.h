@@ -13,6 +13,11 @@ constexpr uint64_t kPackScratchBytes = 10 * kPackTileWords;  // a tile's packed 
 #define CPK_PACK_SLOTS 2048  // slot pool: a tile finding none waits for its offset (0: one per tile)
 #endif
 constexpr uint64_t kPackSlots = CPK_PACK_SLOTS;
+#ifndef CPK_PACK_SMALL
+#define CPK_PACK_SMALL 0  // bytes (a multiple of 16): a tile packing to at most this many goes
+#endif                    // through its own small slot (CPK_PACK_SMALL / 16 KiB of the batch)
+constexpr uint32_t kSmallSlot = CPK_PACK_SMALL;
+constexpr uint32_t kSmallTag = 0xfffffffeu;
 constexpr uint64_t kUnpackTileBytes = 4096;     // packed bytes per unpack tile (>= 2050)
 
 struct PackTileArgs {
@@ -37,7 +42,9 @@ struct PackTileArgs {
   uint64_t* tile_off;          // (unused: offsets come from the descriptors' look-back)
   uint8_t* scr;                // slot pool (nslots * kPackScratchBytes + 16) for the tiles whose
                                // offset is not known in time
-  uint32_t* tslot;             // per tile: its slot (written only by tiles that take one)
+  uint32_t* tslot;             // per tile: its slot (written only by tiles that take one;
+                               // kSmallTag: its own small slot in scr_small)
+  uint8_t* scr_small;          // per tile a kSmallSlot-byte slot for tiles of at most that many bytes
   uint32_t* slot_next;         // slots taken so far (zeroed)
   uint32_t nslots;
   uint32_t* thole;             // byte of a tile's provisional count (~0: none)

@@ -654,6 +654,28 @@ pack_tile_kernel(PackTileArgs a) {
       __builtin_amdgcn_sched_barrier(0);
     }
     lds_barrier();  // ---- C: staged ------------------------------------------------------
+    // A tile of few bytes (sparse words) goes to its own small slot at once -- copying it twice
+    // costs less than a workgroup stalled on a round trip -- while wave 0 publishes its
+    // inclusive prefix when the predecessors have theirs (so the placement launch finds one near).
+    const bool small = kSmallSlot && T != 0 && !windowed && agg <= kSmallSlot;
+    if (small) {
+      if (w == 0) {
+        uint64_t ex = 0;
+        if (pack_lookback(a.desc, T, &ex, false, a.err) && l == 0)
+          store_agent(a.desc + T, kDescIncl | (ex + agg));
+        if (l == 0) {
+          a.tslot[T] = kSmallTag;
+          CPK_PDIAG(0, 1);
+          CPK_PDIAG(2, 1);
+        }
+      }
+      u32x4* const dst = (u32x4*)(a.scr_small + T * kSmallSlot);
+      const uint32_t n16 = (agg + 15u) >> 4;
+      for (uint32_t i = tid + opaque_zero(); i < n16; i += 64 * kWv)
+        dst[i] = ((const u32x4*)stg)[1 + i];
+      s_dst = ~0ull;  // (read by the single-tile ending only, never for such a tile)
+      break;
+    }
     if (win == 0) {
       // The tile's offset, if the tiles before it have all published their byte counts by now
       // (no waiting): then its bytes go straight to the output and the placement launch skips
@@ -681,7 +703,7 @@ pack_tile_kernel(PackTileArgs a) {
         ok = ok && ex + agg <= a.out_capacity;  // (too small an output: placement raises it)
         if (l == 0) {
           if (ok && T != 0) store_agent(a.desc + T, kDescIncl | (ex + agg));
-          if (slot != ~0u) a.tslot[T] = slot;
+          a.tslot[T] = slot;  // (~0: written straight out, or not at all)
           s_dst = ok ? ex : ~0ull;
           s_slot = slot;
         }
@@ -1348,11 +1370,12 @@ __global__ __launch_bounds__(256) void pack_place_kernel(PackTileArgs a) {
     if (l == 0) store_agent(a.desc + T, kDescIncl | (off + n));
   }
   const uint64_t total = off + n;  // (the batch total on the last tile)
-  // (a tile whose offset was known in time wrote its bytes itself: INCL descriptor; the others
-  // are in their slots)
+  // (a tile whose offset was known in time wrote its bytes itself: INCL descriptor, no slot; the
+  // others are in their slots)
+  const uint32_t slot = a.tslot[T];
   if (off + n > a.out_capacity) {
     if (l == 0) raise_error(a.err, kErrCapacity);
-  } else if (!incl && n) {
+  } else if ((!incl || slot == kSmallTag) && n) {
     // the previous tile's count byte that this tile finishes (the previous tile may have left it
     // out, having written its bytes itself)
     if (T > 0 && l == 0) {
@@ -1362,7 +1385,8 @@ __global__ __launch_bounds__(256) void pack_place_kernel(PackTileArgs a) {
     // count byte patched by the next tile (position, value) -- wave-uniform
     const uint32_t hole = T + 1 < a.ntiles ? a.thole[T] : 0xffffffffu;
     const uint32_t pv = hole != 0xffffffffu ? a.tpatch[T + 1] : 0u;
-    const uint8_t* const src = a.scr + a.tslot[T] * (uint64_t)kScr;
+    const uint8_t* const src = slot == kSmallTag ? a.scr_small + T * kSmallSlot
+                                                 : a.scr + slot * (uint64_t)kScr;
     uint8_t* const o0 = a.out + off;
     const uint64_t A0 = (uint64_t)(uintptr_t)o0;
     const uint64_t A1 = A0 + n;
