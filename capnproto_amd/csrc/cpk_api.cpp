@@ -53,6 +53,7 @@ struct cpk_ctx {
   // and one device buffer, so a call is one upload, the kernels, one download of every result
   // and one synchronisation (per-call latency of small messages)
   void* hio = nullptr;
+  uint8_t* hio_dev = nullptr;  // its device view
   size_t hio_size = 0;
   void* dio = nullptr;
   size_t dio_size = 0;
@@ -138,8 +139,13 @@ struct HostIo {
 
 cpk_status host_io(cpk_ctx* ctx, size_t in_bytes, size_t out_bytes, HostIo* io) {
   cpk_status st;
+  void* const hbefore = ctx->hio;
   if ((st = ensure_pinned(&ctx->hio, &ctx->hio_size, in_bytes + 16 + out_bytes)) != CPK_OK)
     return st;
+  // (the device view of the pinned buffer, looked up once per allocation)
+  if ((ctx->hio != hbefore || !ctx->hio_dev) &&
+      hipHostGetDevicePointer((void**)&ctx->hio_dev, ctx->hio, 0) != hipSuccess)
+    return CPK_ERR_HIP;
   void* const before = ctx->dio;
   if ((st = ensure(&ctx->dio, &ctx->dio_size, 16 + out_bytes + in_bytes)) != CPK_OK) return st;
   if (ctx->dio != before && (hipMemset(ctx->dio, 0, 16) != hipSuccess ||
@@ -149,9 +155,7 @@ cpk_status host_io(cpk_ctx* ctx, size_t in_bytes, size_t out_bytes, HostIo* io) 
   uint8_t* const db = (uint8_t*)ctx->dio;
   io->hin = hb;
   io->upload = in_bytes > zero_copy_max();
-  io->din = db + 16 + out_bytes;
-  if (!io->upload && hipHostGetDevicePointer((void**)&io->din, hb, 0) != hipSuccess)
-    return CPK_ERR_HIP;
+  io->din = io->upload ? db + 16 + out_bytes : ctx->hio_dev;
   io->derr = (uint32_t*)db;
   io->dres = db + 16;
   io->herr = (const uint32_t*)(hb + in_bytes);
@@ -160,9 +164,8 @@ cpk_status host_io(cpk_ctx* ctx, size_t in_bytes, size_t out_bytes, HostIo* io) 
   if (!io->upload) {
     // small batches: the kernels also write their results straight to the pinned buffer, and a
     // single-launch kernel its error word (nothing to download then)
-    if (hipHostGetDevicePointer((void**)&io->dres, io->hres, 0) != hipSuccess ||
-        hipHostGetDevicePointer((void**)&io->dherr, (void*)io->herr, 0) != hipSuccess)
-      return CPK_ERR_HIP;
+    io->dres = ctx->hio_dev + in_bytes + 16;
+    io->dherr = (uint32_t*)(ctx->hio_dev + in_bytes);
   }
   return CPK_OK;
 }
