@@ -54,6 +54,10 @@ constexpr int kB = (int)kUnpackTileBytes;  // 4096
 constexpr int kPad = 16;
 constexpr int kDead = 1 << 24;  // chain ran into the end of the batch
 
+#ifndef CPK_PIPE
+#define CPK_PIPE 0  // 1: plain-tile batches read the next batch's record bytes ahead
+#endif
+
 
 #ifdef CPK_DIAG
 // (every 16th workgroup only: a few global atomics per tile from every tile contend enough to
@@ -1344,6 +1348,35 @@ __device__ __forceinline__ void expand_records(const UnpackArgs& a, uint64_t A, 
         list[r++] = (uint16_t)(pbase + b);
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#if CPK_PIPE
+      // the next batch's record bytes are read while this batch computes (two dependent LDS
+      // round trips per batch off the critical path)
+      const uint32_t nhe = (a.debug_skip & 16) ? 0u : nh;
+      int pn = nhe ? (int)list[(uint32_t)l < nh ? (uint32_t)l : nh - 1] : 0;
+      uint32_t n0 = 0, n1 = 0, n2 = 0, n3 = 0;
+      if (nhe) {
+        const uint32_t* dwn = (const uint32_t*)(d + (pn & ~3));
+        n0 = dwn[0];
+        n1 = dwn[1];
+        n2 = dwn[2];
+        n3 = dwn[3];
+      }
+      for (uint32_t b0 = 0; b0 < nhe; b0 += 64) {
+        const uint32_t rr = b0 + l;
+        const bool act = rr < nh;
+        const int p = pn;
+        const uint32_t sh2 = (uint32_t)p & 3;
+        const uint32_t q0 = n0, q1 = n1, q2 = n2, q3 = n3;
+        if (b0 + 64 < nh) {
+          const uint32_t rn = b0 + 64 + l;
+          pn = (int)list[rn < nh ? rn : nh - 1];
+          const uint32_t* dwn = (const uint32_t*)(d + (pn & ~3));
+          n0 = dwn[0];
+          n1 = dwn[1];
+          n2 = dwn[2];
+          n3 = dwn[3];
+        }
+#else
       for (uint32_t b0 = 0; b0 < ((a.debug_skip & 16) ? 0u : nh); b0 += 64) {
         const uint32_t rr = b0 + l;
         const bool act = rr < nh;
@@ -1351,6 +1384,7 @@ __device__ __forceinline__ void expand_records(const UnpackArgs& a, uint64_t A, 
         const uint32_t* dw = (const uint32_t*)(d + (p & ~3));
         const uint32_t sh2 = (uint32_t)p & 3;
         const uint32_t q0 = dw[0], q1 = dw[1], q2 = dw[2], q3 = dw[3];
+#endif
         const uint32_t b0w = __builtin_amdgcn_alignbyte(q1, q0, sh2);  // bytes p .. p+3
         const uint32_t b1w = __builtin_amdgcn_alignbyte(q2, q1, sh2);  // p+4 .. p+7
         const uint32_t b2w = __builtin_amdgcn_alignbyte(q3, q2, sh2);  // p+8 .. p+11
