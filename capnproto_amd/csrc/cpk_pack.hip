@@ -177,16 +177,17 @@ __device__ __forceinline__ uint32_t sum_exit(uint32_t s) { return (s >> 16) & 0x
 // Look-back for tile t (one wave): the exclusive byte prefix from the descriptors of its
 // predecessors -- a first window of 16 (one 128-byte line: these agent-scope reads go past the L2,
 // and the nearest inclusive prefix is usually a few tiles back), then 64 per round trip.
-// wait == false: one round trip over 64 predecessors; gives up (false) when one before the
-// nearest inclusive prefix has not published its byte count yet, or none of them has one.
+// wait == false: gives up (false) when one before the nearest inclusive prefix has not
+// published its byte count yet, or after 272 predecessors (one round trip instead: C3 pack_tile
+// 2.18 -> 3.05 ms, fewer tiles resolve in time and more wait).
 __device__ __forceinline__ bool pack_lookback(const uint64_t* desc, uint64_t t, uint64_t* out,
                                               bool wait, uint32_t* err) {
   const int l = lane_id() + (int)opaque_zero();  // (addresses not hoisted out of the caller's loop)
   uint64_t excl = 0;
   int64_t j = (int64_t)t - 1;
   uint32_t spins = 0;
-  int width = wait ? 16 : 64;  // (not waiting: one round trip, 64 predecessors, then give up)
-  for (;;) {
+  int width = 16;
+  for (int round = 0;;) {
     const int64_t idx = j - l;
     const bool in = l < width;
     const uint64_t d = !in ? 0ull : (idx >= 0 ? load_agent(desc + idx) : kDescIncl);
@@ -209,9 +210,9 @@ __device__ __forceinline__ bool pack_lookback(const uint64_t* desc, uint64_t t, 
       *out = excl;
       return true;
     }
-    if (!wait) return false;
     j -= width;
     width = 64;
+    if (!wait && ++round == 5) return false;
   }
 }
 
