@@ -6,7 +6,11 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <immintrin.h>
+
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <new>
 #include <utility>
 #include <vector>
@@ -22,6 +26,7 @@ struct cpk_ctx {
   // (host entry points, small batches) where a single-launch kernel copies the error word at its
   // end -- a pinned host word, device view -- so that no download is needed; else NULL
   uint32_t* err_host = nullptr;
+  bool fused_last = false;  // the last call was one launch that copied its error word there
   // device staging: [0..2] the *_host entry points, [3] cpk_pack_segments (segment list, flat
   // message, chunk offsets), [4] cpk_split_packed_stream (call state, record-head map)
   void* stage[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -184,16 +189,36 @@ cpk_status host_io_run(cpk_ctx* ctx, const HostIo& io, size_t in_bytes, size_t o
   uint32_t* const saved = ctx->err;
   ctx->err = io.derr;
   ctx->err_host = io.dherr;
+  ctx->fused_last = false;
   cpk_status st = fn(s);
   ctx->err = saved;
   ctx->err_host = nullptr;
   if (st != CPK_OK) return st;
   if (io.dherr) {
-    // results are in place; the error word too when one launch did the call
-    if (hipStreamSynchronize(s) != hipSuccess) return CPK_ERR_HIP;
-    if (*(volatile const uint32_t*)io.herr == kUnset &&
-        hipMemcpy((void*)io.herr, io.derr, 4, hipMemcpyDeviceToHost) != hipSuccess)
-      return CPK_ERR_HIP;
+    // results are in place; the error word too when one launch did the call, written last (after
+    // a system-scope release): spinning on it returns as soon as the kernel is done, a stream
+    // synchronisation only some microseconds later
+    bool seen = false;
+    if (ctx->fused_last) {
+      const auto t0 = std::chrono::steady_clock::now();
+      for (uint32_t i = 0;; i++) {
+        if (*(volatile const uint32_t*)io.herr != kUnset) {
+          seen = true;
+          break;
+        }
+        if ((i & 1023) == 1023 &&
+            std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2))
+          break;  // (long call or a fault: the runtime's synchronisation tells)
+        _mm_pause();
+      }
+      std::atomic_thread_fence(std::memory_order_acquire);
+    }
+    if (!seen) {
+      if (hipStreamSynchronize(s) != hipSuccess) return CPK_ERR_HIP;
+      if (*(volatile const uint32_t*)io.herr == kUnset &&
+          hipMemcpy((void*)io.herr, io.derr, 4, hipMemcpyDeviceToHost) != hipSuccess)
+        return CPK_ERR_HIP;
+    }
   } else if (hipMemcpyAsync((void*)io.herr, io.derr, 16 + out_bytes, hipMemcpyDeviceToHost, s) !=
                  hipSuccess ||
              hipStreamSynchronize(s) != hipSuccess) {
@@ -426,6 +451,7 @@ cpk_status pack_common(cpk_ctx* ctx, const uint64_t* d_words, uint64_t N, const 
   a.gword = s.gword;
   a.gincl = s.gincl;
   a.err_host = single ? ctx->err_host : nullptr;
+  ctx->fused_last = a.err_host != nullptr;
   a.frame_mode = single ? (messages ? 1u : 2u) : 0u;
   a.frame_off = d_off;
   a.frame_n = n;
@@ -584,6 +610,7 @@ cpk_status unpack_common(cpk_ctx* ctx, uint32_t mode, const uint8_t* d_packed, u
   a.desc2 = s.desc2;
   a.hdr_fuse = fuse ? 1u : 0u;
   a.err_host = fuse ? ctx->err_host : nullptr;
+  ctx->fused_last = a.err_host != nullptr;
   a.hdr_limit = limit;
   a.hdr_word_off = d_word_off_out;
   a.hdr_status_out = s.hdr_status;

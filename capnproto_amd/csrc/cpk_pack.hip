@@ -742,9 +742,17 @@ pack_tile_kernel(PackTileArgs a) {
       for (uint64_t i = tid; i <= a.npos; i += 64 * kWv)
         if (a.pos[i] >= N) a.pos_out[i] = agg;
     if (a.total_out && tid == 0) *a.total_out = agg;
-    // the call's error word for the host (this launch is the whole call; tid 0 raised the only
-    // error a single tile can)
-    if (a.err_host && tid == 0) *a.err_host = load_agent32(a.err);
+    // the call's error word for the host, last (this launch is the whole call; tid 0 raised the
+    // only error a single tile can): every wave's stores done, then a system-scope release
+    if (a.err_host) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        __threadfence_system();
+        __hip_atomic_store(a.err_host, load_agent32(a.err), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
   }
 }
 

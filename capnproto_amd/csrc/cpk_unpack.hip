@@ -1798,8 +1798,16 @@ unpack_tiles_kernel(UnpackArgs a) {
   if (a.debug_skip & 256) return;  // diagnostic: + the entry and the look-back
   expand_records<PLAIN>(a, A, d, aux, dep_tab, deposit_sel((uint32_t)l & 15), tm, excl, win, mfirst,
                  mlast, msw, w_tile);
-  // a fused single-tile batch: this wave is the whole call -- its error word for the host
-  if (a.err_host && l == 0) *a.err_host = load_agent32(a.err);
+  // a fused single-tile batch: this wave is the whole call -- its error word for the host, last:
+  // its stores done, then a system-scope release
+  if (a.err_host) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (l == 0) {
+      __threadfence_system();
+      __hip_atomic_store(a.err_host, load_agent32(a.err), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
 #ifdef CPK_DIAG
   ck[6] = clock64();
   for (int k = 0; k < 6; k++) diag_add(16 + k, ck[k + 1] - ck[k]);
