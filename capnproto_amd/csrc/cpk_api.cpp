@@ -517,8 +517,8 @@ struct UnpackScratch {
 };
 
 // Unpack scratch: per message 4 B (header status), per 4 KiB tile 28 B (descriptor, chain-0
-// exit, first message and its start).  The tile descriptors and exits are zeroed (in the header /
-// init launch).
+// exit, first message and its start), and for a flat stream decode 8 B more (second-candidate
+// descriptor).  The tile descriptors and exits are zeroed (in the header / init launch).
 UnpackScratch carve_unpack(void* base, uint64_t ntiles, uint64_t n, bool flat = false) {
   Carve c(base);
   UnpackScratch s;

@@ -270,7 +270,13 @@ __device__ __forceinline__ void copy_out_final(const uint32_t* stg, uint32_t n, 
 // diagnostic build only: 0 tiles, 1 offset known in time, 2 slot taken, 3 waited for the offset
 __device__ unsigned long long g_pdiag[4];
 #define CPK_PDIAG(k, v) atomicAdd(&g_pdiag[k], (unsigned long long)(v))
+// per-tile timeline of the first kPTimeline tiles (wall clock, 100 MHz): start, byte count
+// published, staged, offset or slot known, end; then the outcome (1 in time, 2 slot, 3 waited)
+constexpr int kPTimeline = 1 << 16;
+__device__ unsigned long long g_ptimeline[kPTimeline * 8];
+#define CPK_PSTAMP(k) (pk[k] = wall_clock64())
 #else
+#define CPK_PSTAMP(k)
 #define CPK_PDIAG(k, v)
 #endif
 
@@ -341,6 +347,11 @@ pack_tile_kernel(PackTileArgs a) {
   sel_tab[tid] = make_sel((uint32_t)tid);
   const uint64_t T = blockIdx.x;
   const int l = lane_id();
+#ifdef CPK_DIAG
+  uint64_t pk[5] = {0, 0, 0, 0, 0};
+  uint32_t pout = 0;
+  CPK_PSTAMP(0);
+#endif
   if (a.frame_mode) {
     // a single-tile batch: the framing launch's work first (chunk starts, statuses)
     unsigned long long* const cb = (unsigned long long*)a.chunk_bits;
@@ -570,6 +581,9 @@ pack_tile_kernel(PackTileArgs a) {
       store_agent(a.desc + T, (T == 0 ? kDescIncl : kDescAgg) | agg);
     }
   }
+#ifdef CPK_DIAG
+  CPK_PSTAMP(1);
+#endif
 
   // ---- requested positions (message starts) in this wave: bytes before them in the tile ---
   if (a.pos) {
@@ -655,6 +669,9 @@ pack_tile_kernel(PackTileArgs a) {
       __builtin_amdgcn_sched_barrier(0);
     }
     lds_barrier();  // ---- C: staged ------------------------------------------------------
+#ifdef CPK_DIAG
+    if (win == 0) CPK_PSTAMP(2);
+#endif
     // A tile of few bytes (sparse words) goes to its own small slot at once -- copying it twice
     // costs less than a workgroup stalled on a round trip -- while wave 0 publishes its
     // inclusive prefix when the predecessors have theirs (so the placement launch finds one near).
@@ -700,6 +717,9 @@ pack_tile_kernel(PackTileArgs a) {
         if (l == 0) {
           CPK_PDIAG(0, 1);
           CPK_PDIAG(wait ? 3 : (slot != ~0u ? 2 : 1), 1);
+#ifdef CPK_DIAG
+          pout = wait ? 3 : (slot != ~0u ? 2 : 1);
+#endif
         }
         ok = ok && ex + agg <= a.out_capacity;  // (too small an output: placement raises it)
         if (l == 0) {
@@ -710,6 +730,9 @@ pack_tile_kernel(PackTileArgs a) {
         }
       }
       lds_barrier();  // ---- D: offset or slot ---------------------------------------------
+#ifdef CPK_DIAG
+      CPK_PSTAMP(3);
+#endif
     }
     const uint64_t ex = uniform64(s_dst);
     if (ex != ~0ull) {
@@ -734,6 +757,15 @@ pack_tile_kernel(PackTileArgs a) {
       lds_barrier();
     }
   }
+#ifdef CPK_DIAG
+  CPK_PSTAMP(4);
+  if (tid == 0 && T < (uint64_t)kPTimeline) {
+    for (int k = 0; k < 5; k++) g_ptimeline[8 * T + k] = pk[k];
+    g_ptimeline[8 * T + 5] = pout;
+    g_ptimeline[8 * T + 6] = agg;
+    g_ptimeline[8 * T + 7] = __builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_ID
+  }
+#endif
   if (a.frame_mode) {
     // (a single-tile batch has no placement launch) the total for the positions at the batch
     // end; a tile the output cannot hold raises the capacity error here
@@ -1488,6 +1520,16 @@ hipError_t launch_pack_place(const PackTileArgs& a, hipStream_t stream) {
 }  // namespace cpk
 
 #ifdef CPK_DIAG
+// diagnostic build only: copies out (and zeroes) the pack timeline of the first n tiles
+extern "C" int cpk_debug_ptimeline(uint64_t* out, int n) {
+  if (n > cpk::kPTimeline) n = cpk::kPTimeline;
+  if (hipDeviceSynchronize() != hipSuccess) return 10;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(cpk::g_ptimeline), (size_t)n * 64) != hipSuccess) return 10;
+  static uint64_t z[cpk::kPTimeline * 8];
+  if (hipMemcpyToSymbol(HIP_SYMBOL(cpk::g_ptimeline), z, sizeof z) != hipSuccess) return 10;
+  return 0;
+}
+
 extern "C" int cpk_debug_pdiag(uint64_t* out, int reset) {
   if (hipDeviceSynchronize() != hipSuccess) return 10;
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(cpk::g_pdiag), 4 * sizeof(uint64_t)) != hipSuccess) return 10;

@@ -34,6 +34,10 @@ namespace cpk {
 #ifdef CPK_DIAG
 // diagnostic build only (-DCPK_DIAG): per-phase step counters, read by cpk_debug_diag
 __device__ unsigned long long g_diag[32];
+// per-tile timeline of the first kTimelineTiles tiles: wall-clock stamps (100 MHz) at the phase
+// boundaries the clock counters use, then the wave's hardware id; read by cpk_debug_timeline
+constexpr int kTimelineTiles = 1 << 16;
+__device__ unsigned long long g_timeline[kTimelineTiles * 8];
 #endif
 
 namespace {
@@ -1123,8 +1127,10 @@ __device__ uint64_t lookback_flat(const UnpackArgs& a, uint64_t t, uint32_t* xpr
     const uint64_t* wait_on = nullptr;
     uint64_t want = 0;  // 0: non-zero; kDescIncl: INCL
     if (nb) {
+      CPK_DIAG_ONLY(diag_add(27, 1));
       wait_on = a.desc + (t - 1 - lowest_bit(nb));
     } else if (k == 64) {
+      CPK_DIAG_ONLY(diag_add(26, 1));
       wait_on = a.desc + (t - 64);
       want = kDescIncl;
     } else {
@@ -1156,6 +1162,8 @@ __device__ uint64_t lookback_flat(const UnpackArgs& a, uint64_t t, uint32_t* xpr
           acc += d2j & kD2WordsMask;
           continue;
         }
+        CPK_DIAG_ONLY(diag_add(22, 1); diag_add(23, E < 16); diag_add(24, E >= 64);
+                      diag_add(25, d2j == kD2None));
         stuck = j;
         break;
       }
@@ -1177,6 +1185,194 @@ __device__ uint64_t lookback_flat(const UnpackArgs& a, uint64_t t, uint32_t* xpr
     spins = uniform32(spins);
     if (spins >= kSpinLimit) {
       raise_error(a.err, kErrInternal);
+      *xprev = (uint32_t)kB;
+      return 0;
+    }
+  }
+}
+
+#ifndef CPK_FLAT_SCAN
+#define CPK_FLAT_SCAN 1  // 0: the serial flat look-back (one window, waits for the INCL 64 back)
+#endif
+constexpr int kFlatWindows = 16;
+
+// Flat look-back by composition (CPK_FLAT_SCAN).  A tile's true entry is one of two candidates
+// when the look-back can resolve it: a (E1, the entry the predecessor's chain-0 exit gives: the
+// tile's AGG holds its exit and words) or b (E2, its desc2 candidate).  So each tile is a transfer
+// function from {a, b} to the state its exit gives the next tile ({a, b} or fail) plus words, and
+// runs of tiles compose: a wave composes a window of 64 tiles in six shuffle steps, windows compose
+// in turn, and the look-back reads window after window until an INCL -- the serial resolution (one
+// lane step per tile) and its one-window limit (no INCL within 64 tiles: wait for the INCL 64
+// back, so the INCL frontier moved 64 tiles per hop) are gone.  A tile whose entry matches neither
+// candidate is waited for (its INCL; rare: 0.3 % of the tiles of the bench stream).
+__device__ __forceinline__ uint32_t flat_cls(uint32_t E, uint32_t E1, uint32_t E2, uint32_t v2) {
+  return E == E1 ? 0u : ((v2 && E == E2) ? 1u : 2u);
+}
+__device__ __forceinline__ uint32_t flat_entry(uint32_t x) {
+  return x >= (uint32_t)kDead ? (uint32_t)kB : x - (uint32_t)kB;
+}
+// one lane polls p until (value & mask) == want (want 0: until non-zero); false: spin limit
+__device__ bool flat_wait(const uint64_t* p, uint64_t mask, uint64_t want, uint32_t* spins,
+                          uint32_t* err) {
+  if (lane_id() == 0) {
+    for (;;) {
+      const uint64_t v = load_agent(p);
+      if (want ? (v & mask) == want : v != 0) break;
+      if (++*spins >= kSpinLimit) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  *spins = uniform32(*spins);
+  if (*spins >= kSpinLimit) {
+    raise_error(err, kErrInternal);
+    return false;
+  }
+  return true;
+}
+
+__device__ uint64_t lookback_flat_scan(const UnpackArgs& a, uint64_t t, uint32_t* xprev) {
+  const int l = lane_id();
+  uint32_t spins = 0;
+  for (;;) {  // (a pass; a wait starts the next -- and counts against the spin limit, so a
+              // wait that makes no progress cannot loop for ever)
+    if (++spins >= kSpinLimit) {
+      raise_error(a.err, kErrInternal);
+      *xprev = (uint32_t)kB;
+      return 0;
+    }
+    // composite of the windows read so far, nearest first: far-edge state -> tile t-1's exit
+    // (a: its AGG exit, b: its desc2 exit)
+    uint32_t Gs[2] = {0u, 1u};
+    uint64_t Gw[2] = {0, 0};
+    uint32_t c1 = 0, c2 = 0, cv = 0;  // the nearer window's far tile's candidates
+    uint32_t exA0 = 0, exB0 = 0;
+    const uint64_t* wait_p = nullptr;
+    uint64_t wait_mask = 0, wait_want = 0;
+    int w = 0;
+    while (w < kFlatWindows) {
+      const int64_t base = (int64_t)t - 1 - 64 * w;
+      const int64_t u = base - l;
+      // before tile 0: an inclusive zero whose exit enters tile 0 at byte 0
+      const uint64_t dv = u >= 0 ? load_agent(a.desc + u) : (kDescIncl | kOkBit);
+      const uint64_t stt = dv & kDescFlags;
+      const uint64_t ib = ballot(stt == kDescIncl);
+      const int k = ib ? lowest_bit(ib) : 64;
+      const uint64_t nb = ballot(l < k && stt == 0);
+      if (nb) {  // a descriptor not published yet: wait for it, then read this window again
+        CPK_DIAG_ONLY(diag_add(27, 1));
+        if (!flat_wait(a.desc + (base - lowest_bit(nb)), 0, 0, &spins, a.err)) break;
+        continue;
+      }
+      const bool agg = l < k;  // (AGG: published, not INCL)
+      const uint64_t d2 = agg ? load_agent(a.desc2 + u) : kD2None;
+      const uint32_t xq = agg ? (load_agent32(a.x0p + u - 1) & 0x7fffffffu) : 0u;
+      const uint64_t n2 = ballot(agg && d2 == 0);
+      if (n2) {
+        CPK_DIAG_ONLY(diag_add(27, 1));
+        if (!flat_wait(a.desc2 + (base - lowest_bit(n2)), 0, 0, &spins, a.err)) break;
+        continue;
+      }
+      const uint32_t E1 = flat_entry(xq);
+      const uint32_t v2 = (agg && d2 != kD2None) ? 1u : 0u;
+      const uint32_t E2 = v2 ? (uint32_t)((d2 >> kD2EntryShift) & 0x1fffu) : 0u;
+      const uint32_t exA = desc_exit(dv), exB = v2 ? desc_exit(d2) : exA;
+      // the successor's candidates: lane l - 1's; lane 0: the nearer window's far tile's, or in
+      // window 0 (successor: tile t) the exits themselves, so the state says which exit
+      const int ps = l > 0 ? l - 1 : 0;
+      uint32_t sE1 = shfl32(E1, ps), sE2 = shfl32(E2, ps), sv = shfl32(v2, ps);
+      if (l == 0) {
+        sE1 = w == 0 ? flat_entry(exA) : c1;
+        sE2 = w == 0 ? flat_entry(exB) : c2;
+        sv = w == 0 ? v2 : cv;
+      }
+      if (w == 0) {
+        exA0 = readlane32(exA, 0);
+        exB0 = readlane32(exB, 0);
+      }
+      // the lane's transfer function (lanes >= k: not composed)
+      const uint32_t fa = flat_cls(flat_entry(exA), sE1, sE2, sv);
+      const uint32_t fb = v2 ? flat_cls(flat_entry(exB), sE1, sE2, sv) : 2u;
+      const uint32_t fwa = (uint32_t)(dv & kWordsMask), fwb = (uint32_t)(d2 & kD2WordsMask);
+      uint32_t sa = fa, sb = fb, wa = fwa, wb = fwb;
+      // compose lanes [0, k): lane l ends with tiles l .. k-1 (the predecessor side applied first)
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int q = l + o < 64 ? l + o : 63;
+        const uint32_t psa = shfl32(sa, q), psb = shfl32(sb, q);
+        const uint32_t pwa = shfl32(wa, q), pwb = shfl32(wb, q);
+        if (l + o < k) {
+          const uint32_t na = psa == 2u ? 2u : (psa == 0u ? sa : sb);
+          const uint32_t nwa = pwa + (psa == 0u ? wa : wb);
+          const uint32_t nb2 = psb == 2u ? 2u : (psb == 0u ? sa : sb);
+          const uint32_t nwb = pwb + (psb == 0u ? wa : wb);
+          sa = na;
+          wa = nwa;
+          sb = nb2;
+          wb = nwb;
+        }
+      }
+      const uint32_t Fs[2] = {k ? readlane32(sa, 0) : 0u, k ? readlane32(sb, 0) : 1u};
+      const uint32_t Fw[2] = {k ? readlane32(wa, 0) : 0u, k ? readlane32(wb, 0) : 0u};
+      if (k < 64) {
+        const uint64_t dk = readlane64(dv, k);
+        if (k == 0 && w == 0) {  // tile t - 1 holds an INCL
+          *xprev = desc_exit(dk);
+          return dk & kWordsMask;
+        }
+        // the INCL's exit in the states of the tile after it
+        const uint32_t kE1 = k ? readlane32(E1, k - 1) : c1;
+        const uint32_t kE2 = k ? readlane32(E2, k - 1) : c2;
+        const uint32_t kv = k ? readlane32(v2, k - 1) : cv;
+        const uint32_t s0 = flat_cls(flat_entry(desc_exit(dk)), kE1, kE2, kv);
+        const uint32_t s1 = s0 == 2u ? 2u : Fs[s0];
+        const uint32_t s2 = s1 == 2u ? 2u : Gs[s1];
+        if (s2 != 2u) {
+          CPK_DIAG_ONLY(diag_add(29, w + 1));
+          *xprev = s2 == 0u ? exA0 : exB0;
+          return (dk & kWordsMask) + Fw[s0] + Gw[s1];
+        }
+        // an entry that matches neither candidate: wait for that tile's INCL
+        if (s0 == 2u) {
+          wait_p = a.desc + (k ? base - (k - 1) : base + 1);  // (the tile after the INCL)
+        } else if (s1 == 2u) {
+          // in this window: the state entering lane l is lane l + 1's composite applied to s0
+          const int q = l + 1 < 64 ? l + 1 : 63;
+          const uint32_t qa = shfl32(sa, q), qb = shfl32(sb, q);
+          const uint32_t in = l + 1 >= k ? s0 : (s0 == 2u ? 2u : (s0 == 0u ? qa : qb));
+          const uint32_t out = in == 2u ? 2u : (in == 0u ? fa : fb);
+          const uint64_t fl = ballot(l < k && in != 2u && out == 2u);
+          wait_p = a.desc + (base - (fl ? highest_bit(fl) : 0));
+        } else {
+          wait_p = a.desc + (base + 1);  // (in a nearer window: its far tile)
+        }
+        wait_mask = kDescFlags;
+        wait_want = kDescIncl;
+        break;
+      }
+      // no INCL in this window: G := G after F; this window's far tile's candidates carry over
+      uint32_t ns[2];
+      uint64_t nw[2];
+#pragma unroll
+      for (int s = 0; s < 2; s++) {
+        ns[s] = Fs[s] == 2u ? 2u : Gs[Fs[s]];
+        nw[s] = Fw[s] + (Fs[s] == 2u ? 0ull : Gw[Fs[s]]);
+      }
+      Gs[0] = ns[0];
+      Gs[1] = ns[1];
+      Gw[0] = nw[0];
+      Gw[1] = nw[1];
+      c1 = readlane32(E1, 63);
+      c2 = readlane32(E2, 63);
+      cv = readlane32(v2, 63);
+      w++;
+    }
+    if (!wait_p) {  // no INCL within kFlatWindows windows: the farthest tile read
+      wait_p = a.desc + ((int64_t)t - 64 * kFlatWindows);
+      wait_mask = kDescFlags;
+      wait_want = kDescIncl;
+    }
+    CPK_DIAG_ONLY(diag_add(26, 1); diag_add(28, w));
+    if (spins >= kSpinLimit || !flat_wait(wait_p, wait_mask, wait_want, &spins, a.err)) {
       *xprev = (uint32_t)kB;
       return 0;
     }
@@ -1600,7 +1796,7 @@ unpack_tiles_kernel(UnpackArgs a) {
   __syncthreads();
   const uint64_t t = (uint64_t)blockIdx.x * 4 + wv;
   if (t >= a.ntiles) return;
-  CPK_DIAG_ONLY(uint64_t ck[7]; ck[0] = clock64());
+  CPK_DIAG_ONLY(uint64_t ck[7]; uint64_t wk[7]; ck[0] = clock64(); wk[0] = wall_clock64());
   // the header launch is done: its scan descriptors go back to zero for the next call
   for (uint64_t i = t + a.ntiles * (uint64_t)l; i < a.hdr_nblocks; i += 64 * a.ntiles)
     a.hdr_desc[i] = 0;
@@ -1618,7 +1814,7 @@ unpack_tiles_kernel(UnpackArgs a) {
   const uint64_t msw = aux[l];
   lane_handoff();
   const SubTile st = make_subtile(A, P, msw, nms_tile_after);
-  CPK_DIAG_ONLY(ck[1] = clock64());
+  CPK_DIAG_ONLY(ck[1] = clock64(); wk[1] = wall_clock64());
   if (a.debug_skip & 64) {  // diagnostic: staging + message window only
     if (l == 0 && st.msw == 0) a.x0p[t] = 0x80000000u | (uint32_t)ballot(st.msw != 0);
     return;
@@ -1690,7 +1886,7 @@ unpack_tiles_kernel(UnpackArgs a) {
     }
   }
   if (l == 0) store_agent32(a.x0p + t, 0x80000000u | x0);
-  CPK_DIAG_ONLY(ck[2] = ck[3] = ck[4] = ck[5] = clock64());
+  CPK_DIAG_ONLY(ck[2] = ck[3] = ck[4] = ck[5] = clock64(); wk[2] = wk[3] = wk[4] = wk[5] = wall_clock64());
   if (a.debug_skip & 128) return;  // diagnostic: + chain-0 walks and settle
   if (!settled) {
     // unreachable (the fixed point settles in at most 64 rounds): refuse the batch, write nothing
@@ -1725,13 +1921,15 @@ unpack_tiles_kernel(UnpackArgs a) {
       if (l == 0) store_agent(a.desc + t, make_desc(kDescIncl, x0, x0, w));
     }
   } else {
-    // optimistic entry: where the predecessor's chain 0 leads
-    const uint32_t xp = wait_nonzero32(a.x0p + t - 1, a.err) & 0x7fffffffu;
-    CPK_DIAG_ONLY(ck[3] = ck[4] = ck[5] = clock64());
-    const uint32_t Eopt = entry_from_exit(xp, fms);
+    // optimistic entry: where the predecessor's chain 0 leads (a tile with a message start
+    // publishes its descriptor already, so it goes straight to the look-back)
+    const uint32_t xp = has_start ? 0u : wait_nonzero32(a.x0p + t - 1, a.err) & 0x7fffffffu;
+    CPK_DIAG_ONLY(ck[3] = ck[4] = ck[5] = clock64(); wk[3] = wk[4] = wk[5] = wall_clock64());
+    const uint32_t Eopt = has_start ? ~0u : entry_from_exit(xp, fms);
     uint32_t xE = x0;
     uint64_t runs = runm;
-    if (Eopt != (uint32_t)q0 && Eopt < fms)
+    if (has_start) {
+    } else if (Eopt != (uint32_t)q0 && Eopt < fms)
       tm = enter_chain(d, aux, st, tm0, (int)Eopt, (int)fms, x0, &xE, &runs);
     else if (Eopt >= fms)
       tm = clip_below(tm0, fms, st.s, &xE);
@@ -1762,12 +1960,12 @@ unpack_tiles_kernel(UnpackArgs a) {
       if (l == 0) store_agent(a.desc2 + t, d2);
     }
     uint32_t xprev = xp;
-    CPK_DIAG_ONLY(ck[4] = clock64());
+    CPK_DIAG_ONLY(ck[4] = clock64(); wk[4] = wall_clock64());
     if (!(a.debug_skip & 8)) {
-      if constexpr (FLAT) excl = lookback_flat(a, t, &xprev);
+      if constexpr (FLAT) excl = CPK_FLAT_SCAN ? lookback_flat_scan(a, t, &xprev) : lookback_flat(a, t, &xprev);
       else excl = lookback_tiles(a, t, &xprev);
     }
-    CPK_DIAG_ONLY(ck[5] = clock64());
+    CPK_DIAG_ONLY(ck[5] = clock64(); wk[5] = wall_clock64());
     const uint32_t E = entry_from_exit(xprev, fms);
     CPK_DIAG_ONLY(diag_add(9, E != Eopt); diag_add(10, Eopt > 0 && Eopt < fms));
     if (E != Eopt) {
@@ -1810,7 +2008,12 @@ unpack_tiles_kernel(UnpackArgs a) {
   }
 #ifdef CPK_DIAG
   ck[6] = clock64();
+  wk[6] = wall_clock64();
   for (int k = 0; k < 6; k++) diag_add(16 + k, ck[k + 1] - ck[k]);
+  if (l == 0 && t < (uint64_t)kTimelineTiles) {
+    for (int k = 0; k < 7; k++) g_timeline[8 * t + k] = wk[k];
+    g_timeline[8 * t + 7] = __builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_ID
+  }
 #endif
 }
 
@@ -1886,6 +2089,10 @@ hipError_t launch_unpack_stage(int stage, const UnpackArgs& a, hipStream_t strea
 //  14 tiles whose optimistic entry's exit is not their chain-0 exit (no ok bit)
 //  16..21 clock cycles (s_memtime) per phase: staging and message window, chain 0, waiting for
 //  the predecessor's chain-0 exit, the optimistic entry, the look-back, the expansion
+//  22..27 flat look-back events: stuck (entry matches no candidate), ... with entry < 16, ... with
+//  entry >= 64, ... with no second candidate, waits for an INCL (no INCL within reach, or an entry
+//  matching no candidate), waits for a descriptor not published yet
+//  28/29 composed flat look-back: windows read before an INCL wait, windows read to resolve
 extern "C" int cpk_debug_diag(uint64_t* out, int reset) {
   if (hipDeviceSynchronize() != hipSuccess) return 10;
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(cpk::g_diag), 32 * sizeof(uint64_t)) != hipSuccess) return 10;
@@ -1893,6 +2100,16 @@ extern "C" int cpk_debug_diag(uint64_t* out, int reset) {
     const uint64_t z[32] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(cpk::g_diag), z, sizeof z) != hipSuccess) return 10;
   }
+  return 0;
+}
+
+// diagnostic build only: copies out (and zeroes) the timeline of the first n tiles (8 words each)
+extern "C" int cpk_debug_timeline(uint64_t* out, int n) {
+  if (n > cpk::kTimelineTiles) n = cpk::kTimelineTiles;
+  if (hipDeviceSynchronize() != hipSuccess) return 10;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(cpk::g_timeline), (size_t)n * 64) != hipSuccess) return 10;
+  static uint64_t z[cpk::kTimelineTiles * 8];
+  if (hipMemcpyToSymbol(HIP_SYMBOL(cpk::g_timeline), z, sizeof z) != hipSuccess) return 10;
   return 0;
 }
 #endif
