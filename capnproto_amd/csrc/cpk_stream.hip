@@ -224,8 +224,14 @@ __device__ WalkEnd walk_messages(const Flat& F, const uint64_t* __restrict__ wor
 // blocks in order: a block whose true entry (the previous block's exit) is its guess keeps its
 // walk; any other block is walked again from its true entry.  A last pass writes every block's
 // messages at their global index.
-constexpr uint64_t kSplitBlock = 1ull << 20;  // words per block
-constexpr uint32_t kSplitList = 4096;          // message starts a block keeps
+#ifndef CPK_SPLIT_BLOCK_LOG
+#define CPK_SPLIT_BLOCK_LOG 16  // log2 words per block (20: C5-shaped split 4.1 ms guess walks)
+#endif
+// Blocks are the unit of parallelism of the guess, meet and write walks (one wave each, a few
+// dependent loads per message): 64 Ki-word blocks give a C5-shaped stream ~7 k waves where 1 Mi
+// gave 456, each walking ~150 messages instead of ~2300.
+constexpr uint64_t kSplitBlock = 1ull << CPK_SPLIT_BLOCK_LOG;  // words per block
+constexpr uint32_t kSplitList = CPK_SPLIT_BLOCK_LOG >= 20 ? 4096 : 2048;  // starts a block keeps
 constexpr uint64_t kSplitScan = 1ull << 16;    // words a block searches for its guess
 
 struct SplitBlock {
@@ -372,6 +378,88 @@ __global__ __launch_bounds__(64) void split_meet_kernel(Flat F, const uint64_t* 
   }
 }
 
+// A full window of 64 blocks resolved in parallel.  Block b's entry is, nearly always, one of two
+// known candidates: its guess g (state a: then its walk gives exit x, k messages, stop) or the
+// entry the previous block's guess chain leaves it at, se (state b: split_meet_kernel's walk
+// gives sx, sk, sst).  So each block maps the state of its entry to the state its exit gives the
+// next block (a, b; 2: neither; 3: the chain stopped) plus messages, these maps compose, and six
+// shuffle steps give every block its entry state and message base.  Returns the blocks resolved:
+// up to the first whose entry matches neither candidate (a block passed over by a long message,
+// a wrong guess), which the serial pass then takes.
+__device__ int resolve_window(SplitBlock* blocks, uint64_t base, const SplitBlock& mine,
+                              uint64_t max_msgs, uint64_t& E, uint64_t& hE, uint64_t& K,
+                              int32_t& stop) {
+  const int l = lane_id();
+  const uint64_t g0 = readlane64(mine.g, 0), se0 = readlane64(mine.se, 0);
+  const uint32_t sin = (g0 != kNone && E == g0) ? 0u : ((se0 != kNone && E == se0) ? 1u : 2u);
+  if (sin == 2u) return 0;
+  // the next block's candidates (lane 63: not needed -- the window's exit is carried as a word)
+  const uint64_t ng = shfl64(mine.g, l < 63 ? l + 1 : 63);
+  const uint64_t nse = shfl64(mine.se, l < 63 ? l + 1 : 63);
+  auto cls = [&](uint64_t X) -> uint32_t {
+    if (l == 63) return 0u;
+    return (ng != kNone && X == ng) ? 0u : ((nse != kNone && X == nse) ? 1u : 2u);
+  };
+  const uint32_t fa = mine.g == kNone ? 2u : (mine.stop != kRunOn ? 3u : cls(mine.x));
+  const uint32_t fb = mine.se == kNone ? 2u : (mine.sst != kRunOn ? 3u : cls(mine.sx));
+  const uint64_t ka = mine.k, kb = mine.sk;
+  // inclusive composition toward higher lanes (the earlier block applied first)
+  uint32_t sa = fa, sb = fb;
+  uint64_t wa = ka, wb = kb;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int q = l >= o ? l - o : 0;
+    const uint32_t psa = shfl32(sa, q), psb = shfl32(sb, q);
+    const uint64_t pwa = shfl64(wa, q), pwb = shfl64(wb, q);
+    if (l >= o) {
+      const uint32_t na = psa >= 2u ? psa : (psa == 0u ? sa : sb);
+      const uint64_t nwa = pwa + (psa >= 2u ? 0ull : (psa == 0u ? wa : wb));
+      const uint32_t nb = psb >= 2u ? psb : (psb == 0u ? sa : sb);
+      const uint64_t nwb = pwb + (psb >= 2u ? 0ull : (psb == 0u ? wa : wb));
+      sa = na;
+      wa = nwa;
+      sb = nb;
+      wb = nwb;
+    }
+  }
+  // the state entering each block, and the messages before it
+  const int q = l > 0 ? l - 1 : 0;
+  const uint32_t pa = shfl32(sa, q), pb = shfl32(sb, q);
+  const uint64_t pwa = shfl64(wa, q), pwb = shfl64(wb, q);
+  const uint32_t in = l == 0 ? sin : (sin == 0u ? pa : pb);
+  const uint64_t kin = K + (l == 0 ? 0ull : (sin == 0u ? pwa : pwb));
+  const uint64_t fb2 = ballot(in == 2u);
+  const int f = fb2 ? lowest_bit(fb2) : 64;  // the first block that matches neither
+  if (f == 0) return 0;
+  const bool reached = in < 2u && l < f;
+  const uint64_t kk = in == 0u ? mine.k : mine.sk;
+  const uint64_t kend = kin + kk;
+  // the message limit: the first block it falls in is cut there (the writer walks it)
+  const uint64_t cb = ballot(reached && kend >= max_msgs);
+  const int cut = cb ? lowest_bit(cb) : 64;
+  if (reached && l <= cut) {
+    SplitBlock* const B = blocks + base + l;
+    B->entry = in == 0u ? mine.g : mine.se;
+    B->kbase = kin;
+    B->kend = l == cut ? max_msgs : kend;
+    B->over = (l == cut || in == 1u || mine.over) ? 1u : 0u;
+  }
+  if (cut < 64) {
+    K = max_msgs;
+    stop = sOK;
+    return 64;
+  }
+  // the last block reached: its exit goes on, or the chain stopped in it
+  const int last = 63 - __builtin_clzll(ballot(reached));
+  const uint32_t il = readlane32(in, last);
+  E = readlane64(il == 0u ? mine.x : mine.sx, last);
+  hE = readlane64(il == 0u ? mine.hx : mine.shx, last);
+  K = readlane64(kend, last);
+  const int32_t st = (int32_t)readlane32((uint32_t)(il == 0u ? mine.stop : mine.sst), last);
+  if (st != kRunOn) stop = st;
+  return f;
+}
+
 // One wave over the blocks in order: each block's true entry, global message range and the
 // stream's stop.  A block whose entry is its guess (or that the chain passes over) costs a load;
 // any other block is walked again here.
@@ -388,11 +476,16 @@ __global__ __launch_bounds__(64) void split_resolve_kernel(Flat F, const uint64_
   const int l = lane_id();
   uint64_t E = 0, hE = F.head(0), K = 0;
   int32_t stop = kRunOn;
-  for (uint64_t base = 0; base < nblocks && stop == kRunOn; base += 64) {
+  for (uint64_t base = 0; base < nblocks && stop == kRunOn;) {
     // the next 64 blocks' walks in one round trip (lane j: block base + j)
     SplitBlock mine = {};
     if (base + l < nblocks) mine = blocks[base + l];
-    for (int j = 0; j < 64 && base + j < nblocks && stop == kRunOn; j++) {
+    // in parallel up to the first block whose entry matches neither candidate; that block
+    // serially; then the next window from the block after it (the last, partial window: serially)
+    const bool full = base + 64 <= nblocks;
+    const int done = full ? resolve_window(blocks, base, mine, max_msgs, E, hE, K, stop) : 0;
+    const int jend = full ? (done < 64 ? done + 1 : 64) : 64;
+    for (int j = done; j < jend && base + j < nblocks && stop == kRunOn; j++) {
       const uint64_t b = base + j;
       const uint64_t w1 = (b + 1) * kSplitBlock;
       if (E >= w1) continue;  // the chain passes over the block (a message longer than it)
@@ -460,6 +553,7 @@ __global__ __launch_bounds__(64) void split_resolve_kernel(Flat F, const uint64_
       hE = hx;
       stop = st;
     }
+    base += (uint64_t)jend;
   }
   if (stop == kRunOn) stop = sOK;  // (nblocks covers every decoded word)
   if (l == 0) {

@@ -8,5 +8,5 @@ for v in base ${VARIANTS}; do
   [ $rc = 0 ] || { echo "split prof $v failed"; tail -5 gpurun_out/${TAG}_split_$v.log; exit 1; }
   echo "== $v"; grep "split ms" gpurun_out/${TAG}_split_$v.log
 done
-timeout -k 10 300 python3 tools/diag_unpack.py capnproto_amd/var_diag.so split > gpurun_out/${TAG}_diag_split.log 2>&1 || { tail -5 gpurun_out/${TAG}_diag_split.log; exit 1; }
+timeout -k 10 150 python3 tools/diag_unpack.py capnproto_amd/var_diag.so split > gpurun_out/${TAG}_diag_split.log 2>&1 || { tail -5 gpurun_out/${TAG}_diag_split.log; exit 1; }
 grep -v amdgpu.ids gpurun_out/${TAG}_diag_split.log
