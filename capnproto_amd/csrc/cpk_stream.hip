@@ -234,6 +234,10 @@ constexpr uint64_t kSplitBlock = 1ull << CPK_SPLIT_BLOCK_LOG;  // words per bloc
 constexpr uint32_t kSplitList = CPK_SPLIT_BLOCK_LOG >= 20 ? 4096 : 2048;  // starts a block keeps
 constexpr uint64_t kSplitScan = 1ull << 16;    // words a block searches for its guess
 
+// in-order pass counters (diagnostic, read by cpk_debug_split): windows resolved in parallel,
+// blocks they resolved, then serial blocks by path -- guess, se, se2, walked, passed over
+__device__ unsigned long long g_split_dbg[8];
+
 struct SplitBlock {
   uint64_t g, x, hx, k;  // guess (kNone: none), exit word / head, messages
   int32_t stop;          // kRunOn, or why the walk from the guess ended inside the block
@@ -243,6 +247,10 @@ struct SplitBlock {
   // entry whenever the previous block's true chain met its guess: messages, exit, stop
   uint64_t se, sk, sx, shx;
   int32_t sst;
+  // the same from the previous block's se walk's exit, when that walk did not meet its guess
+  // chain (a guess off the chain: the next block's se then is not its entry)
+  uint64_t se2, sk2, sx2, shx2;
+  int32_t sst2;
 };
 
 __global__ __launch_bounds__(64) void split_spec_kernel(Flat F, const uint64_t* __restrict__ words,
@@ -312,6 +320,9 @@ __global__ __launch_bounds__(64) void split_spec_kernel(Flat F, const uint64_t* 
     r.se = kNone;
     r.sk = r.sx = r.shx = 0;
     r.sst = kRunOn;
+    r.se2 = kNone;
+    r.sk2 = r.sx2 = r.shx2 = 0;
+    r.sst2 = kRunOn;
     blocks[b] = r;
   }
 }
@@ -375,6 +386,45 @@ __global__ __launch_bounds__(64) void split_meet_kernel(Flat F, const uint64_t* 
     B->sx = sx;
     B->shx = shx;
     B->sst = sst;
+  }
+}
+
+// Every block b > 1 whose predecessor's se walk ran past its guess chain without meeting it (the
+// predecessor's guess was off the chain, so its exit is not where the true chain leaves it):
+// walked from that walk's exit until it meets block b's guess chain -- a third candidate entry
+// the in-order pass takes without walking.
+__global__ __launch_bounds__(64) void split_meet2_kernel(Flat F, const uint64_t* __restrict__ words,
+                                                         uint64_t limit, SplitBlock* blocks,
+                                                         const uint64_t* __restrict__ lists,
+                                                         uint64_t nblocks) {
+  F.load();
+  const uint64_t b = (uint64_t)blockIdx.x + 2;
+  if (b >= nblocks) return;
+  const SplitBlock& P = blocks[b - 1];
+  const uint64_t E = P.sx, hE = P.shx;
+  const uint64_t g = blocks[b].g, gk = blocks[b].k, se = blocks[b].se;
+  const uint64_t w1 = (b + 1) * kSplitBlock;
+  if (P.se == kNone || P.sst != kRunOn || E == P.x || E >= w1 || E == g || E == se) return;
+  const bool listed = g != kNone && gk <= kSplitList;
+  uint64_t jl = 0;
+  Meet2 mt{lists + b * kSplitList, listed ? gk : 0, &jl};
+  const WalkEnd we = walk_messages(F, words, E, hE, ~0ull, limit, w1,
+                                   [&](uint64_t, uint64_t, uint64_t) {}, mt);
+  jl = readlane64(jl, 0);
+  if (lane_id() == 0) {
+    SplitBlock* const B = blocks + b;
+    B->se2 = E;
+    if (we.stop == kMet) {
+      B->sk2 = we.k + (gk - jl);
+      B->sx2 = blocks[b].x;
+      B->shx2 = blocks[b].hx;
+      B->sst2 = blocks[b].stop;
+    } else {
+      B->sk2 = we.k;
+      B->sx2 = we.s;
+      B->shx2 = we.hs;
+      B->sst2 = we.stop;
+    }
   }
 }
 
@@ -484,32 +534,50 @@ __global__ __launch_bounds__(64) void split_resolve_kernel(Flat F, const uint64_
     // serially; then the next window from the block after it (the last, partial window: serially)
     const bool full = base + 64 <= nblocks;
     const int done = full ? resolve_window(blocks, base, mine, max_msgs, E, hE, K, stop) : 0;
+    if (l == 0 && done) {
+      atomicAdd(&g_split_dbg[0], 1ull);
+      atomicAdd(&g_split_dbg[1], (unsigned long long)done);
+    }
     const int jend = full ? (done < 64 ? done + 1 : 64) : 64;
     for (int j = done; j < jend && base + j < nblocks && stop == kRunOn; j++) {
       const uint64_t b = base + j;
       const uint64_t w1 = (b + 1) * kSplitBlock;
-      if (E >= w1) continue;  // the chain passes over the block (a message longer than it)
+      if (E >= w1) {  // the chain passes over the block (a message longer than it)
+        if (l == 0) atomicAdd(&g_split_dbg[6], 1ull);
+        continue;
+      }
       const uint64_t g = readlane64(mine.g, j);
       uint64_t x, hx, k;
       int32_t st;
       bool redo = readlane32(mine.over, j) != 0;
       if (g == E) {
+        if (l == 0) atomicAdd(&g_split_dbg[2], 1ull);
         x = readlane64(mine.x, j);
         hx = readlane64(mine.hx, j);
         k = readlane64(mine.k, j);
         st = (int32_t)readlane32((uint32_t)mine.stop, j);
       } else if (readlane64(mine.se, j) == E) {
         // walked in parallel from this very entry (split_meet_kernel)
+        if (l == 0) atomicAdd(&g_split_dbg[3], 1ull);
         x = readlane64(mine.sx, j);
         hx = readlane64(mine.shx, j);
         k = readlane64(mine.sk, j);
         st = (int32_t)readlane32((uint32_t)mine.sst, j);
+        redo = true;
+      } else if (readlane64(mine.se2, j) == E) {
+        // or from this one (split_meet2_kernel)
+        if (l == 0) atomicAdd(&g_split_dbg[4], 1ull);
+        x = readlane64(mine.sx2, j);
+        hx = readlane64(mine.shx2, j);
+        k = readlane64(mine.sk2, j);
+        st = (int32_t)readlane32((uint32_t)mine.sst2, j);
         redo = true;
       } else {
         // the guess was not the entry: walk the block from its true entry until the chain meets
         // the guess's chain (a guess whose chain ran to the block end without failing nearly
         // always joined the true chain early: a few messages here), then take the rest from it
         const uint64_t gk = readlane64(mine.k, j);
+        if (l == 0) atomicAdd(&g_split_dbg[5], 1ull);
         const bool listed = g != kNone && gk <= kSplitList;
         const uint64_t* const list = lists + b * kSplitList;
         uint64_t jl = 0;  // next listed start to compare with (both chains ascend)
@@ -697,6 +765,7 @@ hipError_t launch_split_walk(const uint8_t* packed, uint64_t nbytes, const uint6
   uint64_t* lists = (uint64_t*)((char*)scratch + ((nb * sizeof(SplitBlock) + 15) & ~15ull));
   split_spec_kernel<<<(unsigned)nb, 64, 0, stream>>>(F, words, limit, blocks, lists);
   if (nb > 1) split_meet_kernel<<<(unsigned)(nb - 1), 64, 0, stream>>>(F, words, limit, blocks, lists, nb);
+  if (nb > 2) split_meet2_kernel<<<(unsigned)(nb - 2), 64, 0, stream>>>(F, words, limit, blocks, lists, nb);
   split_resolve_kernel<<<1, 64, 0, stream>>>(F, words, limit, max_msgs, blocks, lists, nb,
                                              msg_word_off, msg_in_off, status, nmsgs);
   split_write_kernel<<<(unsigned)nb, 64, 0, stream>>>(F, words, limit, blocks, lists,
@@ -705,3 +774,12 @@ hipError_t launch_split_walk(const uint8_t* packed, uint64_t nbytes, const uint6
 }
 
 }  // namespace cpk
+
+// diagnostic: copies out and zeroes the split's in-order pass counters (8 u64)
+extern "C" int cpk_debug_split(uint64_t* out) {
+  if (hipDeviceSynchronize() != hipSuccess) return 10;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(cpk::g_split_dbg), 64) != hipSuccess) return 10;
+  const uint64_t z[8] = {};
+  if (hipMemcpyToSymbol(HIP_SYMBOL(cpk::g_split_dbg), z, 64) != hipSuccess) return 10;
+  return 0;
+}
