@@ -12,4 +12,5 @@ for c in ${PMC_CFGS:-c2 c4 c3}; do
   cp gpurun_out/${TAG}_${c}_traffic_$c.json profiles/traffic_$c.json
 done
 echo "pmc done"
+[ -n "$PMC_ONLY" ] && exit 0
 bash tools/gpu_round.sh $TAG

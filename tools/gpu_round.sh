@@ -31,3 +31,10 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gp
   -- python3 "$R/bench.py" --sub none --steps 20 --warmup 3 --no-cpu-baseline --no-host --no-split > "$R/gpurun_out/${TAG}_prof.log" 2>&1 \
   || { echo "rocprof failed"; tail -20 "$R/gpurun_out/${TAG}_prof.log"; exit 1; }
 echo "rocprof done"
+# the HBM-honest configs' kernel summaries too (C3, C4)
+for c in ${PROF_CFGS-c3 c4}; do
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/${TAG}_prof_$c" -o run \
+    -- python3 "$R/bench.py" --config $c --sub none --steps 5 --warmup 2 --no-cpu-baseline --no-host --no-split > "$R/gpurun_out/${TAG}_prof_$c.log" 2>&1 \
+    || { echo "rocprof $c failed"; tail -20 "$R/gpurun_out/${TAG}_prof_$c.log"; exit 1; }
+  echo "rocprof $c done"
+done
