@@ -130,6 +130,7 @@ struct UnpackArgs {
   uint64_t hdr_limit;
   uint64_t* hdr_word_off;
   int32_t* hdr_status_out;
+  uint32_t prio;                // batches of very long messages: raised wave priority (cpk_unpack.hip)
 };
 constexpr uint64_t kUnpackFuseMsgs = 256;
 

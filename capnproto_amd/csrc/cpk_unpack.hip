@@ -58,6 +58,9 @@ constexpr int kB = (int)kUnpackTileBytes;  // 4096
 constexpr int kPad = 16;
 constexpr int kDead = 1 << 24;  // chain ran into the end of the batch
 
+#ifndef CPK_PRIO
+#define CPK_PRIO 0  // 1: raised wave priority until the tile's descriptors are out, every batch
+#endif
 #ifndef CPK_PIPE
 #define CPK_PIPE 0  // 1: plain-tile batches read the next batch's record bytes ahead
 #endif
@@ -1796,6 +1799,10 @@ unpack_tiles_kernel(UnpackArgs a) {
   __syncthreads();
   const uint64_t t = (uint64_t)blockIdx.x * 4 + wv;
   if (t >= a.ntiles) return;
+  // batches of very long messages (whose look-backs reach back to the previous occupancy round):
+  // the phases later tiles wait on (chain 0, the entry, the descriptors) ahead of other waves'
+  // expansions in the SIMD's issue arbitration (C4 unpack_tiles 4.51 -> 4.21 ms; no gain on C2)
+  if (CPK_PRIO || a.prio) __builtin_amdgcn_s_setprio(2);
   CPK_DIAG_ONLY(uint64_t ck[7]; uint64_t wk[7]; ck[0] = clock64(); wk[0] = wall_clock64());
   // the header launch is done: its scan descriptors go back to zero for the next call
   for (uint64_t i = t + a.ntiles * (uint64_t)l; i < a.hdr_nblocks; i += 64 * a.ntiles)
@@ -1994,6 +2001,7 @@ unpack_tiles_kernel(UnpackArgs a) {
 
   // ---- expansion -------------------------------------------------------------------------
   if (a.debug_skip & 256) return;  // diagnostic: + the entry and the look-back
+  if (CPK_PRIO || a.prio) __builtin_amdgcn_s_setprio(0);
   expand_records<PLAIN>(a, A, d, aux, dep_tab, deposit_sel((uint32_t)l & 15), tm, excl, win, mfirst,
                  mlast, msw, w_tile);
   // a fused single-tile batch: this wave is the whole call -- its error word for the host, last:
