@@ -197,11 +197,12 @@ __device__ __forceinline__ uint64_t header_words(const uint8_t* __restrict__ pac
 // on lower ones).  The look-back descriptors are zero at rest: the tile kernel of the same call
 // clears them once every header block is done (UnpackArgs::hdr_desc).  Blocks past nsb compute
 // tile_first and zero the tile kernel's scratch (TileFirstJob).
-#ifndef CPK_HDR_PER
-#define CPK_HDR_PER 4
-#endif
-constexpr int kHdrPerThread = CPK_HDR_PER;
-constexpr uint64_t kHdrBlock = 256 * kHdrPerThread;
+// Headers per thread: 1 for batches of up to kHdrSmall messages (each thread's two dependent
+// loads are the launch's latency: C2 10.1 -> 5.9 us), 4 above (fewer look-back blocks: C3 66.6 ->
+// 56.3 us).
+constexpr uint64_t kHdrSmall = 1ull << 16;
+__host__ __device__ constexpr int hdr_per(uint64_t n) { return n <= kHdrSmall ? 1 : 4; }
+template <int kHdrPerThread>
 __global__ __launch_bounds__(256) void header_kernel(
     const uint8_t* __restrict__ packed, const uint64_t* __restrict__ in_off, uint64_t n,
     uint64_t limit, uint64_t* __restrict__ word_off, int32_t* __restrict__ hdr_status,
@@ -213,6 +214,7 @@ __global__ __launch_bounds__(256) void header_kernel(
   const uint64_t b = blockIdx.x;
   const int l = lane_id();
   const int wv = (int)(threadIdx.x >> 6);
+  constexpr uint64_t kHdrBlock = 256 * kHdrPerThread;
   const uint64_t m0 = b * kHdrBlock + (uint64_t)kHdrPerThread * threadIdx.x;
   uint64_t w[kHdrPerThread];
   uint64_t sum = 0;
@@ -2056,7 +2058,10 @@ hipError_t launch_unpack_init(uint32_t mode, const uint64_t* in_off, const uint6
   return hipGetLastError();
 }
 
-uint64_t header_scan_blocks(uint64_t n) { return (n + kHdrBlock - 1) / kHdrBlock; }
+uint64_t header_scan_blocks(uint64_t n) {
+  const uint64_t blk = 256ull * (uint64_t)hdr_per(n);
+  return (n + blk - 1) / blk;
+}
 
 hipError_t launch_unpack_header(const uint8_t* packed, const uint64_t* in_off, uint64_t n,
                                 uint64_t limit, uint64_t* word_off, int32_t* hdr_status,
@@ -2064,8 +2069,12 @@ hipError_t launch_unpack_header(const uint8_t* packed, const uint64_t* in_off, u
                                 const TileFirstJob& tf, hipStream_t stream) {
   const unsigned nb = (unsigned)header_scan_blocks(n);
   if (nb + tile_first_blocks(tf) == 0) return hipSuccess;
-  hipLaunchKernelGGL(header_kernel, dim3(nb + tile_first_blocks(tf)), dim3(256), 0, stream,
-                     packed, in_off, n, limit, word_off, hdr_status, status, desc, err, tf, nb);
+  if (hdr_per(n) == 1)
+    hipLaunchKernelGGL(header_kernel<1>, dim3(nb + tile_first_blocks(tf)), dim3(256), 0, stream,
+                       packed, in_off, n, limit, word_off, hdr_status, status, desc, err, tf, nb);
+  else
+    hipLaunchKernelGGL(header_kernel<4>, dim3(nb + tile_first_blocks(tf)), dim3(256), 0, stream,
+                       packed, in_off, n, limit, word_off, hdr_status, status, desc, err, tf, nb);
   return hipGetLastError();
 }
 
