@@ -239,6 +239,36 @@ def test_split_limit_and_cut_in_later_blocks(codec):
     assert torch.equal(w2[:mw], words[:mw])
 
 
+def test_split_messages_longer_than_blocks(codec):
+    """Messages of 150 Ki words, longer than the split's 64 Ki-word blocks, between runs of small
+    ones: blocks a message passes over take the in-order pass's serial path between windows it
+    resolves in parallel, and every boundary still matches the generator's layout."""
+    import torch
+
+    parts = []
+    for i, (n, seg) in enumerate(((3000, 200), (24, 150000), (5000, 60), (9, 150000),
+                                  (2000, 1000))):
+        off, total = codec.gen_offsets(n, 1, seg, seed=31 + i)
+        words = codec.gen_messages("mixed", off, total, 1, seed=31 + i)
+        parts.append((off, total, words))
+    offs, tot = [torch.zeros(1, dtype=torch.int64, device=codec.device)], 0
+    for off, total, _ in parts:
+        offs.append(off[1:] + tot)
+        tot += total
+    off = torch.cat(offs)
+    words = torch.cat([w[:t] for _, t, w in parts])
+    n = off.numel() - 1
+    packed, poff, st = codec.pack_messages(words, off)
+    codec.sync()
+    assert (st == 0).all()
+    nbytes = int(poff[-1].item())
+    w2, woff, ioff, status, cnt = codec.split_packed_stream(packed, tot + 16, n + 1, nbytes=nbytes)
+    codec.sync()
+    assert int(cnt.item()) == n and int(status[n].item()) == P.OK
+    assert torch.equal(woff[:n + 1], off) and torch.equal(ioff[:n + 1], poff)
+    assert torch.equal(w2[:tot], words[:tot])
+
+
 def test_split_guess_off_chain(codec, oracle):
     """Messages whose words look like segment tables (valid one-segment headers at record heads)
     everywhere, so the guesses of the blocks land off the chain: the resolve walks those blocks
