@@ -48,6 +48,13 @@ CONFIGS = {
                workload="C3: 1 Mi x 4 KiB flat-struct messages (tag-byte dominated)"),
     "c4": dict(nmsgs=256, nseg=16, seg_words=524288, profile="pointer",
                workload="C4: 256 x 64 MiB pointer-heavy messages, 16 segments each"),
+    # C4's shape with SURVEY 8(d)'s zero-stretch distribution (geometric, mean 300 words;
+    # capnproto_amd/workloads.py) instead of the generator's 264-336-word stretches: an extra
+    # line, not a headline config (no manifest: its packed bytes are checked against the oracle
+    # in tests/test_gpu_configs.py, the round trip here)
+    "c4g": dict(nmsgs=256, nseg=16, seg_words=524288, profile="pointer", stretches="geometric",
+                workload="C4g: 256 x 64 MiB pointer-heavy messages, 16 segments each, "
+                         "geometric zero stretches (mean 300 words)"),
     "c5": dict(nmsgs=(32 << 20) // 8, nseg=1, seg_words=0, profile="mixed", shard="round_robin",
                workload="C5: 32 Mi mixed-size messages (64 B-16 KiB), round-robin, 4 Mi per GPU"),
 }
@@ -291,6 +298,8 @@ def manifest_entry(name, cfg, seed, first, stride, n):
     p = os.path.join(ROOT, "tests", "golden", "manifest.json")
     if not os.path.exists(p):
         return None
+    if cfg.get("stretches"):  # reshaped input: no manifest describes it
+        return None
     man = json.load(open(p)).get("configs", {})
     for c in man.values():
         if (c["seed"], c["first_msg"], c["msg_stride"], c["nmsgs"], c["profile"], c["nseg"],
@@ -325,6 +334,11 @@ def run_config(name, args, steps, warmup, rank, world, dist, codec):
                                    seed=args.seed, first_msg=first, msg_stride=stride)
     words = codec.gen_messages(cfg["profile"], off, total, nseg=cfg["nseg"], seed=args.seed,
                                first_msg=first, msg_stride=stride)
+    if cfg.get("stretches") == "geometric":
+        from capnproto_amd.workloads import geometric_stretches
+
+        geometric_stretches(words, off, cfg["nseg"], seed=args.seed, first_msg=first,
+                            msg_stride=stride)
     cap = codec.packed_bound(total, n * (cfg["nseg"] + 1)) + 64
     packed = torch.empty(cap, dtype=torch.uint8, device=codec.device)
     moff = torch.empty(n + 1, dtype=torch.int64, device=codec.device)
@@ -581,7 +595,10 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic (deterministic on-device generator, SURVEY.md 8(d))",
+            "data": ("synthetic (deterministic on-device generator, SURVEY.md 8(d))"
+                     if not CONFIGS[args.config].get("stretches") else
+                     "synthetic (on-device generator, segment bodies rewritten with geometric "
+                     "zero stretches by capnproto_amd/workloads.py, seeded per message)"),
             "config": s["config"],
             "parity": s["parity"] + ("; CPU codec packed bytes == device on its sample"
                                      if cb else ""),
@@ -661,6 +678,10 @@ def batch_exchange(codec, head, args, rank, world, dist, reps=3):
         goff, gtot = codec.gen_offsets(nglob, nseg=cfg["nseg"], seg_words=cfg["seg_words"],
                                        seed=args.seed)
         gw = codec.gen_messages(cfg["profile"], goff, gtot, nseg=cfg["nseg"], seed=args.seed)
+        if cfg.get("stretches") == "geometric":
+            from capnproto_amd.workloads import geometric_stretches
+
+            geometric_stretches(gw, goff, cfg["nseg"], seed=args.seed)
         ok = torch.equal(woff, goff) and torch.equal(back[:gtot], gw[:gtot])
         del gw, goff
     res["round_trip_exact"] = ok

@@ -152,3 +152,40 @@ def test_c4_traversal_limit_edges(codec):
                                           traversal_limit_words=limit)
         codec.sync()
         assert ust.cpu().numpy().tolist() == [want] * n, limit
+
+
+@pytest.mark.slow
+def test_c4_geometric_stretches_match_oracle(codec):
+    """C4's shape with SURVEY 8(d)'s geometric zero stretches (mean 300 words; the bench's
+    `c4g` line, capnproto_amd/workloads.py): stretches far shorter and far longer than the
+    generator's 264-336 words, most crossing the 256-word run cap.  No manifest describes these
+    words, so the device's packed bytes and offsets for the whole 16 GiB batch are compared with
+    the oracle's on a host copy, and the round trip is exact."""
+    import torch
+
+    from capnproto_amd.workloads import geometric_stretches, zero_stretches
+
+    c = MAN["c4"]
+    n = c["nmsgs"]
+    off, total = codec.gen_offsets(n, nseg=c["nseg"], seg_words=c["seg_words"], seed=c["seed"])
+    words = codec.gen_messages(c["profile"], off, total, nseg=c["nseg"], seed=c["seed"])
+    geometric_stretches(words, off, c["nseg"], seed=c["seed"])
+    packed, moff, st = codec.pack_messages(words, off)
+    codec.sync()
+    assert int((st != 0).sum().item()) == 0
+    Pb = int(moff[-1].item())
+    hw = host_u64(words[:total])
+    zs = zero_stretches(hw[9 : 9 + (8 << 20)])  # message 0's body
+    assert 280 < zs.mean() < 320 and (zs < 264).mean() > 0.4 and (zs > 336).mean() > 0.25
+    ref, roff, rst = P.Oracle().pack_batch(hw, off.cpu().numpy().view(np.uint64))
+    assert (rst == 0).all() and len(ref) == Pb
+    assert (moff.cpu().numpy().view(np.uint64) == roff).all()
+    assert np.array_equal(packed[:Pb].cpu().numpy(), ref), "packed bytes != oracle"
+    del ref, hw
+    back, woff, ust = codec.unpack_messages(packed, moff, total, nbytes=Pb)
+    codec.sync()
+    assert int((ust != 0).sum().item()) == 0
+    assert bool((woff == off).all().item())
+    assert torch.equal(back[:total], words[:total])
+    del words, back
+    torch.cuda.empty_cache()
