@@ -14,14 +14,15 @@ import sys
 from collections import defaultdict
 
 out_dir, tag, cfg = sys.argv[1], sys.argv[2], sys.argv[3]
+# the kernels of the timed step (pack + unpack); the generator's size scan and fills
+# (scan_kernel, fill_kernel, gen_kernel: the bench's input setup) and torch's kernels are not
 KERNELS = {"unpack_tiles_kernel": "unpack_tiles", "header_kernel": "unpack_header",
-           "message_bits_kernel": "pack_framing", "chunk_bits_kernel": "pack_framing",
-           "scan_kernel": "scan", "fill_kernel": "fill"}
+           "message_bits_kernel": "pack_framing", "chunk_bits_kernel": "pack_framing"}
 
 
 def short(name):
-    if "cpk::" not in name:  # torch's own kernels (the bench's checks, input shaping) are not
-        return None          # the codec's, whatever their names share with it
+    if "cpk::" not in name:
+        return None
     if "pack_tile_kernel" in name:
         return "pack_tile"
     if "pack_place_kernel" in name:
