@@ -1,3 +1,8 @@
+#!/bin/bash
+# Round-4 A/B of a raw-run variant (CPK_RUN_SPLIT, measured and not kept: DESIGN.md section 4):
+# GPU tests on capnproto_amd/var_rs.so, the C5 FETCH ablation on it and on the base library, and
+# kernel times for both.  The variant's source change is not in the tree; var_rs.so was built
+# from it with tools/build_variant.sh rs "-DCPK_RUN_SPLIT=1".
 set -o pipefail
 mkdir -p gpurun_out
 cp capnproto_amd/libcpk_hip.so /tmp/base.so
