@@ -1384,256 +1384,192 @@ __device__ uint64_t lookback_flat_scan(const UnpackArgs& a, uint64_t t, uint32_t
   }
 }
 
-// Expansion of a tile's records given its true record-start masks (lane = sub-tile) and excl,
-// the words of the tile's first message before the tile: one lane per record, 64 consecutive
-// records at a time, coalesced stores; zero and raw runs written by the wave.  Records that end
-// or break a message go through handle_record, the reference's checks in the reference's order.
-template <bool PLAIN>
-__device__ __forceinline__ void expand_records(const UnpackArgs& a, uint64_t A, const uint8_t* d,
-                                               uint64_t* aux, const uint64_t* dep_tab,
-                                               uint32_t lut, uint64_t tm, uint64_t excl,
-                                               MsgWin& win, uint64_t mfirst, uint64_t mlast,
-                                               uint64_t msw, uint64_t w_tile) {
+// General expansion (any batch the lean path below does not take: modes 1 and 2, messages beyond
+// the 64-entry window, rejected headers, output too small, empty messages): one lane per record,
+// record positions by binary search over the lane masks, each record's message from the window,
+// every record through handle_record (the reference's checks in the reference's order).  Kept out
+// of line: its registers are not the lean path's.
+__device__ __forceinline__ void expand_general(uint64_t A, const uint8_t* d,
+                                                         uint32_t lut, uint64_t tm, uint64_t excl,
+                                                         MsgWin win, uint64_t mfirst,
+                                                         uint64_t msw) {
+  const UnpackArgs& a = kua();  // (the kernel's arguments stay in the kernarg segment)
   const int l = lane_id();
-  uint16_t* list = (uint16_t*)aux;
-  // Fast expansion when every message touching the tile is in the window, has a valid header,
-  // fits the output, and no two messages start at the same byte.
-  bool fast = a.mode == 0 && mlast - (mfirst - 1) <= 63 && a.word_off && a.words;
-  if (fast) {
-    const int64_t m = win.mw + l;
-    const bool inrange = m >= 0 && (uint64_t)m < mlast;
-    const bool bad = inrange && (!win.ok || win.base + win.total > a.words_capacity);
-    const uint64_t nxs = shfl64(win.start, l < 63 ? l + 1 : 63);
-    const bool dup = inrange && l < 63 && (uint64_t)(m + 1) < mlast && nxs == win.start;
-    fast = ballot(bad || dup) == 0;
-  }
   const uint32_t cnt_all = __popcll(tm);
   const uint32_t Rall_incl = wave_incl_sum32(cnt_all);
   const uint32_t nrec = readlane32(Rall_incl, 63);
-  {
-    // list capacity per quarter tile (records shorter than 2 bytes exist only where message
-    // starts clip them)
-    const uint32_t q1 = readlane32(Rall_incl, 15), q2 = readlane32(Rall_incl, 31),
-                   q3 = readlane32(Rall_incl, 47);
-    constexpr uint32_t kList = kB / 8;
-    if (q1 > kList || q2 - q1 > kList || q3 - q2 > kList || nrec - q3 > kList) fast = false;
-  }
-  if (!fast) {
-    // general path: one lane per record, record positions by binary search, message of each
-    // record from the window (see handle_record for the reference checks)
-    const uint32_t R = Rall_incl - cnt_all;
-    int64_t mcur = (int64_t)mfirst - 1;
-    uint64_t nxt_start = readlane64(win.start, 1);
-    uint64_t sum = 0;
-    uint32_t base_key = 0;
-    for (uint32_t b0 = 0; b0 < nrec; b0 += 64) {
-      const uint32_t r = b0 + l;
-      const bool act = r < nrec;
-      const uint32_t rq = act ? r : 0;
-      // record position: lane j holding record r, then the (r - R_j)-th set bit of its mask
-      int j = 0;
+  const uint32_t R = Rall_incl - cnt_all;
+  int64_t mcur = (int64_t)mfirst - 1;
+  uint64_t nxt_start = readlane64(win.start, 1);
+  uint64_t sum = 0;
+  uint32_t base_key = 0;
+  for (uint32_t b0 = 0; b0 < nrec; b0 += 64) {
+    const uint32_t r = b0 + l;
+    const bool act = r < nrec;
+    const uint32_t rq = act ? r : 0;
+    // record position: lane j holding record r, then the (r - R_j)-th set bit of its mask
+    int j = 0;
 #pragma unroll
-      for (int step = 32; step >= 1; step >>= 1) {
-        const int c = j + step;
-        const uint32_t Rc = shfl32(R, c <= 63 ? c : 63);
-        if (c <= 63 && Rc <= rq) j = c;
-      }
-      const uint32_t Rj = shfl32(R, j);
-      uint64_t mj = shfl64(tm, j);
-      int k = (int)(rq - Rj), pos = 0;
-#pragma unroll
-      for (int w = 32; w >= 1; w >>= 1) {
-        const uint64_t low = mj & ((1ull << w) - 1);
-        const int c = __popcll(low);
-        if (k >= c) {
-          k -= c;
-          mj >>= w;
-          pos += w;
-        } else {
-          mj = low;
-        }
-      }
-      const int p = act ? 64 * j + pos : 0;
-      const uint64_t pabs = A + p;
-      const Rec rc = read_rec(d, p);
-      const uint32_t w = act ? 1 + rc.cnt : 0;
-      // every lane takes part in the shuffle (an inactive source lane would read as 0)
-      const uint64_t msrc = shfl64(msw, p >> 6);
-      const bool is_ms = act && ((msrc >> (p & 63)) & 1);
-      const uint32_t inc = wave_incl_sum32(w);
-      const uint64_t Sx = sum + inc - w;
-      const uint32_t key = is_ms ? (uint32_t)(Sx + 1) : 0;
-      uint32_t km = wave_incl_max32(key);
-      if (km < base_key) km = base_key;
-      const uint64_t wb = km ? Sx - (km - 1) : excl + Sx;
-      const uint32_t lastl = (nrec - b0 < 64 ? nrec - b0 : 64) - 1;
-      const uint64_t maxp = readlane64(pabs, (int)lastl);
-      int64_t m = mcur;
-      if (maxp >= nxt_start) {
-        bool found = false;
-        for (;;) {
-          int c = 0;
-#pragma unroll
-          for (int step = 32; step >= 1; step >>= 1) {
-            const uint64_t probe = shfl64(win.start, c + step <= 63 ? c + step : 63);
-            if (c + step <= 63 && probe <= pabs) c += step;
-          }
-          const bool beyond = act && c == 63 && readlane64(win.start, 63) <= pabs;
-          if (!found && !beyond) m = win.mw + c;
-          found = found || !beyond;
-          if (!ballot(beyond)) break;
-          load_win(a, win.mw + 63, win);
-        }
-        mcur = (int64_t)readlane64((uint64_t)m, (int)lastl);
-        if (mcur - win.mw >= 63) load_win(a, mcur, win);
-        nxt_start = readlane64(win.start, (int)(mcur - win.mw) + 1);
-      }
-      const int64_t wl64 = m - win.mw;
-      const bool inwin = wl64 >= 0 && wl64 < 64;
-      const int wl = inwin ? (int)wl64 : 0;
-      MsgInfo mi;
-      mi.base = shfl64(win.base, wl);
-      mi.total = shfl64(win.total, wl);
-      mi.end = shfl64(win.end, wl);
-      mi.ok = shfl32(win.ok, wl) != 0;
-      if (!inwin && act && m >= 0 && (uint64_t)m < a.nmsgs) mi = msg_info(a, (uint64_t)m);
-      mi.fits = a.word_off ? (mi.base + mi.total <= a.words_capacity) : false;
-      const uint64_t word = expand_word(d, p, rc.tag, lut);
-      RunJob job;
-      job.n = 0;
-      if (act && m >= 0 && (uint64_t)m < a.nmsgs) {
-        const int32_t st = handle_record(a, d, p, pabs, wb, mi, &job, word);
-        if (a.mode == 2) {
-          if (mi.ok) {
-            if (st == kInvalid) {
-              a.status[m] = kInvalid;
-              a.size_out[m] = 0;
-            } else if (st == kSizeDone) {
-              a.status[m] = kOK;
-              a.size_out[m] = wb + 1 + (rc.run ? rc.cnt : 0);
-            }
-          }
-        } else if (st >= 0) {
-          a.status[m] = st;
-          report_end(a, (uint64_t)m, st, job);
-        }
-      }
-      run_jobs_batch(a, job, d, A, (uint32_t)(kB + kPad));
-      base_key = readlane32(km, 63);
-      sum += readlane32(inc, 63);
+    for (int step = 32; step >= 1; step >>= 1) {
+      const int c = j + step;
+      const uint32_t Rc = shfl32(R, c <= 63 ? c : 63);
+      if (c <= 63 && Rc <= rq) j = c;
     }
-    return;
-  }
-  // plain tiles (most tiles of large messages): no message start in the tile, and no record can
-  // reach the end of its message, by words or by bytes (a record reaches at most 2050 bytes past
-  // the tile) -- no per-record message logic at all
-  if constexpr (PLAIN) {
-  const uint64_t cbase0 = readlane64(win.base, 0), ctotal0 = readlane64(win.total, 0);
-  const uint64_t cend0 = readlane64(win.end, 0);
-  if (fast && !a.rec_pos && w_tile != ~0ull && ballot(msw != 0) == 0 && excl + w_tile < ctotal0 &&
-      cend0 > A + kB + 2064 && !(a.debug_skip & 32)) {
-    uint64_t* const wp0 = a.words + cbase0 + excl;
-    uint32_t sum = 0;  // words of the tile's records so far
-    for (int h = 0; h < 4; h++) {
-      const int src = 16 * h + (l >> 2);
-      const uint32_t sh = 16u * ((uint32_t)l & 3);
-      uint32_t bits = (uint32_t)(shfl64(tm, src) >> sh) & 0xffffu;
-      const uint32_t c = __popc(bits);
-      const uint32_t Rin = wave_incl_sum32(c);
-      const uint32_t nh = readlane32(Rin, 63);
-      uint32_t r = Rin - c;
-      const uint32_t pbase = 64u * (uint32_t)src + sh;
-      while (bits) {
-        const uint32_t b = (uint32_t)__builtin_ctz(bits);
-        bits &= bits - 1;
-        list[r++] = (uint16_t)(pbase + b);
+    const uint32_t Rj = shfl32(R, j);
+    uint64_t mj = shfl64(tm, j);
+    int k = (int)(rq - Rj), pos = 0;
+#pragma unroll
+    for (int w = 32; w >= 1; w >>= 1) {
+      const uint64_t low = mj & ((1ull << w) - 1);
+      const int c = __popcll(low);
+      if (k >= c) {
+        k -= c;
+        mj >>= w;
+        pos += w;
+      } else {
+        mj = low;
       }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#if CPK_PIPE
-      // the next batch's record bytes are read while this batch computes (two dependent LDS
-      // round trips per batch off the critical path)
-      const uint32_t nhe = (a.debug_skip & 16) ? 0u : nh;
-      int pn = nhe ? (int)list[(uint32_t)l < nh ? (uint32_t)l : nh - 1] : 0;
-      uint32_t n0 = 0, n1 = 0, n2 = 0, n3 = 0;
-      if (nhe) {
-        const uint32_t* dwn = (const uint32_t*)(d + (pn & ~3));
-        n0 = dwn[0];
-        n1 = dwn[1];
-        n2 = dwn[2];
-        n3 = dwn[3];
-      }
-      for (uint32_t b0 = 0; b0 < nhe; b0 += 64) {
-        const uint32_t rr = b0 + l;
-        const bool act = rr < nh;
-        const int p = pn;
-        const uint32_t sh2 = (uint32_t)p & 3;
-        const uint32_t q0 = n0, q1 = n1, q2 = n2, q3 = n3;
-        if (b0 + 64 < nh) {
-          const uint32_t rn = b0 + 64 + l;
-          pn = (int)list[rn < nh ? rn : nh - 1];
-          const uint32_t* dwn = (const uint32_t*)(d + (pn & ~3));
-          n0 = dwn[0];
-          n1 = dwn[1];
-          n2 = dwn[2];
-          n3 = dwn[3];
-        }
-#else
-      for (uint32_t b0 = 0; b0 < ((a.debug_skip & 16) ? 0u : nh); b0 += 64) {
-        const uint32_t rr = b0 + l;
-        const bool act = rr < nh;
-        const int p = (int)list[rr < nh ? rr : nh - 1];
-        const uint32_t* dw = (const uint32_t*)(d + (p & ~3));
-        const uint32_t sh2 = (uint32_t)p & 3;
-        const uint32_t q0 = dw[0], q1 = dw[1], q2 = dw[2], q3 = dw[3];
-#endif
-        const uint32_t b0w = __builtin_amdgcn_alignbyte(q1, q0, sh2);  // bytes p .. p+3
-        const uint32_t b1w = __builtin_amdgcn_alignbyte(q2, q1, sh2);  // p+4 .. p+7
-        const uint32_t b2w = __builtin_amdgcn_alignbyte(q3, q2, sh2);  // p+8 .. p+11
-        const uint32_t tag = b0w & 0xff;
-        const uint32_t dlo = __builtin_amdgcn_alignbyte(b1w, b0w, 1);  // data bytes 0..3
-        const uint32_t dhi = __builtin_amdgcn_alignbyte(b2w, b1w, 1);  // data bytes 4..7
-        const bool z = tag == 0, f = tag == 0xff;
-        uint32_t cnt = z ? (b0w >> 8) & 0xff : 0u;
-        cnt = f ? (b2w >> 8) & 0xff : cnt;
-        const uint32_t w = act ? 1 + cnt : 0;
-        const uint32_t inc = wave_incl_sum32(w);
-        const uint32_t o = sum + inc - w;  // words of the tile before the record
-        const uint64_t sel = dep_tab[tag];
-        const uint32_t wlo = __builtin_amdgcn_perm(dhi, dlo, (uint32_t)sel);
-        const uint32_t whi = __builtin_amdgcn_perm(dhi, dlo, (uint32_t)(sel >> 32));
-        if (act) wp0[o] = ((uint64_t)whi << 32) | wlo;
-        RunJob job;
-        job.n = act ? cnt : 0u;
-        job.dst = cbase0 + excl + o + 1;
-        job.raw = f;
-        job.src = A + (uint32_t)p + 10;
-        run_jobs_batch(a, job, d, A, (uint32_t)(kB + kPad));
-        sum += readlane32(inc, 63);
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
-    return;
+    const int p = act ? 64 * j + pos : 0;
+    const uint64_t pabs = A + p;
+    const Rec rc = read_rec(d, p);
+    const uint32_t w = act ? 1 + rc.cnt : 0;
+    // every lane takes part in the shuffle (an inactive source lane would read as 0)
+    const uint64_t msrc = shfl64(msw, p >> 6);
+    const bool is_ms = act && ((msrc >> (p & 63)) & 1);
+    const uint32_t inc = wave_incl_sum32(w);
+    const uint64_t Sx = sum + inc - w;
+    const uint32_t key = is_ms ? (uint32_t)(Sx + 1) : 0;
+    uint32_t km = wave_incl_max32(key);
+    if (km < base_key) km = base_key;
+    const uint64_t wb = km ? Sx - (km - 1) : excl + Sx;
+    const uint32_t lastl = (nrec - b0 < 64 ? nrec - b0 : 64) - 1;
+    const uint64_t maxp = readlane64(pabs, (int)lastl);
+    int64_t m = mcur;
+    if (maxp >= nxt_start) {
+      bool found = false;
+      for (;;) {
+        int c = 0;
+#pragma unroll
+        for (int step = 32; step >= 1; step >>= 1) {
+          const uint64_t probe = shfl64(win.start, c + step <= 63 ? c + step : 63);
+          if (c + step <= 63 && probe <= pabs) c += step;
+        }
+        const bool beyond = act && c == 63 && readlane64(win.start, 63) <= pabs;
+        if (!found && !beyond) m = win.mw + c;
+        found = found || !beyond;
+        if (!ballot(beyond)) break;
+        load_win(a, win.mw + 63, win);
+      }
+      mcur = (int64_t)readlane64((uint64_t)m, (int)lastl);
+      if (mcur - win.mw >= 63) load_win(a, mcur, win);
+      nxt_start = readlane64(win.start, (int)(mcur - win.mw) + 1);
+    }
+    const int64_t wl64 = m - win.mw;
+    const bool inwin = wl64 >= 0 && wl64 < 64;
+    const int wl = inwin ? (int)wl64 : 0;
+    MsgInfo mi;
+    mi.base = shfl64(win.base, wl);
+    mi.total = shfl64(win.total, wl);
+    mi.end = shfl64(win.end, wl);
+    mi.ok = shfl32(win.ok, wl) != 0;
+    if (!inwin && act && m >= 0 && (uint64_t)m < a.nmsgs) mi = msg_info(a, (uint64_t)m);
+    mi.fits = a.word_off ? (mi.base + mi.total <= a.words_capacity) : false;
+    const uint64_t word = expand_word(d, p, rc.tag, lut);
+    RunJob job;
+    job.n = 0;
+    if (act && m >= 0 && (uint64_t)m < a.nmsgs) {
+      const int32_t st = handle_record(a, d, p, pabs, wb, mi, &job, word);
+      if (a.mode == 2) {
+        if (mi.ok) {
+          if (st == kInvalid) {
+            a.status[m] = kInvalid;
+            a.size_out[m] = 0;
+          } else if (st == kSizeDone) {
+            a.status[m] = kOK;
+            a.size_out[m] = wb + 1 + (rc.run ? rc.cnt : 0);
+          }
+        }
+      } else if (st >= 0) {
+        a.status[m] = st;
+        report_end(a, (uint64_t)m, st, job);
+      }
+    }
+    run_jobs_batch(a, job, d, A, (uint32_t)(kB + kPad));
+    base_key = readlane32(km, 63);
+    sum += readlane32(inc, 63);
   }
+}
+
+// A record that ends or breaks its message in the lean expansion: the reference's checks
+// (handle_record), its status and end, and its run (out of line: rare).
+__device__ __forceinline__ void lean_special(const uint8_t* d, int p, uint64_t A,
+                                                       uint64_t wb, uint64_t mbase,
+                                                       uint64_t mtotal, uint64_t mend, int64_t m,
+                                                       uint64_t word, bool act) {
+  const UnpackArgs& a = kua();
+  RunJob job;
+  job.n = 0;
+  if (act) {
+    MsgInfo mi;
+    mi.base = mbase;
+    mi.total = mtotal;
+    mi.end = mend;
+    mi.ok = true;
+    mi.fits = true;
+    const int32_t st = handle_record(a, d, p, A + (uint32_t)p, wb, mi, &job, word);
+    if (st >= 0) {
+      kua().status[m] = st;
+      report_end(a, (uint64_t)m, st, job);
+    }
   }
-  // fast path: record list per quarter tile (lanes 16h .. 16h+15), 64 records per batch
-  uint64_t sum = 0;        // words of the tile's records so far
-  uint32_t base_key = 0;   // key of the latest message start so far (key-max reset)
-  uint32_t mcount = 0;     // message starts so far
-  // the current message (window lane mcount): batches without a message start use it as is
-  uint64_t cbase = readlane64(win.base, 0), ctotal = readlane64(win.total, 0);
+  run_jobs(a, job, d, A, (uint32_t)(kB + kPad));
+}
+
+// Lean expansion (mode 0; every message touching the tile in the window, accepted, fitting the
+// output; no empty message in the tile; at most kB/8 records per quarter tile).  Record lists
+// per quarter tile in LDS, one lane per record, 64 consecutive records per batch, coalesced
+// 8-byte stores.  Tile-relative 32-bit arithmetic; the current message's word pointer is
+// wave-uniform.  A batch with no message start whose records cannot reach the message's end --
+// by words or by bytes (a record is at most 2050 bytes): one uniform check -- runs with no
+// per-record message logic; the records of other batches find their message by the start bits
+// and a max-scan, and those that end or break their message go through handle_record.
+// Zero and raw runs of at most kShortRun words from the staged bytes are written by their own
+// lane (most runs of dense data), longer ones by the whole wave.
+constexpr uint32_t kShortRun = 4;
+__device__ __forceinline__ void expand_lean(const UnpackArgs& a, uint64_t A, const uint8_t* d,
+                                            uint64_t* aux, const uint64_t* dep_tab, uint64_t tm,
+                                            uint64_t excl, const MsgWin& win, uint64_t msw) {
+  const int l = lane_id();
+  const bool starts = ballot(msw != 0) != 0;
+  // 16 record-start (and message-start) bits per lane and quarter: u16 number 64h + l of the
+  // sub-tile masks is bits [16(l % 4), +16) of sub-tile 16h + l/4, i.e. tile bytes 1024h + 16l..
+  aux[l] = tm;
+  aux[64 + l] = msw;
+  lane_handoff();
+  // (two quarters per register: an array indexed by the quarter would live in scratch)
+  const uint16_t* const a16 = (const uint16_t*)aux;
+  const uint32_t tq01 = a16[l] | ((uint32_t)a16[64 + l] << 16);
+  const uint32_t tq23 = a16[128 + l] | ((uint32_t)a16[192 + l] << 16);
+  const uint32_t mq01 = a16[256 + l] | ((uint32_t)a16[320 + l] << 16);
+  const uint32_t mq23 = a16[384 + l] | ((uint32_t)a16[448 + l] << 16);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (the lists overwrite aux)
+  uint16_t* const list = (uint16_t*)aux;
+  uint32_t mcount = 0;  // message starts so far
+  // the current message (window lane mcount) and its words before the next batch
+  uint64_t cbase = readlane64(win.base, 0), ctot = readlane64(win.total, 0);
   uint64_t cend = readlane64(win.end, 0);
+  uint64_t mw0 = excl;
+  const uint32_t* const d32 = (const uint32_t*)d;
   for (int h = 0; h < ((a.debug_skip & 32) ? 0 : 4); h++) {
-    // lane l takes bits [16(l%4), +16) of sub-tile 16h + l/4: four lanes per sub-tile keep the
-    // serial bit loop about four times shorter than one lane per sub-tile would
-    const int src = 16 * h + (l >> 2);
-    const uint32_t sh = 16u * ((uint32_t)l & 3);
-    uint32_t bits = (uint32_t)(shfl64(tm, src) >> sh) & 0xffffu;
-    const uint32_t msp = (uint32_t)(shfl64(msw, src) >> sh) & 0xffffu;
+    const uint32_t hs = 16u * ((uint32_t)h & 1u);
+    uint32_t bits = ((h < 2 ? tq01 : tq23) >> hs) & 0xffffu;
+    const uint32_t msp = starts ? ((h < 2 ? mq01 : mq23) >> hs) & 0xffffu : 0u;
     const uint32_t c = __popc(bits);
     const uint32_t Rin = wave_incl_sum32(c);
     const uint32_t nh = readlane32(Rin, 63);
     uint32_t r = Rin - c;
-    const uint32_t pbase = 64u * (uint32_t)src + sh;
+    const uint32_t pbase = 1024u * (uint32_t)h + 16u * (uint32_t)l;
     while (bits) {
       const uint32_t b = (uint32_t)__builtin_ctz(bits);
       bits &= bits - 1;
@@ -1643,117 +1579,168 @@ __device__ __forceinline__ void expand_records(const UnpackArgs& a, uint64_t A, 
     for (uint32_t b0 = 0; b0 < ((a.debug_skip & 16) ? 0u : nh); b0 += 64) {
       const uint32_t rr = b0 + l;
       const bool act = rr < nh;
-      // branch-free body: an inactive lane reads a real entry (LDS stays in bounds) and is
-      // masked by selects, so the batch runs without exec-mask splits
-      const uint32_t e0 = list[rr < nh ? rr : nh - 1];
-      const uint32_t e = act ? e0 : 0u;
-      const int p = (int)(e & 0xfff);
-      const bool is_ms = (e >> 12) & 1;
+      // branch-free body: an inactive lane reads the last entry again (LDS stays in bounds) and
+      // is masked by selects
+      const uint32_t e = list[act ? rr : nh - 1];
+      const uint32_t p = e & 0xfffu;
+      const bool is_ms = act && (e & 0x1000u);
       // bytes p .. p + 12: tag, up to 8 data bytes, count byte
-      const uint32_t* dw = (const uint32_t*)(d + (p & ~3));
-      const uint32_t sh = (uint32_t)p & 3;
-      const uint32_t q0 = dw[0], q1 = dw[1], q2 = dw[2], q3 = dw[3];
+      const uint32_t q = p >> 2, sh = p & 3u;
+      const uint32_t q0 = d32[q], q1 = d32[q + 1], q2 = d32[q + 2], q3 = d32[q + 3];
       const uint32_t b0w = __builtin_amdgcn_alignbyte(q1, q0, sh);  // bytes p .. p+3
       const uint32_t b1w = __builtin_amdgcn_alignbyte(q2, q1, sh);  // p+4 .. p+7
       const uint32_t b2w = __builtin_amdgcn_alignbyte(q3, q2, sh);  // p+8 .. p+11
-      const uint32_t tag = b0w & 0xff;
+      const uint32_t tag = b0w & 0xffu;
+      const uint64_t sel = dep_tab[tag];
       const uint32_t dlo = __builtin_amdgcn_alignbyte(b1w, b0w, 1);  // data bytes 0..3
       const uint32_t dhi = __builtin_amdgcn_alignbyte(b2w, b1w, 1);  // data bytes 4..7
-      const uint32_t nz = __popc(tag);
-      const bool z = tag == 0, f = tag == 0xff;
-      const uint32_t c1 = (b0w >> 8) & 0xff, c9 = (b2w >> 8) & 0xff;
-      uint32_t cnt = z ? c1 : 0u;
-      cnt = f ? c9 : cnt;
-      cnt = act ? cnt : 0u;
-      const uint32_t w = act ? 1 + cnt : 0;
+      const bool z = tag == 0, f = tag == 0xffu;
+      uint32_t cnt = z ? ((b0w >> 8) & 0xffu) : 0u;
+      cnt = f ? ((b2w >> 8) & 0xffu) : cnt;
+      const uint32_t w = act ? 1u + cnt : 0u;
       const uint32_t inc = wave_incl_sum32(w);
       const uint32_t o = inc - w;  // words of the batch before the record
+      const uint32_t btot = readlane32(inc, 63);
       const uint64_t msb = ballot(is_ms);
-      const uint64_t sel = dep_tab[tag];
       const uint32_t wlo = __builtin_amdgcn_perm(dhi, dlo, (uint32_t)sel);
       const uint32_t whi = __builtin_amdgcn_perm(dhi, dlo, (uint32_t)(sel >> 32));
       const uint64_t word = ((uint64_t)whi << 32) | wlo;
-      const uint32_t len = 1 + nz + (uint32_t)(z | f) + (f ? 8 * cnt : 0u);
-      RunJob job;
-      job.n = 0;
-      uint32_t km;
-      int wl;  // window lane of the record's message
-      uint64_t mbase, mtotal, mend, wb;
-      bool special;  // records that end a message (or break it) go through the reference checks
+      uint64_t* wp;  // the record's word
+      bool special = false;
+      int wl = (int)mcount;
+      uint64_t wb = 0;
+      uint32_t kml = 0;
       if (msb == 0) {
-        // the batch continues the current message: wave-uniform base, 32-bit lane arithmetic
-        km = base_key;
-        wl = (int)mcount;
-        mbase = cbase;
-        mtotal = ctotal;
-        mend = cend;
-        const uint64_t sb = km ? sum - (km - 1) : excl + sum;  // message words before the batch
-        const uint64_t r1 = ctotal > sb ? ctotal - sb : 0;
-        const uint64_t r2 = cend > A ? cend - A : 0;
-        const uint32_t lim1 = r1 > 0xffffffffull ? 0xffffffffu : (uint32_t)r1;
-        const uint32_t lim2 = r2 > 0xffffffffull ? 0xffffffffu : (uint32_t)r2;
-        special = act && (inc >= lim1 || (uint32_t)p + len >= lim2);
-        wb = sb + o;
-        if (act && !special) {
-          uint64_t* const wp = a.words + (cbase + sb);
-          wp[o] = word;
-          if (a.rec_pos) a.rec_pos[cbase + sb + o] = A + (uint32_t)p;
-          if (cnt) {
-            job.n = cnt;
-            job.dst = cbase + sb + o + 1;
-            job.raw = f;
-            job.src = A + (uint32_t)p + 10;
-          }
+        // the batch continues the current message: a uniform word pointer
+        wp = a.words + (cbase + mw0) + o;
+        const uint32_t maxp = readlane32(p, 63);  // (inactive lanes repeat the last record)
+        if (mw0 + btot >= ctot || A + maxp + 2050 >= cend) {
+          const uint32_t len = 1u + __popc(tag) + ((z || f) ? 1u : 0u) + (f ? 8u * cnt : 0u);
+          wb = mw0 + o;
+          special = act && (wb + w >= ctot || A + p + len >= cend);
         }
       } else {
-        const uint64_t Sx = sum + o;
-        const uint32_t key = is_ms ? (uint32_t)(Sx + 1) : 0;
-        km = wave_incl_max32(key);
-        if (km < base_key) km = base_key;
+        // message starts in the batch: the latest start at or before each record (key-max scan)
+        const uint32_t key = is_ms ? o + 1u : 0u;
+        const uint32_t km = wave_incl_max32(key);
+        kml = readlane32(km, 63);
         wl = (int)(mcount + (uint32_t)__popcll(msb & mask_le(l)));
-        mbase = shfl64(win.base, wl);
-        mtotal = shfl64(win.total, wl);
-        mend = shfl64(win.end, wl);
-        wb = km ? Sx - (km - 1) : excl + Sx;
-        special = act && (wb + w >= mtotal || A + p + len >= mend);
-        if (act && !special) {
-          a.words[mbase + wb] = word;
-          if (a.rec_pos) a.rec_pos[mbase + wb] = A + (uint32_t)p;
-          if (cnt) {
-            job.n = cnt;
-            job.dst = mbase + wb + 1;
-            job.raw = f;
-            job.src = A + p + 10;
+        const uint64_t mbase = shfl64(win.base, wl);
+        wb = km ? (uint64_t)(o - (km - 1u)) : mw0 + o;
+        wp = a.words + mbase + wb;
+        const uint64_t mtot = shfl64(win.total, wl), mend = shfl64(win.end, wl);
+        const uint32_t len = 1u + __popc(tag) + ((z || f) ? 1u : 0u) + (f ? 8u * cnt : 0u);
+        special = act && (wb + w >= mtot || A + p + len >= mend);
+      }
+      if (act && !special) {
+        *wp = word;
+        if (a.rec_pos) a.rec_pos[wp - a.words] = A + p;
+      }
+      if (ballot(special)) {
+        const uint64_t mbase = msb ? shfl64(win.base, wl) : cbase;
+        const uint64_t mtot = msb ? shfl64(win.total, wl) : ctot;
+        const uint64_t mend = msb ? shfl64(win.end, wl) : cend;
+        lean_special(d, (int)p, A, wb, mbase, mtot, mend, win.mw + wl, word, special);
+      }
+      // runs of the other records: short ones from the staged bytes by their own lane
+      const bool run = act && !special && cnt != 0;
+      if (ballot(run)) {
+        const uint32_t src = p + 10u;  // tile byte of a raw run's first word
+        const bool staged = !f || src + 8u * cnt + 4u <= (uint32_t)(kB + kPad);
+        const bool shrt = run && cnt <= kShortRun && staged;
+        const uint32_t n = shrt ? cnt : 0u;
+        for (uint32_t k = 0; k < kShortRun; k++) {
+          if (!ballot(k < n)) break;
+          if (k < n) {
+            uint64_t v = 0;
+            if (f) {
+              const uint32_t ob = src + 8u * k, qq = ob >> 2, s3 = ob & 3u;
+              const uint32_t r0 = d32[qq], r1 = d32[qq + 1], r2 = d32[qq + 2];
+              v = ((uint64_t)__builtin_amdgcn_alignbyte(r2, r1, s3) << 32) |
+                  __builtin_amdgcn_alignbyte(r1, r0, s3);
+            }
+            wp[1 + k] = v;
+          }
+        }
+        uint64_t lm = ballot(run && !shrt);
+        while (lm) {
+          const int j = lowest_bit(lm);
+          lm &= lm - 1;
+          const uint32_t nj = readlane32(cnt, j);
+          uint64_t* const dst = (uint64_t*)readlane64((uint64_t)(wp + 1), j);
+          const uint32_t sj = readlane32(src, j);
+          if (!readlane32(f ? 1u : 0u, j)) {
+            for (uint32_t k = l; k < nj; k += 64) dst[k] = 0;
+          } else if (sj + 8u * nj + 4u <= (uint32_t)(kB + kPad)) {
+            for (uint32_t k = l; k < nj; k += 64) {
+              const uint32_t ob = sj + 8u * k, qq = ob >> 2, s3 = ob & 3u;
+              const uint32_t r0 = d32[qq], r1 = d32[qq + 1], r2 = d32[qq + 2];
+              dst[k] = ((uint64_t)__builtin_amdgcn_alignbyte(r2, r1, s3) << 32) |
+                       __builtin_amdgcn_alignbyte(r1, r0, s3);
+            }
+          } else {
+            // past the staged bytes: unaligned 8-byte loads from the batch, all of a 256-word
+            // block issued before its stores (clamped indices: no load left outstanding)
+            const uint8_t* const s8 = a.packed + A + sj;
+            for (uint32_t k0 = 0; k0 < nj; k0 += 256) {
+              uint64_t v[4];
+#pragma unroll
+              for (int i = 0; i < 4; i++) {
+                const uint32_t k = k0 + 64 * i + l;
+                __builtin_memcpy(&v[i], s8 + 8ull * (k < nj ? k : nj - 1), 8);
+              }
+#pragma unroll
+              for (int i = 0; i < 4; i++) {
+                const uint32_t k = k0 + 64 * i + l;
+                dst[k < nj ? k : nj - 1] = v[i];
+              }
+            }
           }
         }
       }
-      const uint64_t pabs = A + p;
-      if (special) {
-        const int64_t m = win.mw + wl;
-        MsgInfo mi;
-        mi.base = mbase;
-        mi.total = mtotal;
-        mi.end = mend;
-        mi.ok = true;
-        mi.fits = true;
-        const int32_t st = handle_record(a, d, p, pabs, wb, mi, &job, word);
-        if (st >= 0) {
-          kua().status[m] = st;
-          report_end(a, (uint64_t)m, st, job);
-        }
-      }
-      run_jobs_batch(a, job, d, A, (uint32_t)(kB + kPad));
-      base_key = readlane32(km, 63);
-      sum += readlane32(inc, 63);
-      if (msb) {
+      if (msb == 0) {
+        mw0 += btot;
+      } else {
         mcount += (uint32_t)__popcll(msb);
+        mw0 = btot - (kml - 1u);
         cbase = readlane64(win.base, (int)mcount);
-        ctotal = readlane64(win.total, (int)mcount);
+        ctot = readlane64(win.total, (int)mcount);
         cend = readlane64(win.end, (int)mcount);
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
+}
+
+// Expansion of a tile's records given its true record-start masks (lane = sub-tile) and excl,
+// the words of the tile's first message before the tile: the lean path when the tile's window
+// allows it, else the general one.
+__device__ __forceinline__ void expand_records(const UnpackArgs& a, uint64_t A, const uint8_t* d,
+                                               uint64_t* aux, const uint64_t* dep_tab, uint64_t tm,
+                                               uint64_t excl, MsgWin& win, uint64_t mfirst,
+                                               uint64_t mlast, uint64_t msw) {
+  const int l = lane_id();
+  bool fast = a.mode == 0 && mlast - (mfirst - 1) <= 63 && a.word_off && a.words;
+  if (fast) {
+    const int64_t m = win.mw + l;
+    const bool inrange = m >= 0 && (uint64_t)m < mlast;
+    const bool bad = inrange && (!win.ok || win.base + win.total > a.words_capacity);
+    const uint64_t nxs = shfl64(win.start, l < 63 ? l + 1 : 63);
+    const bool dup = inrange && l < 63 && (uint64_t)(m + 1) < mlast && nxs == win.start;
+    fast = ballot(bad || dup) == 0;
+  }
+  if (fast) {
+    // list capacity per quarter tile (records shorter than 2 bytes exist only where message
+    // starts clip them)
+    const uint32_t cq = __popcll(tm);
+    const uint32_t Rq = wave_incl_sum32(cq);
+    const uint32_t q1 = readlane32(Rq, 15), q2 = readlane32(Rq, 31), q3 = readlane32(Rq, 47);
+    const uint32_t nrec = readlane32(Rq, 63);
+    constexpr uint32_t kList = kB / 8;
+    if (q1 > kList || q2 - q1 > kList || q3 - q2 > kList || nrec - q3 > kList) fast = false;
+  }
+  if (fast) expand_lean(a, A, d, aux, dep_tab, tm, excl, win, msw);
+  else expand_general(A, d, deposit_sel((uint32_t)l & 15), tm, excl, win, mfirst, msw);
 }
 
 #ifndef CPK_PREWALK
@@ -1762,11 +1749,9 @@ __device__ __forceinline__ void expand_records(const UnpackArgs& a, uint64_t A, 
 #ifndef CPK_UNPACK_WPE
 #define CPK_UNPACK_WPE 7  // 72 VGPRs: 7 waves per SIMD (LDS allows 7); 6 at the unconstrained 80
 #endif
-// PLAIN: the plain-tile expansion is compiled in (launched for batches of large messages only:
-// its code costs the kernel a few percent where few tiles are plain).
 // FLAT: the flat stream decode's second-candidate descriptors and look-back are compiled in (a
-// variant of its own: their registers cost the other variants spills).
-template <bool PLAIN, bool FLAT>
+// variant of its own: their registers cost the other variant spills).
+template <bool FLAT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CPK_UNPACK_WPE))) void
 unpack_tiles_kernel(UnpackArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds_data[4][kB + kPad];
@@ -1923,7 +1908,6 @@ unpack_tiles_kernel(UnpackArgs a) {
 
   // ---- the tile's entry and the words before it ------------------------------------------
   uint64_t tm = tm0, excl = 0;
-  uint64_t w_tile = ~0ull;  // words of the tile's records (tiles without a message start)
   if (t == 0 || fms == 0) {
     if (!has_start) {  // (tile 0 without a message start: bytes before the first message)
       const uint64_t w = readlane32(wave_incl_sum32(mask_words(d, st.s, tm0, runm)), 63);
@@ -1990,7 +1974,6 @@ unpack_tiles_kernel(UnpackArgs a) {
       if (!has_start) w = readlane32(wave_incl_sum32(mask_words(d, st.s, tm, runs)), 63);
     }
     if (!has_start) {
-      w_tile = w;
       if (l == 0) store_agent(a.desc + t, make_desc(kDescIncl, xE, x0, excl + w));
     }
     if (a.stamps && l == 0 && t < 1024) {  // diagnostic dump (CPK_STAMPS=1)
@@ -2004,8 +1987,7 @@ unpack_tiles_kernel(UnpackArgs a) {
   // ---- expansion -------------------------------------------------------------------------
   if (a.debug_skip & 256) return;  // diagnostic: + the entry and the look-back
   if (CPK_PRIO || a.prio) __builtin_amdgcn_s_setprio(0);
-  expand_records<PLAIN>(a, A, d, aux, dep_tab, deposit_sel((uint32_t)l & 15), tm, excl, win, mfirst,
-                 mlast, msw, w_tile);
+  expand_records(a, A, d, aux, dep_tab, tm, excl, win, mfirst, mlast, msw);
   // a fused single-tile batch: this wave is the whole call -- its error word for the host, last:
   // its stores done, then a system-scope release
   if (a.err_host) {
@@ -2080,17 +2062,11 @@ hipError_t launch_unpack_header(const uint8_t* packed, const uint64_t* in_off, u
 
 hipError_t launch_unpack_stage(int stage, const UnpackArgs& a, hipStream_t stream) {
   if (a.ntiles == 0) return hipSuccess;
-  {
-    // plain tiles are most tiles when messages span several tiles
-    const bool plain = a.word_off && a.nmsgs && a.nbytes / a.nmsgs >= 4 * (uint64_t)kB;
-    const dim3 grid((unsigned)((a.ntiles + 3) / 4));
-    if (a.desc2)
-      hipLaunchKernelGGL((unpack_tiles_kernel<true, true>), grid, dim3(256), 0, stream, a);
-    else if (plain)
-      hipLaunchKernelGGL((unpack_tiles_kernel<true, false>), grid, dim3(256), 0, stream, a);
-    else
-      hipLaunchKernelGGL((unpack_tiles_kernel<false, false>), grid, dim3(256), 0, stream, a);
-  }
+  const dim3 grid((unsigned)((a.ntiles + 3) / 4));
+  if (a.desc2)
+    hipLaunchKernelGGL((unpack_tiles_kernel<true>), grid, dim3(256), 0, stream, a);
+  else
+    hipLaunchKernelGGL((unpack_tiles_kernel<false>), grid, dim3(256), 0, stream, a);
   (void)stage;
   return hipGetLastError();
 }
