@@ -193,7 +193,13 @@ cpk_status host_io_run(cpk_ctx* ctx, const HostIo& io, size_t in_bytes, size_t o
   cpk_status st = fn(s);
   ctx->err = saved;
   ctx->err_host = nullptr;
-  if (st != CPK_OK) return st;
+  if (st != CPK_OK) {
+    // kernels of this call may still be running (reading the pinned inputs, raising the call's
+    // error word): let them finish and reset the word before the next call reuses both
+    (void)hipStreamSynchronize(s);
+    (void)hipMemset(io.derr, 0, 4);
+    return st;
+  }
   if (io.dherr) {
     // results are in place; the error word too when one launch did the call, written last (after
     // a system-scope release): spinning on it returns as soon as the kernel is done, a stream
@@ -404,19 +410,20 @@ cpk_status pack_common(cpk_ctx* ctx, const uint64_t* d_words, uint64_t N, const 
     tf.zero_words = 0;
     if (messages && n)
       return hip_status(
-          cpk::launch_message_bits(d_words, d_off, n, bits, tstarts, d_status, tf, stream));
+          cpk::launch_message_bits(d_words, d_off, n, N, bits, tstarts, d_status, tf, stream));
     return CPK_OK;
   }
   if (messages && n == 0) return CPK_ERR_INVALID_ARGUMENT;  // words outside any message
   hipError_t e = hipSuccess;
   if (!single)
-    e = messages ? cpk::launch_message_bits(d_words, d_off, n, bits, tstarts, d_status, tf, stream)
+    e = messages ? cpk::launch_message_bits(d_words, d_off, n, N, bits, tstarts, d_status, tf, stream)
                  : cpk::launch_chunk_bits(d_off, n, N, bits, tstarts, tf, stream);
   // the bitmap is zero at rest only if the tile kernel runs and clears it: after any failure
   // from here on it is cleared here
   auto clear_bits = [&]() {
-    (void)hipMemset(bits, 0, pack_bits_words(N, ntiles) * 8);
-    (void)hipDeviceSynchronize();
+    // (on the call's stream, behind the framing launch: the null stream would not order against
+    // a non-blocking stream)
+    (void)cpk::launch_fill(bits, pack_bits_words(N, ntiles) * 8, 0, stream);
   };
   if (e != hipSuccess) {
     clear_bits();
@@ -622,7 +629,12 @@ cpk_status unpack_common(cpk_ctx* ctx, uint32_t mode, const uint8_t* d_packed, u
     TimedLaunch tk(ctx, 2 + stage, stream);
     e = cpk::launch_unpack_stage(stage, a, stream);
     tk.done();
-    if (e != hipSuccess) return CPK_ERR_HIP;
+    if (e != hipSuccess) {
+      // the header launch ran: its look-back descriptors are zero at rest only if the tile
+      // kernel clears them
+      if (a.hdr_nblocks) (void)cpk::launch_fill(ctx->hdr_desc, 8 * a.hdr_nblocks, 0, stream);
+      return CPK_ERR_HIP;
+    }
   }
   tl.done();
   return CPK_OK;
@@ -710,9 +722,15 @@ cpk_status cpk_reserve(cpk_ctx* ctx, uint64_t max_words, uint64_t max_packed_byt
   const uint64_t pt = (max_words + cpk::kPackTileWords - 1) / cpk::kPackTileWords;
   size_t need = pack_scratch_bytes(max_words, pt);
   const uint64_t ut = (max_packed_bytes + cpk::kUnpackTileBytes - 1) / cpk::kUnpackTileBytes;
-  const size_t un = carve_unpack(nullptr, ut, max_items).total + 64;
+  // (the flat stream decode's second-candidate descriptors included)
+  const size_t un = carve_unpack(nullptr, ut, max_items, true).total + 64;
   if (un > need) need = un;
-  return ensure(&ctx->scratch, &ctx->scratch_size, need);
+  cpk_status st = ensure(&ctx->scratch, &ctx->scratch_size, need);
+  if (st != CPK_OK) return st;
+  // the zero-at-rest buffers too: a first call at a new size inside a stream capture would
+  // otherwise allocate and synchronise the device while the stream is capturing
+  if ((st = ensure_pack_bits(ctx, max_words, pt)) != CPK_OK) return st;
+  return ensure_hdr_desc(ctx, max_items);
 }
 
 cpk_status cpk_sync(cpk_ctx* ctx, void* stream) {

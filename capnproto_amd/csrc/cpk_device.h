@@ -156,13 +156,19 @@ __device__ __forceinline__ void mark_chunk(unsigned long long* bits, uint8_t* ts
 // calls it itself for a single-tile batch).
 __device__ __forceinline__ void frame_message(const uint64_t* __restrict__ words,
                                               const uint64_t* __restrict__ off, uint64_t i,
-                                              unsigned long long* __restrict__ bits,
+                                              uint64_t N, unsigned long long* __restrict__ bits,
                                               uint8_t* __restrict__ tstarts,
                                               int32_t* __restrict__ status) {
   const uint64_t w0 = off[i], w1 = off[i + 1];
   int32_t st = 0;
   if (w1 <= w0) {
     if (status) status[i] = 11;  // CPK_ERR_EMPTY_MESSAGE
+    return;
+  }
+  if (w1 > N) {
+    // a message past the batch's words: no bit outside the words the tiles clear (the bitmap is
+    // zero at rest), and nothing read past them
+    if (status) status[i] = 6;  // CPK_ERR_BAD_FRAMING
     return;
   }
   mark_chunk(bits, tstarts, w0);

@@ -14,7 +14,7 @@ namespace {
 // Message i = words[off[i], off[i+1]): segment table (serializeSegmentTable serialize.c++:
 // 311-330) then segments; chunk starts = message start, table end, each segment start.
 __global__ void message_bits_kernel(const uint64_t* __restrict__ words,
-                                    const uint64_t* __restrict__ off, uint64_t n,
+                                    const uint64_t* __restrict__ off, uint64_t n, uint64_t N,
                                     unsigned long long* __restrict__ bits,
                                     uint8_t* __restrict__ tstarts,
                                     int32_t* __restrict__ status, TileFirstJob tf,
@@ -22,7 +22,7 @@ __global__ void message_bits_kernel(const uint64_t* __restrict__ words,
   if (run_tile_first(tf, tf_block)) return;
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  frame_message(words, off, i, bits, tstarts, status);
+  frame_message(words, off, i, N, bits, tstarts, status);
 }
 
 __global__ void chunk_bits_kernel(const uint64_t* __restrict__ off, uint64_t n, uint64_t N,
@@ -40,12 +40,12 @@ __global__ void chunk_bits_kernel(const uint64_t* __restrict__ off, uint64_t n, 
 }  // namespace
 
 hipError_t launch_message_bits(const uint64_t* words, const uint64_t* off, uint64_t n,
-                               uint64_t* bits, uint8_t* tstarts, int32_t* status,
+                               uint64_t N, uint64_t* bits, uint8_t* tstarts, int32_t* status,
                                const TileFirstJob& tf, hipStream_t stream) {
   const unsigned nb = (unsigned)((n + 255) / 256);
   if (nb + tile_first_blocks(tf) == 0) return hipSuccess;
   hipLaunchKernelGGL(message_bits_kernel, dim3(nb + tile_first_blocks(tf)), dim3(256), 0, stream,
-                     words, off, n, (unsigned long long*)bits, tstarts,
+                     words, off, n, N, (unsigned long long*)bits, tstarts,
                      status, tf, nb);
   return hipGetLastError();
 }

@@ -90,7 +90,7 @@ struct TileFirstJob {
 // pack tile of kPackTileWords words), tile_first and the zeroing of TileFirstJob::zero in one
 // launch.
 hipError_t launch_message_bits(const uint64_t* words, const uint64_t* off, uint64_t n,
-                               uint64_t* bits, uint8_t* tstarts, int32_t* status,
+                               uint64_t N, uint64_t* bits, uint8_t* tstarts, int32_t* status,
                                const TileFirstJob& tf, hipStream_t stream);
 hipError_t launch_chunk_bits(const uint64_t* off, uint64_t n, uint64_t N, uint64_t* bits,
                              uint8_t* tstarts, const TileFirstJob& tf, hipStream_t stream);

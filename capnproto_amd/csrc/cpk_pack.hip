@@ -357,7 +357,7 @@ pack_tile_kernel(PackTileArgs a) {
     unsigned long long* const cb = (unsigned long long*)a.chunk_bits;
     if (a.frame_mode == 1) {
       for (uint64_t i = tid; i < a.frame_n; i += 64 * kWv)
-        frame_message(a.words, a.frame_off, i, cb, a.tile_starts, a.frame_status);
+        frame_message(a.words, a.frame_off, i, N, cb, a.tile_starts, a.frame_status);
     } else {
       if (tid == 0) mark_chunk(cb, a.tile_starts, 0);  // word 0 always starts a chunk
       for (uint64_t i = tid; i < a.frame_n; i += 64 * kWv) {

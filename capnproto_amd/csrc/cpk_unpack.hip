@@ -1782,6 +1782,9 @@ unpack_tiles_kernel(UnpackArgs a) {
     const uint64_t o = before + inc - w;
     if (m < a.nmsgs) a.hdr_word_off[m] = o;
     if (m + 1 == a.nmsgs) a.hdr_word_off[a.nmsgs] = o + w;
+    // (waves 1-3 leave at the tile check below: their stores, which may go to pinned host
+    // memory, are complete before wave 0 publishes the call's error word for the host)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
   const uint64_t t = (uint64_t)blockIdx.x * 4 + wv;

@@ -296,3 +296,43 @@ def test_captured_then_eager_calls(codec):
     codec.sync()
     assert torch.equal(packed[:P], ref[:P]) and torch.equal(moff, rmoff) and (st == 0).all()
     assert torch.equal(back[:total], words[:total]) and (ust == 0).all()
+
+
+@pytest.mark.gpu
+def test_reserve_then_capture_fresh_context():
+    """cpk_reserve on a fresh context makes every buffer a pack and an unpack of that size need
+    (the scratch, the zero-at-rest chunk-start bitmap and header-scan descriptors), so both can be
+    captured into a HIP graph as the first calls of the context (include/cpk.h cpk_reserve; no
+    allocation or device synchronisation happens while the stream is capturing)."""
+    import capnproto_amd
+    import torch
+
+    c = capnproto_amd.Codec(0)
+    try:
+        ref_codec = capnproto_amd.Codec(0)
+        off, total = ref_codec.gen_offsets(300, seed=23)
+        words = ref_codec.gen_messages("mixed", off, total, seed=23)
+        ref, rmoff, _ = ref_codec.pack_messages(words, off)
+        ref_codec.sync()
+        P = int(rmoff[-1].item())
+        ref_codec.close()
+        c.reserve(total, P, 300)
+        packed = torch.zeros_like(ref)
+        moff = torch.zeros_like(rmoff)
+        st = torch.full((300,), -1, dtype=torch.int32, device=c.device)
+        back = torch.zeros(total + 8, dtype=torch.int64, device=c.device)
+        woff = torch.zeros(301, dtype=torch.int64, device=c.device)
+        ust = torch.full((300,), -1, dtype=torch.int32, device=c.device)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            c.pack_messages(words, off, out=packed, msg_out_off=moff, status=st)
+            c.unpack_messages(ref, rmoff, total, nbytes=P, words=back, msg_word_off=woff,
+                              status=ust)
+        g.replay()
+        torch.cuda.synchronize()
+        c.sync()
+        assert torch.equal(packed[:P], ref[:P]) and torch.equal(moff, rmoff) and (st == 0).all()
+        assert torch.equal(back[:total], words[:total]) and torch.equal(woff, off)
+        assert (ust == 0).all()
+    finally:
+        c.close()
