@@ -56,7 +56,9 @@ CONFIGS = {
                 workload="C4g: 256 x 64 MiB pointer-heavy messages, 16 segments each, "
                          "geometric zero stretches (mean 300 words)"),
     "c5": dict(nmsgs=(32 << 20) // 8, nseg=1, seg_words=0, profile="mixed", shard="round_robin",
-               workload="C5: 32 Mi mixed-size messages (64 B-16 KiB), round-robin, 4 Mi per GPU"),
+               one_gpu_shard_of=8,
+               workload="C5: 32 Mi mixed-size messages (64 B-16 KiB), round-robin, 4 Mi per GPU "
+                        "(at N = 1: shard 0 of the 8-GPU run, messages 0, 8, 16, ...)"),
 }
 DEBUG_ENV = ("CPK_DEBUG_SKIP", "CPK_STAMPS")
 # kernel-selection knobs (env): a headline number comes from the default kernels unless --ab is
@@ -73,7 +75,7 @@ def parse():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--sub", default=None,
                     help="comma-separated extra configs measured after the headline "
-                         "(default at N=1: c3,c4; 'none' to skip)")
+                         "(default at N=1: c3,c4,c5; 'none' to skip)")
     ap.add_argument("--sub-steps", type=int, default=5)
     ap.add_argument("--shard", default=None, choices=["block", "round_robin", "bytes"],
                     help="message assignment to ranks (default: the config's)")
@@ -241,12 +243,34 @@ def cpu_baseline(sample_words, sample_off, seconds, threads):
     }, ref_packed, jobs[0].poff.copy(), one.n
 
 
-def measure_copy(codec, nbytes=1 << 30, reps=10):
+def config_cpu_baseline(res, seconds):
+    """cpu_baseline on a bounded sample of one measured config (rank 0, N = 1): ~4 MiB of its
+    messages per host thread, copied from the device batch; also checks that the CPU codec's
+    packed bytes of its first slice equal the device's.  Returns (baseline dict, same)."""
+    import numpy as np
+
+    words, off, packed, moff, total, cap = res["tensors"]
+    nt = host_threads()
+    per = max(1, (4 << 20) // max(1, res["U"] // res["n"]))  # ~4 MiB per thread
+    k = min(res["n"], per * nt)
+    o = off[: k + 1].cpu().numpy().astype(np.uint64)
+    ws = words[: int(o[-1])].cpu().numpy().view(np.uint64)
+    cb, ref_packed, ref_off, k1 = cpu_baseline(ws, o, seconds, nt)
+    gp = packed[: int(moff[k1].item())].cpu().numpy()
+    same = gp.tobytes() == np.asarray(ref_packed).tobytes()
+    if not same:
+        print(f"bench: {res['name']}: CPU codec packed bytes differ from the device's",
+              file=sys.stderr)
+    return cb, same
+
+
+def measure_copy(codec, nbytes=1 << 31, reps=6):
     """Device-to-device copy ceiling in the same run: our streaming copy kernel (16 B per lane;
-    capnproto_amd/csrc/cpk_stream.hip copy_kernel), best over 4 or 8 loads in flight per lane,
-    default or non-temporal loads and four grid sizes, read + write bytes / time, timed with
-    HIP events on the stream it runs on.  (The torch copy_ it replaces measured ~4.8 TB/s;
-    MI355X_MICROARCH.md quotes 6.29 TB/s for a float4 copy.)"""
+    capnproto_amd/csrc/cpk_stream.hip copy_kernel), the best of a sweep over 4 / 8 / 16 loads in
+    flight per lane, default or non-temporal loads and stores, grid-strided or contiguous
+    per-block shares, and four grid sizes; read + write bytes / time of 2 GiB each way, timed with
+    HIP events on the stream it runs on.  (MI355X_MICROARCH.md quotes 6.29 TB/s for a float4
+    copy.)"""
     import ctypes as C
 
     torch = codec.torch
@@ -256,8 +280,9 @@ def measure_copy(codec, nbytes=1 << 30, reps=10):
     s = torch.cuda.current_stream(codec.device)
     best = 0.0
     sweep = {}
-    for form in range(4):
-      for g in (4096, 8192, 16384, 32768):
+    names = {0: "x4", 1: "x8", 2: "x16"}
+    for form in (0, 1, 2, 4, 5, 6, 8, 9, 10, 12, 13, 14):
+      for g in (2048, 4096, 8192, 16384):
         blocks = (form << 24) | g
 
         def run():
@@ -274,7 +299,8 @@ def measure_copy(codec, nbytes=1 << 30, reps=10):
         e1.record(s)
         torch.cuda.synchronize()
         gbps = 2 * nbytes / (e0.elapsed_time(e1) / reps * 1e-3) / 1e9
-        sweep[f"{('x4', 'x8', 'x4nt', 'x8nt')[form]}/{g}"] = round(gbps, 1)
+        tag = names[form & 3] + ("nt" if form & 4 else "") + ("c" if form & 8 else "")
+        sweep[f"{tag}/{g}"] = round(gbps, 1)
         best = max(best, gbps)
     ok = torch.equal(a, b)
     del a, b
@@ -322,6 +348,12 @@ def run_config(name, args, steps, warmup, rank, world, dist, codec):
 
     mode = args.shard or cfg.get("shard", "block")
     n_global = cfg["nmsgs"] * world
+    vrank, vworld = rank, world
+    if world == 1 and cfg.get("one_gpu_shard_of"):
+        # a config quoted across 8 GPUs, measured on one: its rank-0 shard (the same messages,
+        # and the same manifest, as rank 0 of the 8-GPU run)
+        vworld = cfg["one_gpu_shard_of"]
+        n_global = cfg["nmsgs"] * vworld
     if mode == "bytes":
         goff, _ = codec.gen_offsets(n_global, nseg=cfg["nseg"], seg_words=cfg["seg_words"],
                                     seed=args.seed)
@@ -329,7 +361,7 @@ def run_config(name, args, steps, warmup, rank, world, dist, codec):
         stride = 1
         del goff
     else:
-        first, stride, n = shard_messages(rank, world, n_global, mode)
+        first, stride, n = shard_messages(vrank, vworld, n_global, mode)
     off, total = codec.gen_offsets(n, nseg=cfg["nseg"], seg_words=cfg["seg_words"],
                                    seed=args.seed, first_msg=first, msg_stride=stride)
     words = codec.gen_messages(cfg["profile"], off, total, nseg=cfg["nseg"], seed=args.seed,
@@ -425,6 +457,7 @@ def run_config(name, args, steps, warmup, rank, world, dist, codec):
            "ok_all": red["ok_all"], "ref_checked": man is not None, "ref_ok": ref_ok,
            "kms": kms, "steps": steps, "warmup": warmup, "graph": graph is not None}
     res["tensors"] = (words, off, packed, moff, total, cap)
+    res["shard"] = (first, stride)
     return res
 
 
@@ -540,17 +573,8 @@ def main():
 
     cb = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        words, off, packed, moff, total, cap = head["tensors"]
-        nt = host_threads()
-        per = max(1, (4 << 20) // max(1, head["U"] // head["n"]))  # ~4 MiB per thread
-        k = min(head["n"], per * nt)
-        o = off[: k + 1].cpu().numpy().astype(np.uint64)
-        ws = words[: int(o[-1])].cpu().numpy().view(np.uint64)
-        cb, ref_packed, ref_off, k1 = cpu_baseline(ws, o, args.cpu_seconds, nt)
-        # the CPU codec's packed bytes of its first slice must equal the device's bit for bit
-        gp = packed[: int(moff[k1].item())].cpu().numpy()
-        if gp.tobytes() != np.asarray(ref_packed).tobytes():
-            ok = False
+        cb, same = config_cpu_baseline(head, args.cpu_seconds)
+        ok = ok and same
     hi = None
     if world == 1 and not args.no_host:
         # the path starts and ends in host memory: serial and pipelined host-inclusive rates
@@ -569,9 +593,14 @@ def main():
     torch.cuda.empty_cache()
 
     subs = []
-    sub = args.sub if args.sub is not None else ("c3,c4" if world == 1 else "none")
+    sub = args.sub if args.sub is not None else ("c3,c4,c5" if world == 1 else "none")
     for nm in [s for s in sub.split(",") if s and s != "none" and s != args.config]:
         r = run_config(nm, args, args.sub_steps, 2, rank, world, dist, codec)
+        r["cpu_baseline"] = None
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            # the reference codec on a bounded sample of this config too (per config)
+            r["cpu_baseline"], same = config_cpu_baseline(r, args.cpu_seconds / 2)
+            ok = ok and same
         r.pop("tensors")
         torch.cuda.empty_cache()
         ok = ok and r["ok_all"]
@@ -617,6 +646,8 @@ def main():
             for r in subs:
                 sr = summarize(r, world, copy_gbps)
                 sr["steps"] = r["steps"]
+                if r.get("cpu_baseline"):
+                    sr["cpu_baseline"] = r["cpu_baseline"]
                 result["sub_results"].append(sr)
         if hi is not None:
             result["host_inclusive"] = hi
@@ -637,13 +668,14 @@ def batch_exchange(codec, head, args, rank, world, dist, reps=3):
     at their global offsets (capnproto_amd.shard.gather_packed: an all-gather of per-rank totals,
     then RCCL send/recv over xGMI into slices of rank 0's buffer), outside the timed step.
     Timed on every rank between barriers; rank 0 then unpacks the gathered stream with the
-    global offsets and, for contiguous shards, checks it against the global batch regenerated on
-    the device.  Reported as its own number, never folded into `value`."""
+    global offsets and checks it against the global batch regenerated on the device (round-robin
+    shards included: gather_packed places every message at its global index).  Reported as its own number, never folded into `value`."""
     import torch
 
     from capnproto_amd.shard import gather_packed
 
     words, off, packed, moff, total, cap = head["tensors"]
+    first, stride = head["shard"]
     n = head["n"]
     times = []
     out = offs = None
@@ -652,7 +684,8 @@ def batch_exchange(codec, head, args, rank, world, dist, reps=3):
         torch.cuda.synchronize()
         dist.barrier()
         t0 = time.perf_counter()
-        out, offs = gather_packed(packed, moff, n, dst=0, dist=dist, device=codec.device)
+        out, offs = gather_packed(packed, moff, n, dst=0, dist=dist, device=codec.device,
+                                  first_msg=first, msg_stride=stride, codec=codec)
         torch.cuda.synchronize()
         dist.barrier()
         times.append(time.perf_counter() - t0)
@@ -673,8 +706,7 @@ def batch_exchange(codec, head, args, rank, world, dist, reps=3):
     back, woff, ust = codec.unpack_messages(out, offs, int(U) // 8, nbytes=G)
     codec.sync()
     ok = bool((ust == 0).all().item()) and int(woff[-1].item()) * 8 == int(U)
-    mode = args.shard or cfg.get("shard", "block")
-    if ok and mode != "round_robin":
+    if ok:  # (message k of the global batch at position k, whatever the shard assignment)
         goff, gtot = codec.gen_offsets(nglob, nseg=cfg["nseg"], seg_words=cfg["seg_words"],
                                        seed=args.seed)
         gw = codec.gen_messages(cfg["profile"], goff, gtot, nseg=cfg["nseg"], seed=args.seed)

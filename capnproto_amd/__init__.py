@@ -69,6 +69,7 @@ def load_library():
         "cpk_destroy": (C.c_int, [vp]),
         "cpk_reserve": (C.c_int, [vp, u64, u64, u64]),
         "cpk_sync": (C.c_int, [vp, vp]),
+        "cpk_copy_ranges": (C.c_int, [vp, vp, vp, vp, vp, u64, vp, vp]),
         "cpk_packed_bound": (u64, [u64, u64]),
         "cpk_pack_chunks": (C.c_int, [vp, vp, u64, vp, u64, vp, u64, vp, vp]),
         "cpk_pack_messages": (C.c_int, [vp, vp, u64, vp, u64, vp, u64, vp, vp, vp]),
@@ -142,6 +143,17 @@ class Codec:
 
     def sync(self, stream=None):
         self._check(self.lib.cpk_sync(self.ctx, self._stream(stream)), "cpk_sync")
+
+    def copy_ranges(self, src, src_off, dst_off, length, dst, stream=None):
+        """dst[dst_off[i] : +length[i]] = src[src_off[i] : +length[i]] for every i (device u8
+        tensors, int64 offset / length tensors of one size; include/cpk.h cpk_copy_ranges)."""
+        n = src_off.numel()
+        if dst_off.numel() != n or length.numel() != n:
+            raise ValueError("copy_ranges: offset and length tensors differ in size")
+        self._check(self.lib.cpk_copy_ranges(self.ctx, _ptr(src), _ptr(src_off), _ptr(dst_off),
+                                             _ptr(length), n, _ptr(dst), self._stream(stream)),
+                    "cpk_copy_ranges")
+        return dst
 
     def reserve(self, max_words, max_packed_bytes, max_items):
         self._check(self.lib.cpk_reserve(self.ctx, max_words, max_packed_bytes, max_items),

@@ -733,6 +733,17 @@ cpk_status cpk_reserve(cpk_ctx* ctx, uint64_t max_words, uint64_t max_packed_byt
   return ensure_hdr_desc(ctx, max_items);
 }
 
+cpk_status cpk_copy_ranges(cpk_ctx* ctx, const uint8_t* d_src, const uint64_t* d_src_off,
+                           const uint64_t* d_dst_off, const uint64_t* d_len, uint64_t n,
+                           uint8_t* d_dst, void* stream) {
+  if (!ctx || (n && (!d_src || !d_src_off || !d_dst_off || !d_len || !d_dst)))
+    return CPK_ERR_INVALID_ARGUMENT;
+  if (hipSetDevice(ctx->device) != hipSuccess) return CPK_ERR_HIP;
+  if (n >= (1ull << 33)) return CPK_ERR_INVALID_ARGUMENT;
+  return hip_status(cpk::launch_copy_ranges(d_src, d_src_off, d_dst_off, d_len, n, d_dst,
+                                            (hipStream_t)stream));
+}
+
 cpk_status cpk_sync(cpk_ctx* ctx, void* stream) {
   if (!ctx) return CPK_ERR_INVALID_ARGUMENT;
   if (hipSetDevice(ctx->device) != hipSuccess) return CPK_ERR_HIP;

@@ -179,6 +179,11 @@ hipError_t launch_split_walk(const uint8_t* packed, uint64_t nbytes, const uint6
                              uint64_t* msg_word_off, uint64_t* msg_in_off, int32_t* status,
                              uint64_t* nmsgs, hipStream_t stream);
 
+// n byte ranges src[src_off[i], +len[i]) -> dst[dst_off[i], ...) (the multi-GPU gather).
+hipError_t launch_copy_ranges(const uint8_t* src, const uint64_t* src_off,
+                              const uint64_t* dst_off, const uint64_t* len, uint64_t n,
+                              uint8_t* dst, hipStream_t stream);
+
 hipError_t launch_gather_segments(const uint64_t* meta, uint32_t nseg, uint64_t total,
                                   uint64_t* out, hipStream_t stream);
 

@@ -47,20 +47,35 @@ __global__ void fill_kernel(uint8_t* __restrict__ p, uint64_t n, uint8_t value) 
 // stores: the measured HBM ceiling bench.py quotes beside the 8 TB/s spec (MI355X_MICROARCH.md:
 // 6.29 TB/s for a float4 copy).  Diagnostic, not on the codec path.
 typedef uint32_t cu32x4 __attribute__((ext_vector_type(4)));
-template <int U, bool NT>
+template <int U, bool NT, bool CONTIG>
 __global__ __launch_bounds__(256) void copy_kernel(const cu32x4* __restrict__ src,
                                                    cu32x4* __restrict__ dst, uint64_t n16) {
-  const uint64_t stride = (uint64_t)gridDim.x * 256;
-  uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  for (; i + (U - 1) * stride < n16; i += U * stride) {
+  // CONTIG: block b copies its own contiguous share of the buffer (256 lanes x U blocks of 16 B
+  // per step); else grid-strided.  NT: non-temporal loads and stores (no cache allocation).
+  uint64_t i, stride, end;
+  if (CONTIG) {
+    const uint64_t per = (n16 + gridDim.x - 1) / gridDim.x;
+    const uint64_t b0 = (uint64_t)blockIdx.x * per;
+    end = b0 + per < n16 ? b0 + per : n16;
+    i = b0 + threadIdx.x;
+    stride = 256;
+  } else {
+    end = n16;
+    stride = (uint64_t)gridDim.x * 256;
+    i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  }
+  for (; i + (U - 1) * stride < end; i += U * stride) {
     cu32x4 v[U];
 #pragma unroll
     for (int k = 0; k < U; k++)
       v[k] = NT ? __builtin_nontemporal_load(src + i + k * stride) : src[i + k * stride];
 #pragma unroll
-    for (int k = 0; k < U; k++) dst[i + k * stride] = v[k];
+    for (int k = 0; k < U; k++) {
+      if (NT) __builtin_nontemporal_store(v[k], dst + i + k * stride);
+      else dst[i + k * stride] = v[k];
+    }
   }
-  for (; i < n16; i += stride) dst[i] = src[i];
+  for (; i < end; i += stride) dst[i] = src[i];
 }
 
 struct Flat {
@@ -701,7 +716,60 @@ __global__ __launch_bounds__(256) void gather_kernel(const uint64_t* __restrict_
   (void)tw;
 }
 
+// ---- message placement for the batch exchange ------------------------------------------------
+// n byte ranges src[src_off[i], +len[i]) -> dst[dst_off[i], ...): one wave per range, the body
+// as 16-byte stores aligned on the destination, each from five aligned source dwords shifted by
+// v_alignbyte (the head and tail bytes one per lane).  Used by the multi-GPU gather to put
+// round-robin shards' messages at their global positions (capnproto_amd/shard.py).
+__global__ __launch_bounds__(256) void copy_ranges_kernel(const uint8_t* __restrict__ src,
+                                                          const uint64_t* __restrict__ src_off,
+                                                          const uint64_t* __restrict__ dst_off,
+                                                          const uint64_t* __restrict__ len,
+                                                          uint64_t n, uint8_t* __restrict__ dst) {
+  const uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= n) return;
+  const uint32_t l = threadIdx.x & 63u;
+  const uint64_t nb = len[i];
+  if (nb == 0) return;
+  const uint8_t* const s0 = src + src_off[i];
+  uint8_t* const o0 = dst + dst_off[i];
+  const uint64_t A0 = (uint64_t)(uintptr_t)o0, A1 = A0 + nb;
+  const uint64_t al = (A0 + 15) & ~15ull;
+  const uint64_t head = (al < A1 ? al : A1) - A0;  // bytes before 16-byte alignment
+  if (l < head) o0[l] = s0[l];
+  if (A1 <= al) return;
+  const uint64_t body = (A1 & ~15ull) - A0;
+  const uint64_t nblk = (body - head) >> 4;
+  // output block k = source bytes [head + 16k, +16): aligned source dwords from there, shifted
+  const uint64_t sb = (uint64_t)(uintptr_t)(s0 + head);
+  const uint32_t* const s32 = (const uint32_t*)(sb & ~3ull);
+  const uint32_t rr = (uint32_t)(sb & 3u);
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  u32x4* const ob = (u32x4*)(o0 + head);
+  for (uint64_t k = l; k < nblk; k += 64) {
+    const uint32_t* const q = s32 + 4 * k;
+    // (the fifth dword is read only when the shift needs it: it may lie past the range)
+    const uint32_t v0 = q[0], v1 = q[1], v2 = q[2], v3 = q[3], v4 = rr ? q[4] : 0u;
+    u32x4 v;
+    v.x = __builtin_amdgcn_alignbyte(v1, v0, rr);
+    v.y = __builtin_amdgcn_alignbyte(v2, v1, rr);
+    v.z = __builtin_amdgcn_alignbyte(v3, v2, rr);
+    v.w = __builtin_amdgcn_alignbyte(v4, v3, rr);
+    ob[k] = v;
+  }
+  if (body + l < nb) o0[body + l] = s0[body + l];
+}
+
 }  // namespace
+
+hipError_t launch_copy_ranges(const uint8_t* src, const uint64_t* src_off,
+                              const uint64_t* dst_off, const uint64_t* len, uint64_t n,
+                              uint8_t* dst, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  copy_ranges_kernel<<<(unsigned)((n + 3) / 4), 256, 0, stream>>>(src, src_off, dst_off, len, n,
+                                                                   dst);
+  return hipGetLastError();
+}
 
 hipError_t launch_gather_segments(const uint64_t* meta, uint32_t nseg, uint64_t total,
                                   uint64_t* out, hipStream_t stream) {
@@ -725,17 +793,31 @@ hipError_t launch_copy(void* dst, const void* src, uint64_t nbytes, uint32_t blo
                        hipStream_t stream) {
   if (nbytes == 0) return hipSuccess;
   if (((uintptr_t)dst | (uintptr_t)src | nbytes) & 15) return hipErrorInvalidValue;
-  // blocks: low 24 bits the grid, bits 24-25 the form (0: 4 loads in flight per lane, 1: 8,
-  // 2: 4 non-temporal, 3: 8 non-temporal)
+  // blocks: low 24 bits the grid; bits 24-25 the loads in flight per lane (4, 8, 16), bit 26
+  // non-temporal loads and stores, bit 27 contiguous per-block shares instead of grid strides
   const unsigned g = (blocks & 0xffffffu) ? (blocks & 0xffffffu) : 4096u;
   const auto* s16 = (const cu32x4*)src;
   auto* d16 = (cu32x4*)dst;
-  switch ((blocks >> 24) & 3u) {
-    case 0: copy_kernel<4, false><<<g, 256, 0, stream>>>(s16, d16, nbytes / 16); break;
-    case 1: copy_kernel<8, false><<<g, 256, 0, stream>>>(s16, d16, nbytes / 16); break;
-    case 2: copy_kernel<4, true><<<g, 256, 0, stream>>>(s16, d16, nbytes / 16); break;
-    default: copy_kernel<8, true><<<g, 256, 0, stream>>>(s16, d16, nbytes / 16); break;
+  const uint64_t n = nbytes / 16;
+  const unsigned form = (blocks >> 24) & 15u;
+#define CPK_COPY_CASE(F, U, NT, C) \
+  case F: copy_kernel<U, NT, C><<<g, 256, 0, stream>>>(s16, d16, n); break;
+  switch (form) {
+    CPK_COPY_CASE(0, 4, false, false)
+    CPK_COPY_CASE(1, 8, false, false)
+    CPK_COPY_CASE(2, 16, false, false)
+    CPK_COPY_CASE(4, 4, true, false)
+    CPK_COPY_CASE(5, 8, true, false)
+    CPK_COPY_CASE(6, 16, true, false)
+    CPK_COPY_CASE(8, 4, false, true)
+    CPK_COPY_CASE(9, 8, false, true)
+    CPK_COPY_CASE(10, 16, false, true)
+    CPK_COPY_CASE(12, 4, true, true)
+    CPK_COPY_CASE(13, 8, true, true)
+    CPK_COPY_CASE(14, 16, true, true)
+    default: return hipErrorInvalidValue;
   }
+#undef CPK_COPY_CASE
   return hipGetLastError();
 }
 

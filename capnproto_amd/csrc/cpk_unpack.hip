@@ -1533,14 +1533,18 @@ __device__ __forceinline__ void lean_special(const uint8_t* d, int p, uint64_t A
 // wave-uniform.  A batch with no message start whose records cannot reach the message's end --
 // by words or by bytes (a record is at most 2050 bytes): one uniform check -- runs with no
 // per-record message logic; the records of other batches find their message by the start bits
-// and a max-scan, and those that end or break their message go through handle_record.
-// Zero and raw runs of at most kShortRun words from the staged bytes are written by their own
-// lane (most runs of dense data), longer ones by the whole wave.
-constexpr uint32_t kShortRun = 4;
+// and a max-scan, and those that end or break their message go through handle_record.  The
+// first word of every zero or raw run is written by the record's own lane with the record (most
+// runs of dense data are one word); the rest of a run by the whole wave.
 __device__ __forceinline__ void expand_lean(const UnpackArgs& a, uint64_t A, const uint8_t* d,
                                             uint64_t* aux, const uint64_t* dep_tab, uint64_t tm,
                                             uint64_t excl, const MsgWin& win, uint64_t msw) {
   const int l = lane_id();
+  // No vector load of the phases before is outstanding here (the look-back's were all used).  An
+  // explicit vmcnt(0) tells the compiler so: without it, it waits for vmcnt(0) -- which on gfx950
+  // counts stores too, so every store of the expansion so far -- before the loops below reuse
+  // such a load's register, once per record batch.
+  __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0); expcnt, lgkmcnt not waited
   const bool starts = ballot(msw != 0) != 0;
   // 16 record-start (and message-start) bits per lane and quarter: u16 number 64h + l of the
   // sub-tile masks is bits [16(l % 4), +16) of sub-tile 16h + l/4, i.e. tile bytes 1024h + 16l..
@@ -1561,19 +1565,29 @@ __device__ __forceinline__ void expand_lean(const UnpackArgs& a, uint64_t A, con
   uint64_t cend = readlane64(win.end, 0);
   uint64_t mw0 = excl;
   const uint32_t* const d32 = (const uint32_t*)d;
+  constexpr uint32_t kStaged = (uint32_t)(kB + kPad);
   for (int h = 0; h < ((a.debug_skip & 32) ? 0 : 4); h++) {
     const uint32_t hs = 16u * ((uint32_t)h & 1u);
     uint32_t bits = ((h < 2 ? tq01 : tq23) >> hs) & 0xffffu;
-    const uint32_t msp = starts ? ((h < 2 ? mq01 : mq23) >> hs) & 0xffffu : 0u;
     const uint32_t c = __popc(bits);
     const uint32_t Rin = wave_incl_sum32(c);
     const uint32_t nh = readlane32(Rin, 63);
-    uint32_t r = Rin - c;
     const uint32_t pbase = 1024u * (uint32_t)h + 16u * (uint32_t)l;
-    while (bits) {
-      const uint32_t b = (uint32_t)__builtin_ctz(bits);
-      bits &= bits - 1;
-      list[r++] = (uint16_t)((pbase + b) | (((msp >> b) & 1u) << 12));
+    uint16_t* lp = list + (Rin - c);
+    if (starts) {
+      // (the message-start flag in bit 12 of each entry)
+      const uint32_t msp = ((h < 2 ? mq01 : mq23) >> hs) & 0xffffu;
+      while (bits) {
+        const uint32_t b = (uint32_t)__builtin_ctz(bits);
+        bits &= bits - 1;
+        *lp++ = (uint16_t)((pbase + b) | (((msp >> b) & 1u) << 12));
+      }
+    } else {
+      while (bits) {
+        const uint32_t b = (uint32_t)__builtin_ctz(bits);
+        bits &= bits - 1;
+        *lp++ = (uint16_t)(pbase + b);
+      }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     for (uint32_t b0 = 0; b0 < ((a.debug_skip & 16) ? 0u : nh); b0 += 64) {
@@ -1587,6 +1601,11 @@ __device__ __forceinline__ void expand_lean(const UnpackArgs& a, uint64_t A, con
       // bytes p .. p + 12: tag, up to 8 data bytes, count byte
       const uint32_t q = p >> 2, sh = p & 3u;
       const uint32_t q0 = d32[q], q1 = d32[q + 1], q2 = d32[q + 2], q3 = d32[q + 3];
+      // a raw run's first word: bytes p + 10 .. p + 17 (read for every lane, used by 0xff records
+      // whose word lies in the staged bytes)
+      const uint32_t rb = p + 10u, rq = rb >> 2, rs = rb & 3u;
+      const uint32_t rqc = rq < kStaged / 4 - 2 ? rq : kStaged / 4 - 3;
+      const uint32_t r0 = d32[rqc], r1 = d32[rqc + 1], r2 = d32[rqc + 2];
       const uint32_t b0w = __builtin_amdgcn_alignbyte(q1, q0, sh);  // bytes p .. p+3
       const uint32_t b1w = __builtin_amdgcn_alignbyte(q2, q1, sh);  // p+4 .. p+7
       const uint32_t b2w = __builtin_amdgcn_alignbyte(q3, q2, sh);  // p+8 .. p+11
@@ -1605,6 +1624,11 @@ __device__ __forceinline__ void expand_lean(const UnpackArgs& a, uint64_t A, con
       const uint32_t wlo = __builtin_amdgcn_perm(dhi, dlo, (uint32_t)sel);
       const uint32_t whi = __builtin_amdgcn_perm(dhi, dlo, (uint32_t)(sel >> 32));
       const uint64_t word = ((uint64_t)whi << 32) | wlo;
+      const uint64_t rw = f ? (((uint64_t)__builtin_amdgcn_alignbyte(r2, r1, rs) << 32) |
+                               __builtin_amdgcn_alignbyte(r1, r0, rs))
+                            : 0ull;
+      // the run's first word is in the staged bytes (always for a zero run)
+      const bool inl = !f || rb + 12u <= kStaged;  // (its three dwords unclamped)
       uint64_t* wp;  // the record's word
       bool special = false;
       int wl = (int)mcount;
@@ -1632,8 +1656,10 @@ __device__ __forceinline__ void expand_lean(const UnpackArgs& a, uint64_t A, con
         const uint32_t len = 1u + __popc(tag) + ((z || f) ? 1u : 0u) + (f ? 8u * cnt : 0u);
         special = act && (wb + w >= mtot || A + p + len >= mend);
       }
-      if (act && !special) {
-        *wp = word;
+      const bool put = act && !special;
+      if (put) {
+        wp[0] = word;
+        if (cnt != 0 && inl) wp[1] = rw;
         if (a.rec_pos) a.rec_pos[wp - a.words] = A + p;
       }
       if (ballot(special)) {
@@ -1642,58 +1668,40 @@ __device__ __forceinline__ void expand_lean(const UnpackArgs& a, uint64_t A, con
         const uint64_t mend = msb ? shfl64(win.end, wl) : cend;
         lean_special(d, (int)p, A, wb, mbase, mtot, mend, win.mw + wl, word, special);
       }
-      // runs of the other records: short ones from the staged bytes by their own lane
-      const bool run = act && !special && cnt != 0;
-      if (ballot(run)) {
-        const uint32_t src = p + 10u;  // tile byte of a raw run's first word
-        const bool staged = !f || src + 8u * cnt + 4u <= (uint32_t)(kB + kPad);
-        const bool shrt = run && cnt <= kShortRun && staged;
-        const uint32_t n = shrt ? cnt : 0u;
-        for (uint32_t k = 0; k < kShortRun; k++) {
-          if (!ballot(k < n)) break;
-          if (k < n) {
-            uint64_t v = 0;
-            if (f) {
-              const uint32_t ob = src + 8u * k, qq = ob >> 2, s3 = ob & 3u;
-              const uint32_t r0 = d32[qq], r1 = d32[qq + 1], r2 = d32[qq + 2];
-              v = ((uint64_t)__builtin_amdgcn_alignbyte(r2, r1, s3) << 32) |
-                  __builtin_amdgcn_alignbyte(r1, r0, s3);
-            }
-            wp[1 + k] = v;
+      // the rest of the runs (the words after the first, or a raw run whose first word is past
+      // the staged bytes): the whole wave per run, from the staged bytes when they hold it
+      uint64_t lm = ballot(put && (cnt > 1u || (cnt != 0 && !inl)));
+      while (lm) {
+        const int j = lowest_bit(lm);
+        lm &= lm - 1;
+        const uint32_t k0 = readlane32(inl ? 1u : 0u, j);
+        const uint32_t nj = readlane32(cnt, j);
+        uint64_t* const dst = (uint64_t*)readlane64((uint64_t)(wp + 1), j);
+        const uint32_t sj = readlane32(rb, j);
+        if (!readlane32(f ? 1u : 0u, j)) {
+          for (uint32_t k = k0 + l; k < nj; k += 64) dst[k] = 0;
+        } else if (sj + 8u * nj + 4u <= kStaged) {
+          for (uint32_t k = k0 + l; k < nj; k += 64) {
+            const uint32_t ob = sj + 8u * k, qq = ob >> 2, s3 = ob & 3u;
+            const uint32_t x0 = d32[qq], x1 = d32[qq + 1], x2 = d32[qq + 2];
+            dst[k] = ((uint64_t)__builtin_amdgcn_alignbyte(x2, x1, s3) << 32) |
+                     __builtin_amdgcn_alignbyte(x1, x0, s3);
           }
-        }
-        uint64_t lm = ballot(run && !shrt);
-        while (lm) {
-          const int j = lowest_bit(lm);
-          lm &= lm - 1;
-          const uint32_t nj = readlane32(cnt, j);
-          uint64_t* const dst = (uint64_t*)readlane64((uint64_t)(wp + 1), j);
-          const uint32_t sj = readlane32(src, j);
-          if (!readlane32(f ? 1u : 0u, j)) {
-            for (uint32_t k = l; k < nj; k += 64) dst[k] = 0;
-          } else if (sj + 8u * nj + 4u <= (uint32_t)(kB + kPad)) {
-            for (uint32_t k = l; k < nj; k += 64) {
-              const uint32_t ob = sj + 8u * k, qq = ob >> 2, s3 = ob & 3u;
-              const uint32_t r0 = d32[qq], r1 = d32[qq + 1], r2 = d32[qq + 2];
-              dst[k] = ((uint64_t)__builtin_amdgcn_alignbyte(r2, r1, s3) << 32) |
-                       __builtin_amdgcn_alignbyte(r1, r0, s3);
+        } else {
+          // past the staged bytes: unaligned 8-byte loads from the batch, all of a 256-word
+          // block issued before its stores (clamped indices: no load left outstanding)
+          const uint8_t* const s8 = a.packed + A + sj;
+          for (uint32_t kb = k0; kb < nj; kb += 256) {
+            uint64_t v[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+              const uint32_t k = kb + 64 * i + l;
+              __builtin_memcpy(&v[i], s8 + 8ull * (k < nj ? k : nj - 1), 8);
             }
-          } else {
-            // past the staged bytes: unaligned 8-byte loads from the batch, all of a 256-word
-            // block issued before its stores (clamped indices: no load left outstanding)
-            const uint8_t* const s8 = a.packed + A + sj;
-            for (uint32_t k0 = 0; k0 < nj; k0 += 256) {
-              uint64_t v[4];
 #pragma unroll
-              for (int i = 0; i < 4; i++) {
-                const uint32_t k = k0 + 64 * i + l;
-                __builtin_memcpy(&v[i], s8 + 8ull * (k < nj ? k : nj - 1), 8);
-              }
-#pragma unroll
-              for (int i = 0; i < 4; i++) {
-                const uint32_t k = k0 + 64 * i + l;
-                dst[k < nj ? k : nj - 1] = v[i];
-              }
+            for (int i = 0; i < 4; i++) {
+              const uint32_t k = kb + 64 * i + l;
+              dst[k < nj ? k : nj - 1] = v[i];
             }
           }
         }

@@ -70,34 +70,49 @@ def global_offsets(local_packed_total: int, dist=None, device=None):
     return sum(vals[:r]), sum(vals)
 
 
-def gather_packed(packed, msg_out_off, nmsgs: int, dst: int = 0, dist=None, device=None):
+def gather_packed(packed, msg_out_off, nmsgs: int, dst: int = 0, dist=None, device=None,
+                  first_msg=None, msg_stride: int = 1, codec=None):
     """The batch case of SURVEY.md 8(e): every rank's packed messages land on rank ``dst`` as ONE
-    packed stream, rank r's bytes at the sum of the packed totals of ranks < r (the offsets
-    ``global_offsets`` computes), with the global per-message offsets.
+    packed stream holding the global batch in global message order -- message k at position k,
+    as one rank packing every message writes it and as the reference's readers take messages
+    back to back from one stream (serialize-packed-test.c++:348-371) -- with the N_global + 1
+    global byte offsets.
 
     packed: u8 tensor holding this rank's packed batch (at least P bytes); msg_out_off: its
-    nmsgs + 1 int64 byte offsets (``Codec.pack_messages``).  One all-gather of (P, nmsgs) per
-    rank, then point-to-point sends of the bytes and the offsets, received in place -- into
-    slices of the destination's output at their global positions, so nothing is copied after the
-    receive but the rebasing of the received offsets.  With block or byte-balanced shards
-    (contiguous message ranges) the result is the packed stream of the global batch in message
-    order, i.e. what a single rank packing every message writes.
+    nmsgs + 1 int64 byte offsets (``Codec.pack_messages``).  Local message i is global message
+    ``first_msg + msg_stride * i`` (``shard_messages``); first_msg None means the ranks hold
+    contiguous ranges in rank order (block or byte-balanced shards).
 
-    Returns (stream, offsets) on ``dst`` -- the u8 stream of the global total and the
-    N_global + 1 int64 message offsets -- and (None, None) on the other ranks."""
+    One all-gather of (P, nmsgs, first_msg, msg_stride) per rank, then each rank's packed bytes
+    and local offsets sent point to point.  Contiguous ranges in rank order are received in
+    place, at their global byte offsets (nothing copied after the receive but the rebasing of the
+    offsets).  Otherwise (round-robin, C5) the bytes are received rank after rank into a staging
+    buffer and every message is copied to its global offset -- the exclusive sum of the global
+    per-message sizes -- by one device launch (``Codec.copy_ranges``, one wave per message; pass
+    ``codec`` for device tensors; host tensors, as in the gloo tests, are copied by torch).
+
+    Returns (stream, offsets) on ``dst`` and (None, None) on the other ranks."""
     import torch
 
     P = int(msg_out_off[nmsgs].item())
     if dist is None:
         return packed[:P], msg_out_off[: nmsgs + 1]
     world, rank = dist.get_world_size(), dist.get_rank()
-    meta = torch.tensor([P, nmsgs], dtype=torch.int64, device=device)
+    contiguous_flag = 1 if first_msg is None else 0
+    meta = torch.tensor([P, nmsgs, 0 if first_msg is None else first_msg, msg_stride,
+                         contiguous_flag], dtype=torch.int64, device=device)
     parts = [torch.zeros_like(meta) for _ in range(world)]
     dist.all_gather(parts, meta)
     sizes = [int(p[0].item()) for p in parts]
     counts = [int(p[1].item()) for p in parts]
+    firsts = [int(p[2].item()) for p in parts]
+    strides = [max(1, int(p[3].item())) for p in parts]
     bases = [sum(sizes[:r]) for r in range(world)]
     mbase = [sum(counts[:r]) for r in range(world)]
+    # rank-order contiguous ranges: global message ids mbase[r] + i on every rank
+    in_order = all(int(p[4].item()) == 1 or (firsts[r] == mbase[r] and (strides[r] == 1 or
+                                                                      counts[r] <= 1))
+                   for r, p in enumerate(parts))
     if rank != dst:
         ops = []
         if P:
@@ -109,26 +124,62 @@ def gather_packed(packed, msg_out_off, nmsgs: int, dst: int = 0, dist=None, devi
                 req.wait()
         return None, None
     total, ntotal = sum(sizes), sum(counts)
-    out = torch.empty(total, dtype=torch.uint8, device=packed.device)
-    offs = torch.empty(ntotal + 1, dtype=torch.int64, device=packed.device)
+    dev = packed.device
+    # rank order: rank r's bytes at bases[r], its local offsets at mbase[r] -- the final layout
+    # when the ranks hold contiguous ranges in rank order, else the staging of the placement
+    buf = torch.empty(total, dtype=torch.uint8, device=dev)
+    loff = torch.empty(ntotal + 1, dtype=torch.int64, device=dev)
     ops = []
     for r in range(world):
         if r == dst:
             continue
         if sizes[r]:
-            ops.append(dist.P2POp(dist.irecv, out[bases[r]:bases[r] + sizes[r]], r))
+            ops.append(dist.P2POp(dist.irecv, buf[bases[r]:bases[r] + sizes[r]], r))
         if counts[r]:
-            ops.append(dist.P2POp(dist.irecv, offs[mbase[r]:mbase[r] + counts[r]], r))
+            ops.append(dist.P2POp(dist.irecv, loff[mbase[r]:mbase[r] + counts[r]], r))
     reqs = dist.batch_isend_irecv(ops) if ops else []
-    out[bases[dst]:bases[dst] + P].copy_(packed[:P])
-    offs[mbase[dst]:mbase[dst] + nmsgs].copy_(msg_out_off[:nmsgs])
+    buf[bases[dst]:bases[dst] + P].copy_(packed[:P])
+    loff[mbase[dst]:mbase[dst] + nmsgs].copy_(msg_out_off[:nmsgs])
     for req in reqs:
         req.wait()
-    for r in range(world):  # rank-local offsets -> global
-        if counts[r] and bases[r]:
-            offs[mbase[r]:mbase[r] + counts[r]] += bases[r]
-    offs[ntotal] = total
-    return out, offs
+    if in_order:
+        for r in range(world):  # rank-local offsets -> global
+            if counts[r] and bases[r]:
+                loff[mbase[r]:mbase[r] + counts[r]] += bases[r]
+        loff[ntotal] = total
+        return buf, loff
+    # global message id, size and source offset of every received message (rank order)
+    gid = torch.cat([firsts[r] + strides[r] * torch.arange(counts[r], dtype=torch.int64,
+                                                            device=dev)
+                     for r in range(world)]) if ntotal else torch.zeros(0, dtype=torch.int64,
+                                                                         device=dev)
+    ends = loff[1:ntotal + 1].clone()
+    for r in range(world):  # each rank's last message ends at its packed total
+        if counts[r]:
+            ends[mbase[r] + counts[r] - 1] = sizes[r]
+    msize = ends - loff[:ntotal]
+    src = loff[:ntotal] + torch.repeat_interleave(
+        torch.tensor(bases, dtype=torch.int64, device=dev),
+        torch.tensor(counts, dtype=torch.int64, device=dev))
+    if ntotal and (int(gid.min().item()) < 0 or int(gid.max().item()) >= ntotal or
+                   int(torch.bincount(gid, minlength=ntotal).max().item()) != 1):
+        raise ValueError("gather_packed: the ranks' messages are not a permutation of the "
+                         "global batch (first_msg / msg_stride)")
+    gsize = torch.zeros(ntotal, dtype=torch.int64, device=dev)
+    gsize[gid] = msize
+    goff = torch.zeros(ntotal + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(gsize, 0, out=goff[1:])
+    dst_off = goff[gid]
+    out = torch.empty(total, dtype=torch.uint8, device=dev)
+    if dev.type == "cpu":
+        # host tensors (the gloo tests): the same placement, message by message
+        for s_, d_, n_ in zip(src.tolist(), dst_off.tolist(), msize.tolist()):
+            out[d_:d_ + n_] = buf[s_:s_ + n_]
+    else:
+        if codec is None:
+            raise ValueError("gather_packed: pass codec= to place device tensors")
+        codec.copy_ranges(buf, src, dst_off, msize, out)
+    return out, goff
 
 
 def reduce_step(dt_s: float, unpacked: float, packed: float, pack_ms: float, unpack_ms: float,

@@ -188,6 +188,16 @@ cpk_status cpk_unpack_chunks(cpk_ctx* ctx, const uint8_t* d_packed, uint64_t tot
                              uint64_t* d_words, uint64_t words_capacity, int32_t* d_status,
                              void* stream);
 
+/* Batch exchange (multi-GPU): copies n byte ranges
+ * d_src[d_src_off[i], +d_len[i]) to d_dst[d_dst_off[i], ...) on the device -- the placement of
+ * each shard's packed messages at their global offsets when the shards are not contiguous
+ * message ranges (round-robin: message k of the global batch at position k of the one packed
+ * stream, as serialize-packed-test.c++:348-371 reads messages back to back).  Ranges must not
+ * overlap in d_dst.  No reference counterpart (the reference has one process, one stream). */
+cpk_status cpk_copy_ranges(cpk_ctx* ctx, const uint8_t* d_src, const uint64_t* d_src_off,
+                           const uint64_t* d_dst_off, const uint64_t* d_len, uint64_t n,
+                           uint8_t* d_dst, void* stream);
+
 /* ------------------------------------------------------------------------------------------
  * Host-buffer convenience: the path the reference actually sits on (a socket or file buffer).
  * These stage through the context's device buffers and include the H2D and D2H copies.

@@ -114,7 +114,7 @@ def test_balanced_ranges(world):
     assert max(loads) - min(loads) <= 2 * int(sizes.max())
 
 
-def _gather_worker(rank, world, port, dst, q):
+def _gather_worker(rank, world, port, dst, q, mode="block"):
     import torch
     import torch.distributed as dist
 
@@ -126,8 +126,8 @@ def _gather_worker(rank, world, port, dst, q):
         import pyoracle
 
         msgs = _global_batch()
-        first, stride, count = shard_messages(rank, world, len(msgs), "block")
-        mine = msgs[first:first + count]
+        first, stride, count = shard_messages(rank, world, len(msgs), mode)
+        mine = [msgs[first + stride * i] for i in range(count)]
         off = np.cumsum([0] + [len(m) for m in mine]).astype(np.uint64)
         packed, poff, st = pyoracle.Oracle().pack_batch(
             np.concatenate(mine) if count else np.zeros(0, np.uint64), off)
@@ -135,21 +135,27 @@ def _gather_worker(rank, world, port, dst, q):
         buf = torch.zeros(int(poff[-1]) + 64, dtype=torch.uint8)
         buf[: int(poff[-1])] = torch.from_numpy(np.asarray(packed[: int(poff[-1])]).copy())
         moff = torch.from_numpy(poff.astype(np.int64))
-        out, offs = gather_packed(buf, moff, count, dst=dst, dist=dist)
+        if mode == "block":  # (contiguous ranges in rank order: no ids needed)
+            out, offs = gather_packed(buf, moff, count, dst=dst, dist=dist)
+        else:
+            out, offs = gather_packed(buf, moff, count, dst=dst, dist=dist, first_msg=first,
+                                      msg_stride=stride)
         q.put((rank, None if out is None else (bytes(out.numpy()), offs.numpy().tolist())))
     finally:
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("mode", ["block", "round_robin"])
 @pytest.mark.parametrize("world,dst", [(2, 0), (2, 1), (3, 1)])
-def test_gloo_gather_packed_equals_single_rank_pack(world, dst):
-    """The batch case: block shards packed on each rank, gathered onto rank
-    `dst` by point-to-point sends into their global offsets -- the gathered stream and message
-    offsets equal a single rank packing the whole batch."""
+def test_gloo_gather_packed_equals_single_rank_pack(world, dst, mode):
+    """The batch case: block or round-robin shards (C5's assignment) packed on
+    each rank, gathered onto rank `dst` -- the gathered stream holds message k at position k and
+    the stream and message offsets equal a single rank packing the whole batch (the reference's
+    readers take messages back to back from one stream, serialize-packed-test.c++:348-371)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, dst, q))
+    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, dst, q, mode))
              for r in range(world)]
     for p in procs:
         p.start()
