@@ -305,72 +305,60 @@ cpk_status order_streams(cpk_ctx* ctx, hipStream_t s) {
   return CPK_OK;
 }
 
-#ifndef CPK_PACK_DIRECT
-#define CPK_PACK_DIRECT 0  // 1: pack_direct_kernel (no scratch slots / scan / placement)
-#endif
-
 struct PackScratch {
   uint32_t* state;
-  uint64_t* bits;
-  uint32_t* ticket;
+  unsigned long long* arena_next;
   uint64_t* desc;
-  uint64_t* gword;
-  uint64_t* gincl;
+  uint64_t* gdesc;
   size_t zero_bytes;
   uint64_t* tile_first;
   uint64_t* tile_bytes;
-  uint64_t* tile_off;
   uint32_t* thole;
   uint32_t* tpatch;
-  uint8_t* scr;
-  uint8_t* scr_small;
-  uint32_t* tslot;
-  uint32_t nslots;
+  uint64_t* tpiece;
+  uint8_t* arena;
+  uint64_t arena_cap;
   size_t total;
 };
 
-// Pack scratch: the zeroed part (exit budgets polled by the next tile, the count of pool slots
-// taken, the tiles' look-back descriptors; zeroed by the framing launch), then per tile the first
-// requested position, byte count, count-byte patch and pool slot, then the slot pool (at most
-// kPackSlots slots of kPackScratchBytes: ~40 MiB whatever the batch size) for the bytes of tiles
-// whose offset was not known in time.  (The chunk-start bitmap
-// is zero at rest in its own buffer, ctx->pack_bits.)
-PackScratch carve_pack(void* base, uint64_t N, uint64_t ntiles, bool direct) {
-  (void)N;
+// Byte arena of a pack of N words: the packed bytes of the tiles whose offset is not known in time
+// wait there for the placement launch, each in a piece of exactly its size.  Half the unpacked
+// bytes (at least 8 MiB, at most the worst-case packed size or 8 GiB): a tile finding it full
+// waits for its offset instead.
+uint64_t pack_arena_bytes(uint64_t N, uint64_t ntiles) {
+  uint64_t cap = N * 4;
+  if (cap < (8ull << 20)) cap = 8ull << 20;
+  const uint64_t worst = N * 10 + 16 * ntiles;
+  if (cap > worst) cap = worst;
+  if (cap > (8ull << 30)) cap = 8ull << 30;
+  return (cap + 15) & ~15ull;
+}
+
+// Pack scratch: the zeroed part (exit budgets polled by the next tile, the arena's fill counter,
+// the tiles' look-back descriptors and the placement groups'; zeroed by the framing launch), then
+// per tile the first requested position, byte count, count-byte patch and arena piece, then the
+// arena.  (The chunk-start bitmap is zero at rest in its own buffer, ctx->pack_bits.)
+PackScratch carve_pack(void* base, uint64_t N, uint64_t ntiles) {
   Carve c(base);
   PackScratch s;
-  s.bits = nullptr;
   s.state = c.take<uint32_t>(ntiles);
-  s.ticket = c.take<uint32_t>(4);  // (direct kernel: tile tickets; tile kernel: slots taken)
-  s.desc = c.take<uint64_t>(ntiles);  // tile descriptors (direct kernel; tiles resolved in time)
-  s.gword = c.take<uint64_t>(direct ? ntiles / 64 + 1 : 0);
-  s.gincl = c.take<uint64_t>(direct ? ntiles / 64 + 1 : 0);
+  s.arena_next = c.take<unsigned long long>(2);
+  s.desc = c.take<uint64_t>(ntiles);
+  s.gdesc = c.take<uint64_t>(cpk::pack_place_groups(ntiles));
   s.zero_bytes = c.off;
-  if (direct) {  // the direct kernel writes straight to the output: no slots, counts, offsets
-    s.tile_first = c.take<uint64_t>(ntiles);
-    s.tile_bytes = s.tile_off = nullptr;
-    s.thole = s.tpatch = s.tslot = nullptr;
-    s.scr_small = nullptr;
-    s.nslots = 0;
-    s.scr = nullptr;
-    s.total = c.off;
-    return s;
-  }
   s.tile_first = c.take<uint64_t>(ntiles);
   s.tile_bytes = c.take<uint64_t>(ntiles);
-  s.tile_off = nullptr;
   s.thole = c.take<uint32_t>(ntiles);
   s.tpatch = c.take<uint32_t>(ntiles);
-  s.tslot = c.take<uint32_t>(ntiles);
-  s.scr_small = c.take<uint8_t>(ntiles * cpk::kSmallSlot + 16);
-  s.nslots = (uint32_t)(cpk::kPackSlots == 0 || ntiles < cpk::kPackSlots ? ntiles : cpk::kPackSlots);
-  s.scr = c.take<uint8_t>(s.nslots * cpk::kPackScratchBytes + 16);
+  s.tpiece = c.take<uint64_t>(ntiles);
+  s.arena_cap = ntiles > 1 ? pack_arena_bytes(N, ntiles) : 0;
+  s.arena = c.take<uint8_t>(s.arena_cap + 16);
   s.total = c.off;
   return s;
 }
 
 size_t pack_scratch_bytes(uint64_t N, uint64_t ntiles) {
-  return carve_pack(nullptr, N, ntiles, CPK_PACK_DIRECT).total + 64;
+  return carve_pack(nullptr, N, ntiles).total + 64;
 }
 
 cpk_status ensure_pack_bits(cpk_ctx* ctx, uint64_t N, uint64_t ntiles);
@@ -386,12 +374,10 @@ cpk_status pack_common(cpk_ctx* ctx, const uint64_t* d_words, uint64_t N, const 
   const uint64_t ntiles = (N + T - 1) / T;
   // a batch of one tile (a single small message): one launch, the tile kernel framing the batch
   // itself and writing its bytes at offset 0 (no framing or placement launch)
-  const bool direct = CPK_PACK_DIRECT;
-  const bool single = !direct && ntiles == 1;
-  cpk_status st = ensure(&ctx->scratch, &ctx->scratch_size,
-                         carve_pack(nullptr, N, ntiles, direct).total + 64);
+  const bool single = ntiles == 1;
+  cpk_status st = ensure(&ctx->scratch, &ctx->scratch_size, carve_pack(nullptr, N, ntiles).total + 64);
   if (st != CPK_OK) return st;
-  PackScratch s = carve_pack(ctx->scratch, N, ntiles, direct);
+  PackScratch s = carve_pack(ctx->scratch, N, ntiles);
   if ((st = ensure_pack_bits(ctx, N, ntiles)) != CPK_OK) return st;
   uint64_t* const bits = ctx->pack_bits;
   uint8_t* const tstarts = (uint8_t*)(bits + (N + 63) / 64 + 1);
@@ -444,19 +430,15 @@ cpk_status pack_common(cpk_ctx* ctx, const uint64_t* d_words, uint64_t N, const 
   a.total_out = nullptr;
   a.state = s.state;
   a.tile_bytes = s.tile_bytes;
-  a.tile_off = s.tile_off;
-  a.scr = s.scr;
-  a.tslot = s.tslot;
-  a.scr_small = s.scr_small;
-  a.slot_next = s.ticket;
-  a.nslots = s.nslots;
+  a.arena = s.arena;
+  a.arena_cap = s.arena_cap;
+  a.arena_next = s.arena_next;
+  a.tpiece = s.tpiece;
+  a.gdesc = s.gdesc;
   a.thole = s.thole;
   a.tpatch = s.tpatch;
   a.err = ctx->err;
-  a.ticket = s.ticket;
   a.desc = s.desc;
-  a.gword = s.gword;
-  a.gincl = s.gincl;
   a.err_host = single ? ctx->err_host : nullptr;
   ctx->fused_last = a.err_host != nullptr;
   a.frame_mode = single ? (messages ? 1u : 2u) : 0u;
@@ -464,14 +446,7 @@ cpk_status pack_common(cpk_ctx* ctx, const uint64_t* d_words, uint64_t N, const 
   a.frame_n = n;
   a.frame_status = d_status;
   TimedLaunch tl(ctx, 0, stream);
-  if (direct) {
-    e = cpk::launch_pack_direct(a, stream);
-    tl.done();
-    if (e != hipSuccess) clear_bits();
-    return hip_status(e);
-  }
-  // tiles -> output (offset known in time) or scratch slots; the rest placed by the look-back
-  // of the placement launch
+  // tiles -> output (offset known in time) or arena pieces, placed by the placement launch
   e = cpk::launch_pack_tiles(a, stream);
   if (e != hipSuccess) clear_bits();
   if (e == hipSuccess && !single) e = cpk::launch_pack_place(a, stream);

@@ -9,15 +9,6 @@ namespace cpk {
 
 constexpr uint64_t kPackTileWords = 2048;       // words per workgroup tile (cpk_pack.hip)
 constexpr uint64_t kPackScratchBytes = 10 * kPackTileWords;  // a tile's packed bytes, worst case
-#ifndef CPK_PACK_SLOTS
-#define CPK_PACK_SLOTS 2048  // slot pool: a tile finding none waits for its offset (0: one per tile)
-#endif
-constexpr uint64_t kPackSlots = CPK_PACK_SLOTS;
-#ifndef CPK_PACK_SMALL
-#define CPK_PACK_SMALL 0  // bytes (a multiple of 16): a tile packing to at most this many goes
-#endif                    // through its own small slot (CPK_PACK_SMALL / 16 KiB of the batch)
-constexpr uint32_t kSmallSlot = CPK_PACK_SMALL;
-constexpr uint32_t kSmallTag = 0xfffffffeu;
 constexpr uint64_t kUnpackTileBytes = 4096;     // packed bytes per unpack tile (>= 2050)
 
 struct PackTileArgs {
@@ -39,21 +30,14 @@ struct PackTileArgs {
   // scratch
   uint32_t* state;             // ntiles exit budgets (0x80000000 | raw << 8 | budget), zeroed
   uint64_t* tile_bytes;        // ntiles packed bytes per tile
-  uint64_t* tile_off;          // (unused: offsets come from the descriptors' look-back)
-  uint8_t* scr;                // slot pool (nslots * kPackScratchBytes + 16) for the tiles whose
-                               // offset is not known in time
-  uint32_t* tslot;             // per tile: its slot (written only by tiles that take one;
-                               // kSmallTag: its own small slot in scr_small)
-  uint8_t* scr_small;          // per tile a kSmallSlot-byte slot for tiles of at most that many bytes
-  uint32_t* slot_next;         // slots taken so far (zeroed)
-  uint32_t nslots;
+  uint8_t* arena;              // byte arena (16-byte aligned pieces) for the tiles whose offset is
+  uint64_t arena_cap;          // not known in time, arena_cap bytes
+  unsigned long long* arena_next;  // bytes of the arena taken so far (zeroed)
+  uint64_t* tpiece;            // per tile: its arena piece (~0: written straight out or not at all)
+  uint64_t* gdesc;             // placement group descriptors (zeroed)
   uint32_t* thole;             // byte of a tile's provisional count (~0: none)
   uint32_t* tpatch;            // the next tile's final value for it (0x100 | v; 0: none)
   uint32_t* err;
-  // zeroed: tile tickets (direct kernel), tile descriptors (AGG | bytes, INCL | inclusive prefix;
-  // both kernels), per 64-tile group (count << 48) + bytes and the groups' inclusive byte prefix
-  // (direct kernel)
-  uint32_t* ticket;
   // single-tile batches: the framing launch's work done by the tile kernel itself (frame_mode 1:
   // message batch, frame_off = message word offsets, statuses to frame_status; 2: chunk
   // offsets; 0: framed by the framing launch)
@@ -62,18 +46,18 @@ struct PackTileArgs {
   const uint64_t* frame_off;
   uint64_t frame_n;
   int32_t* frame_status;
-  uint64_t* desc;
-  uint64_t* gword;
-  uint64_t* gincl;
+  uint64_t* desc;              // tile descriptors (AGG | bytes, INCL | inclusive prefix), zeroed
 };
 
-// tiles -> out when the tile's offset is known in time, else its scratch slot (tile_bytes, thole,
-// tpatch, desc); then placement: offsets by look-back over desc, scratch -> out
+// tiles -> out when the tile's offset is known in time, else a piece of the byte arena
+// (tile_bytes, thole, tpatch, desc, tpiece); then placement: offsets from a scan of the tile byte
+// counts (kPlaceGroup tiles per workgroup), arena pieces -> out
 hipError_t launch_pack_tiles(const PackTileArgs& a, hipStream_t stream);
 hipError_t launch_pack_place(const PackTileArgs& a, hipStream_t stream);
-// tiles -> out directly (persistent, ticketed, two-level look-back resolved one tile late): no
-// scratch slots, no scan, no placement
-hipError_t launch_pack_direct(const PackTileArgs& a, hipStream_t stream);
+constexpr uint64_t kPackPlaceGroup = 16;
+inline uint64_t pack_place_groups(uint64_t ntiles) {
+  return (ntiles + kPackPlaceGroup - 1) / kPackPlaceGroup;
+}
 // tile_first (first i with pos[i] >= tile start, per tile) as extra blocks of a prologue
 // kernel: one launch fewer per call.  ntiles == 0: no such job.
 struct TileFirstJob {
@@ -117,7 +101,7 @@ struct UnpackArgs {
   unsigned long long* stamps;   // diagnostic build only (env CPK_STAMPS), else NULL
   uint32_t debug_skip;          // diagnostic (env CPK_DEBUG_SKIP): 4 no chain-0 walks, 8 no look-back,
                                 // 16 no record batches, 32 no lists; return after 64 staging and
-                                // message window, 128 chain 0, 256 entry and look-back
+                                // message window, 128 chain 0, 256 entry and look-back; 512 at once
   const uint64_t* tile_firstpos;  // in_off[tile_first[t]]: the first message start >= tile start
   uint64_t* hdr_desc;           // the header launch's scan descriptors (zero at rest): cleared
   uint64_t hdr_nblocks;         // by the tile kernel once the headers are done (0: none)

@@ -50,6 +50,7 @@ constexpr uint32_t kCap = 9 * kTW;             // staging window (bytes)
 constexpr uint32_t kPadF = 16;                 // front pad: records straddling the window start
 constexpr int kSlotDw = (kPadF + kCap + 64) / 4;
 constexpr int kTrashDw = 64 + 4;               // lane l: dwords l .. l + 3
+constexpr uint32_t kArenaTile = 4096;          // tiles of at most this many bytes use the arena
 constexpr uint64_t kScr = kPackScratchBytes;    // scratch slot per tile (<= 10 B per word)
 static_assert(kScr >= 10 * kTW && kScr % 16 == 0, "a tile's bytes fit its scratch slot");
 
@@ -338,7 +339,7 @@ pack_tile_kernel(PackTileArgs a) {
   __shared__ uint32_t s_hole;        // byte of the tile's provisional count (~0: none)
   __shared__ uint64_t s_dst;         // the tile's output offset when resolved in time (~0: not)
   __shared__ uint32_t s_patch;       // previous tile's count byte | its distance before ours << 8
-  __shared__ uint32_t s_slot;        // the tile's slot of the pool (~0: none)
+  __shared__ uint64_t s_piece;       // the tile's arena piece (byte offset; ~0: none)
 
   const int tid = (int)threadIdx.x;
   const int w = (int)uniform32(threadIdx.x >> 6);
@@ -672,61 +673,42 @@ pack_tile_kernel(PackTileArgs a) {
 #ifdef CPK_DIAG
     if (win == 0) CPK_PSTAMP(2);
 #endif
-    // A tile of few bytes (sparse words) goes to its own small slot at once -- copying it twice
-    // costs less than a workgroup stalled on a round trip -- while wave 0 publishes its
-    // inclusive prefix when the predecessors have theirs (so the placement launch finds one near).
-    const bool small = kSmallSlot && T != 0 && !windowed && agg <= kSmallSlot;
-    if (small) {
-      if (w == 0) {
-        uint64_t ex = 0;
-        if (pack_lookback(a.desc, T, &ex, false, a.err) && l == 0)
-          store_agent(a.desc + T, kDescIncl | (ex + agg));
-        if (l == 0) {
-          a.tslot[T] = kSmallTag;
-          CPK_PDIAG(0, 1);
-          CPK_PDIAG(2, 1);
-        }
-      }
-      u32x4* const dst = (u32x4*)(a.scr_small + T * kSmallSlot);
-      const uint32_t n16 = (agg + 15u) >> 4;
-      for (uint32_t i = tid + opaque_zero(); i < n16; i += 64 * kWv)
-        dst[i] = ((const u32x4*)stg)[1 + i];
-      s_dst = ~0ull;  // (read by the single-tile ending only, never for such a tile)
-      break;
-    }
     if (win == 0) {
       // The tile's offset, if the tiles before it have all published their byte counts by now
-      // (no waiting): then its bytes go straight to the output and the placement launch skips
-      // it.  Otherwise a slot of the pool holds them for the placement launch; with the pool
-      // used up (or more bytes than one staging window), the tile waits for its offset after all
-      // (only ever on lower tiles, which publish their byte counts before anything they could
-      // wait for).
+      // (no waiting): then its bytes go straight to the output.  Otherwise a tile of few bytes
+      // (sparse words: at most kArenaTile) goes to a piece of the byte arena -- exactly its size,
+      // taken by one atomic add -- for the placement launch, where copying it costs less than
+      // holding the CU while it waits; a denser tile (or one finding the arena used up, or one of
+      // more bytes than one staging window) waits for its offset: copying it twice costs more
+      // than the wait (only ever on lower tiles, which publish their byte counts before anything
+      // they could wait for).
       if (w == 0) {
         uint64_t ex = 0;
-        bool ok = T == 0, wait = windowed;
-        uint32_t slot = ~0u;
+        bool ok = T == 0, wait = windowed || agg > kArenaTile;
+        uint64_t piece = ~0ull;
         while (!ok) {
           ok = pack_lookback(a.desc, T, &ex, wait, a.err);
           if (ok || wait) break;
-          if (l == 0) slot = atomicAdd(a.slot_next, 1u);
-          slot = readlane32(slot, 0);
-          if (slot < a.nslots) break;
-          slot = ~0u;
+          const uint64_t need = ((uint64_t)agg + 15u) & ~15ull;
+          if (l == 0) piece = atomicAdd((unsigned long long*)a.arena_next, (unsigned long long)need);
+          piece = readlane64(piece, 0);
+          if (piece + need <= a.arena_cap) break;
+          piece = ~0ull;  // (the arena is full: the counter stays past its end)
           wait = true;
         }
         if (l == 0) {
           CPK_PDIAG(0, 1);
-          CPK_PDIAG(wait ? 3 : (slot != ~0u ? 2 : 1), 1);
+          CPK_PDIAG(wait ? 3 : (piece != ~0ull ? 2 : 1), 1);
 #ifdef CPK_DIAG
-          pout = wait ? 3 : (slot != ~0u ? 2 : 1);
+          pout = wait ? 3 : (piece != ~0ull ? 2 : 1);
 #endif
         }
         ok = ok && ex + agg <= a.out_capacity;  // (too small an output: placement raises it)
         if (l == 0) {
           if (ok && T != 0) store_agent(a.desc + T, kDescIncl | (ex + agg));
-          a.tslot[T] = slot;  // (~0: written straight out, or not at all)
+          a.tpiece[T] = piece;  // (~0: written straight out, or not at all)
           s_dst = ok ? ex : ~0ull;
-          s_slot = slot;
+          s_piece = piece;
         }
       }
       lds_barrier();  // ---- D: offset or slot ---------------------------------------------
@@ -742,10 +724,10 @@ pack_tile_kernel(PackTileArgs a) {
       const uint32_t pt = uniform32(s_patch);
       if (win == 0 && tid == 0 && pt != 0) a.out[ex - (pt >> 8)] = (uint8_t)pt;
     } else if (!windowed) {
-      const uint32_t slot = uniform32(s_slot);
-      if (slot != ~0u) {
-        // the tile's bytes to its slot: aligned 16-byte copies
-        u32x4* const dst = (u32x4*)(a.scr + slot * (uint64_t)kScr);
+      const uint64_t piece = uniform64(s_piece);
+      if (piece != ~0ull) {
+        // the tile's bytes to its arena piece: aligned 16-byte copies
+        u32x4* const dst = (u32x4*)(a.arena + piece);
         const uint32_t n16 = (agg + 15u) >> 4;
         for (uint32_t i = tid + opaque_zero(); i < n16; i += 64 * kWv)
           dst[i] = ((const u32x4*)stg)[1 + i];
@@ -789,711 +771,127 @@ pack_tile_kernel(PackTileArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// 1b. Direct pack: the same tile analysis and emission as pack_tile_kernel, but each tile's
-//     bytes go straight to their final offset -- no scratch slot, no scan, no placement launch,
-//     so P is written once.  Workgroups are persistent and take tiles by ticket (a tile only ever
-//     waits on lower tickets, whose workgroups are running).  The offset comes from a two-level
-//     decoupled look-back that a workgroup resolves one tile LATE: tile j's bytes stay staged in
-//     one of two LDS slots while the workgroup analyses and emits its next tile, and are copied
-//     out after that, by when the predecessors' byte counts have long been published.
-//       desc[t]   AGG | bytes of tile t (published right after its byte count)
-//       gword[g]  (tiles counted << 48) + bytes of group g (64 tiles), one atomic add per tile
-//       gincl[g]  INCL | bytes of groups 0..g, published by the tile that completed group g
-//     Offset of tile t = gincl of the nearest published group below t's group + the complete
-//     group sums in between + the AGGs of t's group before t.
-//     The count byte of a run still open at a tile end is written by the next tile (which alone
-//     knows where the run stops) at its own offset minus the distance the budget gives; the tile
-//     leaves that byte out of its stores.
-constexpr int kGroupD = 64;
-constexpr uint32_t kCapD = 10240;                  // staging window per slot (bytes)
-constexpr int kSlotDwD = (kPadF + kCapD + 64) / 4;
-constexpr uint64_t kGCount = 1ull << 48;
+// 2. Placement: one workgroup per group of kPlaceGroup consecutive tiles.  The offsets come from a
+//    scan of the tile byte counts (every tile's descriptor holds its count, or its inclusive
+//    prefix when the tile kernel resolved it): a group holding such an inclusive prefix knows
+//    every offset of the group from it at once (forward and backward from that tile); a group
+//    without one looks back over the groups before it (decoupled look-back on group descriptors,
+//    zero at rest).  Then the tiles whose bytes wait in the arena are copied to their offsets --
+//    one wave per tile, 16-byte stores -- with the count byte of a run the next tile closed, and
+//    the requested positions become output offsets.
+constexpr int kPlaceGroup = (int)kPackPlaceGroup;  // tiles per workgroup (lane l < 16 of wave 0:
+                                                   // tile 16g + l)
 
-#ifndef CPK_PACKD_WPE
-#define CPK_PACKD_WPE 4  // waves per SIMD (registers: 110 VGPRs); 4 workgroups of ~24 KiB LDS per CU
-#endif
-
-struct DirectLB {
-  uint64_t din, gi, gw;  // lane's in-group AGG, group INCL and group word (window 0)
-};
-
-__device__ __forceinline__ uint32_t direct_group_size(uint64_t g, uint64_t ntiles) {
-  const uint64_t left = ntiles - g * kGroupD;
-  return (uint32_t)(left < (uint64_t)kGroupD ? left : (uint64_t)kGroupD);
-}
-
-// First round of tile t's look-back, issued before the wave has other work to do.
-__device__ __forceinline__ void direct_lb_issue(const uint64_t* desc, const uint64_t* gincl,
-                                                const uint64_t* gword, uint64_t t, DirectLB& lb) {
-  const int l = lane_id();
-  const uint64_t g = t / kGroupD, k = t % kGroupD;
-  lb.din = (uint64_t)l < k ? load_agent(desc + g * kGroupD + l) : 0ull;
-  const int64_t G = (int64_t)g - 1 - l;
-  lb.gi = G >= 0 ? load_agent(gincl + G) : kDescIncl;  // before group 0: an inclusive zero
-  lb.gw = G >= 0 ? load_agent(gword + G) : 0ull;
-}
-
-// Resolves tile t's exclusive byte offset from the first round (polling what is not yet there).
-// Returns the offset and (*gpre) the bytes before t's group.
-__device__ uint64_t direct_lb_resolve(const uint64_t* desc, const uint64_t* gincl,
-                                      const uint64_t* gword, uint64_t ntiles, uint32_t* err,
-                                      uint64_t t, DirectLB lb, uint64_t* gpre) {
-  const int l = lane_id();
-  const uint64_t g = t / kGroupD, k = t % kGroupD;
-  uint32_t spins = 0;
-  // in-group: every AGG of the tiles before t in its group
-  while (ballot((uint64_t)l < k && (lb.din & kDescFlags) == 0)) {
-    if (++spins >= kSpinLimit) {
-      raise_error(err, kErrInternal);
-      return 0;
-    }
-    __builtin_amdgcn_s_sleep(1);
-    if ((uint64_t)l < k && (lb.din & kDescFlags) == 0)
-      lb.din = load_agent(desc + g * kGroupD + l);
-  }
-  const uint64_t ing = wave_sum64((uint64_t)l < k ? (lb.din & kDescValue) : 0ull);
-  // groups below g: the nearest published INCL, every group nearer than it complete
-  uint64_t acc = 0;
-  int64_t G0 = (int64_t)g - 1;
-  for (;;) {
-    const int64_t G = G0 - l;
-    const uint64_t sb = ballot((lb.gi & kDescFlags) == kDescIncl);
-    const int s = sb ? lowest_bit(sb) : 64;
-    const bool need = l < s && G >= 0;
-    const bool done = !need || (lb.gw >> 48) == direct_group_size((uint64_t)G, ntiles);
-    if (ballot(!done)) {
-      if (++spins >= kSpinLimit) {
-        raise_error(err, kErrInternal);
-        return 0;
-      }
-      __builtin_amdgcn_s_sleep(1);
-      lb.gi = G >= 0 ? load_agent(gincl + G) : kDescIncl;
-      lb.gw = G >= 0 ? load_agent(gword + G) : 0ull;
-      continue;
-    }
-    acc += wave_sum64(need ? (lb.gw & (kGCount - 1)) : 0ull);
-    if (s < 64) {
-      acc += readlane64(lb.gi, s) & kDescValue;
-      break;
-    }
-    G0 -= 64;
-    const int64_t Gn = G0 - l;
-    lb.gi = Gn >= 0 ? load_agent(gincl + Gn) : kDescIncl;
-    lb.gw = Gn >= 0 ? load_agent(gword + Gn) : 0ull;
-  }
-  *gpre = acc;
-  return acc + ing;
-}
-
-// Copies staged bytes [0, n) of a slot to o0 (absolute address A0 = o0) with 16-byte stores
-// shifted into place, byte stores at both ends and around the byte `hole` (left to the next
-// tile; ~0: none), by every thread of the workgroup.
-__device__ __forceinline__ void direct_copy_out(const uint32_t* slot, uint32_t wlo, uint32_t n,
-                                                uint8_t* o0, uint32_t hole) {
-  const int tid = (int)threadIdx.x;
-  const uint8_t* const sb8 = (const uint8_t*)slot + kPadF;
-  const uint64_t A0 = (uint64_t)(uintptr_t)o0;
-  const uint32_t head = min((uint32_t)((16u - (A0 & 15u)) & 15u), n);
-  const uint32_t hw = hole - wlo;  // window-relative (huge when none or outside)
-  if ((uint32_t)tid < head && (uint32_t)tid != hw) o0[tid] = sb8[tid];
-  const uint32_t nblk = (n - head) >> 4;
-  const uint32_t r = (kPadF + head) & 3u;
-  const uint32_t q0 = (kPadF + head) >> 2;
-  u32x4* const ob = (u32x4*)(o0 + head);
-  for (uint32_t i = tid; i < nblk; i += 64 * kWv) {
-    const uint32_t q = q0 + 4 * i;
-    const uint32_t v0 = slot[q], v1 = slot[q + 1], v2 = slot[q + 2], v3 = slot[q + 3],
-                   v4 = slot[q + 4];
-    u32x4 v;
-    v.x = __builtin_amdgcn_alignbyte(v1, v0, r);
-    v.y = __builtin_amdgcn_alignbyte(v2, v1, r);
-    v.z = __builtin_amdgcn_alignbyte(v3, v2, r);
-    v.w = __builtin_amdgcn_alignbyte(v4, v3, r);
-    const uint32_t bo = hw - (head + 16 * i);
-    if (bo < 16u) {
-      uint8_t* const ob8 = (uint8_t*)(ob + i);
-      const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (uint32_t j = 0; j < 16; j++)
-        if (j != bo) ob8[j] = (uint8_t)(vv[j >> 2] >> (8 * (j & 3)));
-    } else {
-      ob[i] = v;
-    }
-  }
-  const uint32_t tail = head + 16 * nblk;
-  if (tail + (uint32_t)tid < n && tail + (uint32_t)tid != hw) o0[tail + tid] = sb8[tail + tid];
-}
-
-// What a workgroup keeps of a tile between its emission and its (late) copy-out: in LDS, one
-// record per staging slot (registers stay with the tile being analysed).
-struct DirectPending {
-  uint64_t T;       // tile
-  uint64_t gsum;    // its group's bytes, when it completed the group (gdone)
-  uint32_t agg;     // its bytes
-  uint32_t hole;    // tile-relative byte left to the next tile (~0: none)
-  uint32_t patch;   // 0x100 | value of the previous tile's open-run count byte (0: none)
-  uint32_t dist;    // that byte's distance back from this tile's offset
-  uint32_t gdone;   // this tile completed its group: it publishes the group's INCL
-  uint32_t pad;
-};
-
-// The kernel's arguments re-read from the kernarg segment at every use (an opaque copy of its
-// address per use): a persistent loop otherwise keeps every argument it touches in SGPRs for the
-// whole kernel, and the pack's ~25 arguments beside the tile's own values spilled registers.
-typedef const __attribute__((address_space(4))) PackTileArgs KPackArgs;
-__device__ __forceinline__ KPackArgs* kargs() {
-  KPackArgs* p = (KPackArgs*)__builtin_amdgcn_kernarg_segment_ptr();
-  asm volatile("" : "+s"(p));
-  return p;
-}
-#define A_ (*kargs())
-
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CPK_PACKD_WPE))) void
-pack_direct_kernel(PackTileArgs args) {
-  (void)args;
-  __shared__ __attribute__((aligned(16))) uint32_t stg[2][kSlotDwD];
-  __shared__ __attribute__((aligned(16))) uint32_t trash[kWv][kTrashDw];
-  __shared__ uint64_t sel_tab[256];
-  __shared__ uint32_t s_sum[kWv];    // wave summaries (sum_pack)
-  __shared__ uint32_t s_bytes[kWv];  // wave byte counts
-  __shared__ uint32_t s_sexit[kWv];  // serial mode: exit of each wave
-  __shared__ uint32_t s_ticket[2];   // by iteration parity
-  __shared__ uint32_t s_texit, s_nsync;
-  __shared__ uint64_t s_off;
-  __shared__ DirectPending s_pend[2];  // by slot
-
+__global__ __launch_bounds__(256) void pack_place_kernel(PackTileArgs a) {
+  __shared__ uint64_t s_off[kPlaceGroup];
   const int tid = (int)threadIdx.x;
   const int l = lane_id();
   const int w = (int)uniform32(threadIdx.x >> 6);
-  const uint64_t N = A_.nwords;
-  const uint64_t nbitw = (N + 63) >> 6;
-  sel_tab[tid] = make_sel((uint32_t)tid);
-  for (int i = tid; i < 2 * kSlotDwD; i += 64 * kWv) (&stg[0][0])[i] = 0;
-  if (tid == 0) s_ticket[0] = atomicAdd(A_.ticket, 1u);
+  const uint64_t g = blockIdx.x;
+  const uint64_t T0 = g * kPlaceGroup;
+  if (w == 0) {
+    const uint64_t T = T0 + (uint64_t)l;
+    const bool in = l < kPlaceGroup && T < a.ntiles;
+    const uint64_t n = in ? a.tile_bytes[T] : 0ull;
+    const uint64_t dT = in ? load_agent(a.desc + T) : 0ull;
+    const bool incl = in && (dT & kDescFlags) == kDescIncl;
+    const uint64_t inc = wave_incl_sum64(n);  // bytes of the group's tiles up to this one
+    const uint64_t gsum = readlane64(inc, kPlaceGroup - 1);
+    // the last tile of the group whose inclusive prefix the tile kernel published
+    const uint64_t ib = ballot(incl);
+    uint64_t base;  // bytes before the group
+    if (ib) {
+      const int k = highest_bit(ib);
+      base = readlane64((dT & kDescValue) - inc, k);
+      if (l == 0) store_agent(a.gdesc + g, kDescIncl | (base + gsum));
+    } else {
+      if (l == 0) store_agent(a.gdesc + g, (g == 0 ? kDescIncl : kDescAgg) | gsum);
+      base = 0;
+      if (g > 0) {
+        pack_lookback(a.gdesc, g, &base, true, a.err);
+        if (l == 0) store_agent(a.gdesc + g, kDescIncl | (base + gsum));
+      }
+    }
+    if (in) s_off[l] = base + inc - n;
+    if (in && T + 1 == a.ntiles && a.total_out) *a.total_out = base + inc;
+  }
   __syncthreads();
-  uint64_t T = uniform32(s_ticket[0]);
-  uint32_t it = 0;  // iteration parity: the first iteration takes its next ticket into s_ticket[1]
-  uint32_t cur_slot = 0;
-  bool have_pend = false;  // the other slot holds a tile waiting for its copy-out
-
-  // wave 0: the offset of the tile in slot `ps` (first look-back round in lb), and the group
-  // INCL it publishes when it completed its group; then s_off
-  auto resolve = [&](uint32_t ps, DirectLB lb) {
-    const uint64_t pT = s_pend[ps].T;
-    uint64_t gp;
-    const uint64_t off = direct_lb_resolve(A_.desc, A_.gincl, A_.gword, A_.ntiles, A_.err, pT, lb, &gp);
-    if (l == 0) {
-      s_off = off;
-      if (s_pend[ps].gdone) store_agent(A_.gincl + pT / kGroupD, kDescIncl | (gp + s_pend[ps].gsum));
-    }
-  };
-  // every thread, after a barrier behind resolve(): the tile of slot ps copied out (copy), the
-  // previous tile's open-run count byte, the tile's requested positions made absolute, the total
-  auto finish = [&](uint32_t ps, bool copy) {
-    const uint64_t toff = uniform64(s_off);
-    const uint64_t pT = uniform64(s_pend[ps].T);
-    const uint32_t agg = uniform32(s_pend[ps].agg);
-    const bool fits = toff + agg <= A_.out_capacity;
-    if (copy && !fits) {
-      if (tid == 0) raise_error(A_.err, kErrCapacity);
-    } else if (copy && agg) {
-      direct_copy_out(stg[ps], 0, agg, A_.out + toff, uniform32(s_pend[ps].hole));
-    }
-    if (tid == 0) {
-      const uint32_t patch = s_pend[ps].patch, dist = s_pend[ps].dist;
-      if (patch && toff >= dist && toff - dist < A_.out_capacity)
-        A_.out[toff - dist] = (uint8_t)patch;
-      if (pT + 1 == A_.ntiles && A_.total_out) *A_.total_out = toff + agg;
-    }
-    if (A_.pos) {
-      const uint64_t i0 = A_.tile_first[pT];
-      const uint64_t i1 = pT + 1 < A_.ntiles ? A_.tile_first[pT + 1] : A_.npos + 1;
-      for (uint64_t i = i0 + (uint64_t)tid; i < i1; i += 64 * kWv) {
-        if (pT + 1 == A_.ntiles && A_.pos[i] >= N) {
-          A_.pos_out[i] = toff + agg;
-        } else {
-          const uint64_t rel = __hip_atomic_load(A_.pos_out + i, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-          A_.pos_out[i] = rel + toff;
-        }
+  // the tiles in the arena: one wave per tile
+  for (int j = w; j < kPlaceGroup; j += 4) {
+    const uint64_t T = T0 + (uint64_t)j;
+    if (T >= a.ntiles) break;
+    const uint64_t off = s_off[j];
+    const uint32_t n = (uint32_t)a.tile_bytes[T];
+    const uint64_t piece = a.tpiece[T];
+    if (off + n > a.out_capacity) {
+      if (l == 0) raise_error(a.err, kErrCapacity);
+    } else if (piece != ~0ull && n) {
+      // the previous tile's count byte that this tile finishes (the previous tile may have left
+      // it out, having written its bytes itself)
+      if (T > 0 && l == 0) {
+        const uint32_t ph = a.thole[T - 1], pp = a.tpatch[T];
+        if (ph != 0xffffffffu && pp) a.out[off - a.tile_bytes[T - 1] + ph] = (uint8_t)pp;
       }
-    }
-  };
-
-  while (T < A_.ntiles) {
-    // lane and wave ids re-derived per tile behind opaque moves: otherwise the compiler hoists
-    // every mask and comparison built from them out of the loop and spills them
-    int l = lane_id(), w = (int)uniform32(threadIdx.x >> 6);
-    asm volatile("" : "+v"(l));
-    asm volatile("" : "+s"(w));
-    it ^= 1u;
-    if (tid == 0) s_ticket[it] = atomicAdd(A_.ticket, 1u);
-    const uint64_t tbase = T * kTW;
-    const uint64_t tend = tbase + kTW < N ? tbase + kTW : N;
-    const uint64_t wbase = tbase + (uint64_t)kWW * w;
-    const int nvw = wbase >= N ? 0 : (int)((N - wbase) < (uint64_t)kWW ? (N - wbase) : kWW);
-    const uint64_t w0 = wbase + (uint64_t)kK * l;  // the lane's first word
-
-    // ---- loads: all issued before any is waited for ------------------------------------
-    uint32_t xlo[kK], xhi[kK];
-    if (nvw == kWW) {
-      const u32x4* src = (const u32x4*)(A_.words + w0);
-#pragma unroll
-      for (int i = 0; i < kK / 2; i++) {
-        const u32x4 v = src[i];
-        xlo[2 * i] = v.x;
-        xhi[2 * i] = v.y;
-        xlo[2 * i + 1] = v.z;
-        xhi[2 * i + 1] = v.w;
-      }
-    } else {
-#pragma unroll
-      for (int k = 0; k < kK; k++) {
-        const uint64_t x0 = A_.words[w0 + k < N ? w0 + k : N - 1];
-        const uint64_t x = w0 + k < N ? x0 : 0;  // words past the batch read as zero
-        xlo[k] = (uint32_t)x;
-        xhi[k] = (uint32_t)(x >> 32);
-      }
-    }
-    const uint64_t cbi = (wbase >> 6) + (uint64_t)(l >> 3);
-    const uint64_t cb0 = A_.chunk_bits[cbi < nbitw ? cbi : nbitw - 1];
-    const uint64_t xi = l == 0 ? (wbase > 0 ? wbase - 1 : 0) : (tend < N ? tend : N - 1);
-    const uint64_t xw0 = A_.words[xi < N ? xi : N - 1];
-    const uint64_t nbi = T + 1 + (uint64_t)opaque_zero();  // the next tile's start byte
-    const uint64_t nb0 = A_.tile_starts[nbi];
-    const uint64_t pidx = A_.pos ? A_.tile_first[T] : 0;
-    const uint64_t pi = pidx + l;
-    const bool pv = A_.pos && pi <= A_.npos;
-    const uint64_t p00 = (A_.pos ? A_.pos : A_.words)[pv ? pi : 0];
-    const uint64_t cbw = cbi < nbitw ? cb0 : 0;
-    const uint64_t xw = (wbase > 0 || l != 0) ? xw0 : 0;
-    const uint64_t p0 = pv ? p00 : ~0ull;
-    // ---- classes -----------------------------------------------------------------------
-    uint32_t Zm = 0, Rm = 0, Fm = 0, nzA = 0;
-    uint32_t tags[kK / 4] = {0, 0};
-#pragma unroll
-    for (int k = 0; k < kK; k++) {
-      const uint32_t tg = tag_of(xlo[k], xhi[k]);
-      const uint32_t nz = __popc(tg);
-      tags[k >> 2] |= tg << (8 * (k & 3));
-      Zm |= (tg == 0 ? 1u : 0u) << k;
-      Rm |= (nz >= 7 ? 1u : 0u) << k;
-      Fm |= (tg == 0xffu ? 1u : 0u) << k;
-      nzA |= nz << (4 * k);
-    }
-    const int kv = nvw - kK * l;
-    const uint32_t V = kv >= kK ? 0xffu : (kv <= 0 ? 0u : ((1u << kv) - 1u));
-    Zm &= V;
-    Rm &= V;
-    Fm &= V;
-    uint32_t zc = shfl32(Zm >> 7, l > 0 ? l - 1 : 0) & 1u;
-    uint32_t rc = shfl32(Rm >> 7, l > 0 ? l - 1 : 0) & 1u;
-    const uint32_t xtag = tag_of((uint32_t)xw, (uint32_t)(xw >> 32));
-    if (l == 0) {
-      zc = (wbase > 0 && xw == 0) ? 1u : 0u;
-      rc = (wbase > 0 && __popc(xtag) >= 7) ? 1u : 0u;
-    }
-    const uint32_t C = (uint32_t)(cbw >> (8 * (l & 7))) & 0xffu;
-    const uint32_t O = V & ~Zm & ~Rm;
-    const uint32_t SY =
-        (C | O | (Zm & ~((Zm << 1) | zc)) | (Rm & ~((Rm << 1) | rc)) | ~V) & 0xffu;
-    const bool lv = kv >= kK;
-
-    const uint64_t hs = ballot(SY != 0);
-    const bool simple = SY != 0 || Zm == 0xffu || Fm == 0xffu;
-    const uint64_t nonsimple = ballot(!simple && kv > 0);
-    const Cov c0 = cover8(Zm, Fm, Rm, SY, 0u, lv);
-    const uint32_t fs = SY ? (uint32_t)__builtin_ctz(SY) : 8u;
-    const uint64_t above = hs & ~mask_le(l);
-    const int ja = above ? lowest_bit(above) : 0;
-    const uint32_t fsa = shfl32(fs, ja);
-    uint32_t t_exit = 0;
-    auto publish_state = [&](uint32_t ex) {
-      const uint32_t lz = readlane32(Zm >> 7, 63) & 1u;
-      t_exit = ex | ((ex != 0 && !lz) ? 0x100u : 0u);
-      if (l == 0) store_agent32(A_.state + T, 0x80000000u | t_exit);
-    };
-    {
-      const uint32_t exit0 = hs != 0 ? wave_exit(0u, hs, nonsimple, c0.b_out, Zm, Fm) : 0u;
-      if (w == kWv - 1 && hs != 0) publish_state(exit0);
-      const int L0 = hs ? lowest_bit(hs) : 0;
-      const uint32_t fsl = shfl32(fs, L0);
-      const uint32_t fsw = hs ? (uint32_t)(kK * L0) + fsl : (uint32_t)kWW;
-      if (l == 0) s_sum[w] = sum_pack(hs != 0, nonsimple == 0, fsw, exit0);
-    }
-    bool next_sync = true;
-    if (w == kWv - 1) {
-      const uint32_t ntag = tag_of((uint32_t)xw0, (uint32_t)(xw0 >> 32));
-      const uint32_t nnz = __popc(ntag);
-      const bool nC = nb0 != 0;
-      const uint32_t lastZ = readlane32(Zm >> 7, 63) & 1u, lastR = readlane32(Rm >> 7, 63) & 1u;
-      const bool nZ = ntag == 0, nR = nnz >= 7;
-      const bool ns = nC || (!nZ && !nR) || (nZ && !lastZ) || (nR && !lastR);
-      next_sync = tend >= N || readlane32(ns ? 1u : 0u, 63) != 0;
-    }
-    __syncthreads();  // ---- A: wave summaries -------------------------------------------
-    if ((l & 7) == 0 && cbi < nbitw && cbw != 0) A_.chunk_bits[cbi] = 0;  // zero at rest
-    if (w == kWv - 1 && l == 0 && nb0) A_.tile_starts[nbi] = 0;
-
-    uint32_t sm[kWv];
-#pragma unroll
-    for (int v = 0; v < kWv; v++) sm[v] = uniform32(s_sum[v]);
-    bool serial = false;
-#pragma unroll
-    for (int v = 0; v < kWv; v++) serial |= !sum_sync(sm[v]) && !sum_simple(sm[v]);
-    const bool first_sync = sum_fsw(sm[0]) == 0;
-    auto tile_entry = [&]() -> uint32_t {
-      if (first_sync || T == 0) return 0u;
-      return wait_nonzero32(A_.state + T - 1, A_.err) & 0x1ffu;
-    };
-    const bool last_sync = sum_sync(sm[kWv - 1]);
-    uint32_t bT = 0, bw = 0;
-    bool have_bT = false;
-    if (!serial) {
-      int js = -1;
-#pragma unroll
-      for (int v = 0; v < kWv; v++)
-        if (sum_sync(sm[v])) js = v;
-      if (js >= 0 && !last_sync && w == kWv - 1) publish_state(sum_exit(sm[js]));
-      int jb = -1;
-#pragma unroll
-      for (int v = 0; v < kWv; v++)
-        if (v < w && sum_sync(sm[v])) jb = v;
-      if (jb >= 0) {
-        bw = sum_exit(sm[jb]);
-      } else {
-        bT = tile_entry();
-        have_bT = true;
-        bw = bT & 0xffu;
-      }
-      if (js < 0 && w == kWv - 1) publish_state(bw);
-    } else {
-#pragma nounroll
-      for (int v = 0; v < kWv; v++) {
-        if (w == v) {
-          if (v == 0) {
-            bT = tile_entry();
-            have_bT = true;
-            bw = bT & 0xffu;
-          } else {
-            bw = uniform32(s_sexit[v - 1]);
+      // count byte patched by the next tile (position, value) -- wave-uniform
+      const uint32_t hole = T + 1 < a.ntiles ? a.thole[T] : 0xffffffffu;
+      const uint32_t pv = hole != 0xffffffffu ? a.tpatch[T + 1] : 0u;
+      const uint8_t* const src = a.arena + piece;
+      uint8_t* const o0 = a.out + off;
+      const uint64_t A0 = (uint64_t)(uintptr_t)o0;
+      const uint64_t A1 = A0 + n;
+      const uint64_t al = (A0 + 15) & ~15ull;
+      const uint32_t head = (uint32_t)((al < A1 ? al : A1) - A0);  // bytes before 16-byte alignment
+      auto byte_at = [&](uint32_t q) -> uint8_t {
+        const uint8_t v = src[q];
+        return (pv && q == hole) ? (uint8_t)pv : v;
+      };
+      if ((uint32_t)l < head) o0[l] = byte_at(l);
+      if (A1 > al) {
+        const uint32_t body = (uint32_t)((A1 & ~15ull) - A0);
+        const uint32_t nblk = (body - head) >> 4;
+        // output block i = source bytes [head + 16i, head + 16i + 16): source dwords from
+        // (head >> 2) + 4i, shifted by head & 3 bytes
+        const uint32_t rr = head & 3u;
+        const uint32_t* const s32 = (const uint32_t*)src;
+        u32x4* const ob = (u32x4*)(o0 + head);
+        for (uint32_t i = l; i < nblk; i += 64) {
+          const uint32_t d = (head >> 2) + 4 * i;
+          const uint32_t v0 = s32[d], v1 = s32[d + 1], v2 = s32[d + 2], v3 = s32[d + 3],
+                         v4 = s32[d + 4];
+          u32x4 v;
+          v.x = __builtin_amdgcn_alignbyte(v1, v0, rr);
+          v.y = __builtin_amdgcn_alignbyte(v2, v1, rr);
+          v.z = __builtin_amdgcn_alignbyte(v3, v2, rr);
+          v.w = __builtin_amdgcn_alignbyte(v4, v3, rr);
+          const uint32_t b0 = head + 16 * i;
+          if (pv && hole >= b0 && hole < b0 + 16) {
+            const uint32_t q = hole - b0, sh = 8 * (q & 3), m = ~(0xffu << sh),
+                           x = (pv & 0xffu) << sh;
+            if (q < 4) v.x = (v.x & m) | x;
+            else if (q < 8) v.y = (v.y & m) | x;
+            else if (q < 12) v.z = (v.z & m) | x;
+            else v.w = (v.w & m) | x;
           }
-          const uint32_t ex =
-              hs != 0 ? sum_exit(sm[v]) : wave_exit(bw, hs, nonsimple, c0.b_out, Zm, Fm);
-          if (l == 0) s_sexit[v] = ex;
-          if (v == kWv - 1 && !last_sync) publish_state(ex);
+          ob[i] = v;
         }
-        __syncthreads();
+        if (body + (uint32_t)l < n) o0[body + l] = byte_at(body + l);
       }
     }
-    if (w == 0 && !have_bT) bT = tile_entry();
-
-    // ---- coverage, bytes, offsets --------------------------------------------------------
-    const uint32_t ent = lane_entries(bw, hs, nonsimple, c0.b_out, Zm, Fm);
-    const Cov cv = cover8(Zm, Fm, Rm, SY, ent, lv);
-    const uint32_t heads = V & ~cv.cov;
-    const uint32_t rh = cv.zh | cv.fh;
-    const uint32_t crf = cv.cov & Rm & ~Fm;
-    const uint32_t nzsum = (((nzA & 0x0f0f0f0fu) + ((nzA >> 4) & 0x0f0f0f0fu)) * 0x01010101u) >> 24;
-    const uint32_t bytes = nzsum + __popc(heads) + __popc(rh) + __popc(crf);
-    const uint32_t incl = wave_incl_sum32(bytes);
-    const uint32_t loff = incl - bytes;
-    if (l == 63) s_bytes[w] = incl;
-    if (w == kWv - 1 && l == 0) {
-      s_texit = t_exit;
-      s_nsync = next_sync ? 1u : 0u;
-    }
-    __syncthreads();  // ---- B: wave byte counts -----------------------------------------
-
-    uint32_t woff = 0, agg = 0, s0 = (uint32_t)kTW;
-#pragma unroll
-    for (int v = 0; v < kWv; v++) {
-      const uint32_t bv = uniform32(s_bytes[v]);
-      if (v < w) woff += bv;
-      agg += bv;
-      const uint32_t fv = sum_fsw(sm[v]);
-      if (fv < (uint32_t)kWW && (uint32_t)(kWW * v) + fv < s0) s0 = (uint32_t)(kWW * v) + fv;
-    }
-    uint32_t nsl = (uint32_t)kTW;
-    if (above) {
-      nsl = (uint32_t)(kWW * w + kK * ja) + fsa;
-    } else {
-#pragma unroll
-      for (int v = kWv - 1; v >= 0; v--)
-        if (v > w && sum_fsw(sm[v]) < (uint32_t)kWW) nsl = (uint32_t)(kWW * v) + sum_fsw(sm[v]);
-    }
-    // the tile's byte count goes out at once; the run open at its end, when the word after the
-    // tile goes on with its stretch, leaves its count byte to the next tile
-    DirectLB lb;
-    if (w == 0) {
-      const uint64_t g = T / kGroupD;
-      if (l == 0) {
-        store_agent(A_.desc + T, kDescAgg | agg);
-        const uint64_t old = atomicAdd((unsigned long long*)(A_.gword + g), kGCount | agg);
-        DirectPending& c = s_pend[cur_slot];
-        c.T = T;
-        c.agg = agg;
-        c.gdone = (old >> 48) + 1 == direct_group_size(g, A_.ntiles) ? 1u : 0u;
-        c.gsum = (old & (kGCount - 1)) + agg;
-        const uint32_t tb = s_texit;
-        const uint32_t hb = tb & 0xffu;
-        c.hole = (hb != 0 && !s_nsync) ? agg - 1u - ((tb & 0x100u) ? 8u * (255u - hb) : 0u)
-                                       : 0xffffffffu;
-        const uint32_t b = bT & 0xffu;
-        c.patch = (b != 0 && !first_sync && T > 0) ? 0x100u | (255u - b + (s0 < b ? s0 : b)) : 0u;
-        c.dist = 1u + ((bT & 0x100u) ? 8u * (255u - b) : 0u);
+    // requested positions: tile-relative offsets (pack_tile) + the tile's output offset;
+    // positions at or past the batch end (the last tile's share) take the total
+    if (a.pos) {
+      const uint64_t i0 = a.tile_first[T];
+      const uint64_t i1 = T + 1 < a.ntiles ? a.tile_first[T + 1] : a.npos + 1;
+      for (uint64_t i = i0 + l; i < i1; i += 64) {
+        if (T + 1 == a.ntiles && a.pos[i] >= a.nwords) a.pos_out[i] = off + n;
+        else a.pos_out[i] += off;
       }
-      if (have_pend) direct_lb_issue(A_.desc, A_.gincl, A_.gword, uniform64(s_pend[cur_slot ^ 1u].T), lb);  // resolved
-    }                                                                                // after the emission
-
-    // ---- requested positions (message starts) in this wave: bytes before them in the tile
-    if (A_.pos) {
-      const uint64_t wend = wbase + kWW < tend ? wbase + kWW : tend;
-      uint64_t idx = pidx;
-      for (bool first = true;; first = false) {
-        const uint64_t i = idx + l;
-        const uint64_t p = first ? p0 : (i <= A_.npos ? A_.pos[i] : ~0ull);
-        const bool in_t = p >= tbase && p < tend;
-        const bool in_w = p >= wbase && p < wend;
-        const uint32_t rel = in_w ? (uint32_t)(p - wbase) : 0u;
-        const int L = (int)(rel >> 3);
-        const uint32_t k = rel & 7u;
-        const uint32_t oL = shfl32(loff, L), hL = shfl32(heads, L), rL = shfl32(rh, L);
-        const uint32_t cL = shfl32(crf, L), aL = shfl32(nzA, L);
-        const uint32_t mk = (1u << k) - 1u;
-        const uint32_t an = aL & ((1u << (4 * k)) - 1u);
-        const uint32_t nb = (((an & 0x0f0f0f0fu) + ((an >> 4) & 0x0f0f0f0fu)) * 0x01010101u) >> 24;
-        const uint32_t before = nb + __popc(hL & mk) + __popc(rL & mk) + __popc(cL & mk);
-        if (in_w)  // tile-relative, made absolute at the copy-out (by another wave: agent scope)
-          __hip_atomic_store(A_.pos_out + i, (uint64_t)(woff + oL + before), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-        const uint64_t inm = ballot(in_t);
-        idx += __popcll(inm);
-        if (inm != ~0ull) break;
-      }
-    }
-
-    // ---- emission into this tile's slot -------------------------------------------------
-    const uint32_t nwin = agg <= kCapD ? 1u : (agg + kCapD - 1) / kCapD;
-    uint32_t* const wtr = trash[w] + l;
-    uint32_t* const slot = stg[cur_slot];
-    for (uint32_t win = 0; win < nwin; win++) {
-      const uint32_t wlo = win * kCapD;
-      const uint32_t whi = wlo + kCapD;
-      const bool windowed = nwin > 1;
-#pragma unroll
-      for (int k = 0; k < kK; k++) asm volatile("" : "+v"(xlo[k]), "+v"(xhi[k]));
-      uint32_t ecov = cv.cov, ezh = cv.zh, efh = cv.fh, eSY = SY, eR = Rm, enz = nzA, ensl = nsl;
-      uint32_t et0 = tags[0], et1 = tags[1];
-      asm volatile("" : "+v"(ecov), "+v"(ezh), "+v"(efh), "+v"(eSY), "+v"(eR), "+v"(enz));
-      asm volatile("" : "+v"(ensl), "+v"(et0), "+v"(et1));
-      const uint32_t etags[2] = {et0, et1};
-      uint32_t o = woff + loff;
-      const uint32_t lbase = (uint32_t)(kWW * w + kK * l);
-      uint64_t sel_next = sel_tab[etags[0] & 0xffu];
-#pragma unroll
-      for (int k = 0; k < kK; k++) {
-        const uint32_t lo = xlo[k], hi = xhi[k];
-        const uint32_t tg = (etags[k >> 2] >> (8 * (k & 3))) & 0xffu;
-        const uint64_t sel = sel_next;
-        if (k + 1 < kK) sel_next = sel_tab[(etags[(k + 1) >> 2] >> (8 * ((k + 1) & 3))) & 0xffu];
-        const uint32_t nz = (enz >> (4 * k)) & 15u;
-        const bool cvk = (ecov >> k) & 1, zhk = (ezh >> k) & 1, fhk = (efh >> k) & 1;
-        const uint32_t aft = eSY & (0xfeu << k);
-        const uint32_t ns = aft ? lbase + (uint32_t)__builtin_ctz(aft) : ensl;
-        const uint32_t c8 = min(ns - (lbase + (uint32_t)k) - 1u, 255u) << 8;
-        uint32_t r0 = __builtin_amdgcn_perm(hi, lo, (uint32_t)sel) | tg | (zhk ? c8 : 0u);
-        uint32_t r1 = __builtin_amdgcn_perm(hi, lo, (uint32_t)(sel >> 32));
-        uint32_t r2 = fhk ? ((hi >> 24) | c8) : 0u;
-        uint32_t L = 1u + nz + ((zhk || fhk) ? 1u : 0u);
-        if (cvk) {
-          r0 = lo;
-          r1 = hi;
-          r2 = 0;
-          L = ((eR >> k) & 1) ? 8u : 0u;
-        }
-        bool put = L != 0;
-        if (windowed) put = put && o < whi && o + L > wlo;
-        const uint32_t so = kPadF + o - wlo;
-        const uint32_t sh = 8u * (so & 3u);
-        uint32_t* const wp = put ? slot + (so >> 2) : wtr;
-        const uint64_t q01 = (((uint64_t)r1 << 32) | r0) << sh;
-        const uint64_t q12 = (((uint64_t)r2 << 32) | r1) << sh;
-        const uint32_t w3 = (uint32_t)(((uint64_t)r2 << sh) >> 32);
-        atomicOr(wp, (uint32_t)q01);
-        atomicOr(wp + 1, (uint32_t)(q01 >> 32));
-        atomicOr(wp + 2, (uint32_t)(q12 >> 32));
-        if (ballot(w3 != 0)) atomicOr(wp + 3, w3);
-        o += L;
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      if (!windowed) break;
-      // a tile too large for its slot (rare): the pending tile out first, then this tile's
-      // offset at once and its bytes window by window
-      if (win == 0) {
-        if (w == 0 && have_pend) resolve(cur_slot ^ 1u, lb);
-        __syncthreads();
-        if (have_pend) {
-          finish(cur_slot ^ 1u, true);
-          __syncthreads();
-          for (int i = tid; i < kSlotDwD; i += 64 * kWv) stg[cur_slot ^ 1u][i] = 0;
-          have_pend = false;
-        }
-        if (w == 0) {
-          DirectLB lb2;
-          direct_lb_issue(A_.desc, A_.gincl, A_.gword, T, lb2);
-          resolve(cur_slot, lb2);
-        }
-      }
-      __syncthreads();
-      const uint64_t toff = uniform64(s_off);
-      const uint32_t n = (whi < agg ? whi : agg) - wlo;
-      if (toff + agg <= A_.out_capacity) {
-        direct_copy_out(slot, wlo, n, A_.out + toff + wlo, uniform32(s_pend[cur_slot].hole));
-      } else if (win == 0 && tid == 0) {
-        raise_error(A_.err, kErrCapacity);
-      }
-      __syncthreads();
-      for (int i = tid; i < kSlotDwD; i += 64 * kWv) slot[i] = 0;
-      __syncthreads();
-    }
-    if (nwin > 1) {
-      finish(cur_slot, false);  // the previous tile's count byte, positions, total
-    } else {
-      // ---- the pending tile: its offset, its bytes out (its slot then free for the next tile)
-      if (have_pend) {
-        if (w == 0) resolve(cur_slot ^ 1u, lb);
-        __syncthreads();  // ---- C: emitted; the pending tile's offset known ----------------
-        finish(cur_slot ^ 1u, true);
-        __syncthreads();
-        for (int i = tid; i < kSlotDwD; i += 64 * kWv) stg[cur_slot ^ 1u][i] = 0;
-      }
-      have_pend = true;
-      cur_slot ^= 1u;
-    }
-    __syncthreads();  // the next ticket is in s_ticket[it]; the freed slot is zero
-    T = uniform32(s_ticket[it]);
-  }
-  // the last pending tile
-  if (have_pend) {
-    if (w == 0) {
-      DirectLB lb2;
-      direct_lb_issue(A_.desc, A_.gincl, A_.gword, uniform64(s_pend[cur_slot ^ 1u].T), lb2);
-      resolve(cur_slot ^ 1u, lb2);
-    }
-    __syncthreads();
-    finish(cur_slot ^ 1u, true);
-  }
-}
-
-#undef A_
-
-// ---------------------------------------------------------------------------------------------
-// 2. Placement: one wave per tile moves the tile's bytes from its scratch slot to their final
-//    place, writing the final count byte of a run the next tile closed, and turns the tile's
-//    requested positions into output offsets.  The tile's offset: its inclusive descriptor when
-//    the tile kernel resolved it (and then wrote the bytes itself), else a decoupled look-back
-//    over the tile kernel's byte counts (AGG) and this launch's inclusive prefixes -- no separate
-//    scan launch.  (A tile's bytes are a few KiB at most: a whole workgroup per tile spent more on
-//    its own start than on the copy.)
-__global__ __launch_bounds__(256) void pack_place_kernel(PackTileArgs a) {
-  const int l = lane_id();
-  const uint64_t T = (uint64_t)blockIdx.x * 4 + uniform32(threadIdx.x >> 6);
-  if (T >= a.ntiles) return;
-  const uint32_t n = (uint32_t)a.tile_bytes[T];
-  const uint64_t dT = uniform64(load_agent(a.desc + T));
-  const bool incl = (dT & kDescFlags) == kDescIncl;
-  uint64_t off;
-  if (incl) {
-    off = (dT & kDescValue) - n;
-  } else {
-    pack_lookback(a.desc, T, &off, true, a.err);
-    if (l == 0) store_agent(a.desc + T, kDescIncl | (off + n));
-  }
-  const uint64_t total = off + n;  // (the batch total on the last tile)
-  // (a tile whose offset was known in time wrote its bytes itself: INCL descriptor, no slot; the
-  // others are in their slots)
-  const uint32_t slot = a.tslot[T];
-  if (off + n > a.out_capacity) {
-    if (l == 0) raise_error(a.err, kErrCapacity);
-  } else if ((!incl || slot == kSmallTag) && n) {
-    // the previous tile's count byte that this tile finishes (the previous tile may have left it
-    // out, having written its bytes itself)
-    if (T > 0 && l == 0) {
-      const uint32_t ph = a.thole[T - 1], pp = a.tpatch[T];
-      if (ph != 0xffffffffu && pp) a.out[off - a.tile_bytes[T - 1] + ph] = (uint8_t)pp;
-    }
-    // count byte patched by the next tile (position, value) -- wave-uniform
-    const uint32_t hole = T + 1 < a.ntiles ? a.thole[T] : 0xffffffffu;
-    const uint32_t pv = hole != 0xffffffffu ? a.tpatch[T + 1] : 0u;
-    const uint8_t* const src = slot == kSmallTag ? a.scr_small + T * kSmallSlot
-                                                 : a.scr + slot * (uint64_t)kScr;
-    uint8_t* const o0 = a.out + off;
-    const uint64_t A0 = (uint64_t)(uintptr_t)o0;
-    const uint64_t A1 = A0 + n;
-    const uint64_t al = (A0 + 15) & ~15ull;
-    const uint32_t head = (uint32_t)((al < A1 ? al : A1) - A0);  // bytes before 16-byte alignment
-    auto byte_at = [&](uint32_t j) -> uint8_t {
-      const uint8_t v = src[j];
-      return (pv && j == hole) ? (uint8_t)pv : v;
-    };
-    if ((uint32_t)l < head) o0[l] = byte_at(l);
-    if (A1 > al) {
-      const uint32_t body = (uint32_t)((A1 & ~15ull) - A0);
-      const uint32_t nblk = (body - head) >> 4;
-      // output block i = source bytes [head + 16i, head + 16i + 16): source dwords from
-      // (head >> 2) + 4i, shifted by head & 3 bytes
-      const uint32_t rr = head & 3u;
-      const uint32_t* const s32 = (const uint32_t*)src;
-      u32x4* const ob = (u32x4*)(o0 + head);
-      for (uint32_t i = l; i < nblk; i += 64) {
-        const uint32_t d = (head >> 2) + 4 * i;
-        const uint32_t v0 = s32[d], v1 = s32[d + 1], v2 = s32[d + 2], v3 = s32[d + 3],
-                       v4 = s32[d + 4];
-        u32x4 v;
-        v.x = __builtin_amdgcn_alignbyte(v1, v0, rr);
-        v.y = __builtin_amdgcn_alignbyte(v2, v1, rr);
-        v.z = __builtin_amdgcn_alignbyte(v3, v2, rr);
-        v.w = __builtin_amdgcn_alignbyte(v4, v3, rr);
-        const uint32_t b0 = head + 16 * i;
-        if (pv && hole >= b0 && hole < b0 + 16) {
-          const uint32_t q = hole - b0, sh = 8 * (q & 3), m = ~(0xffu << sh),
-                         x = (pv & 0xffu) << sh;
-          if (q < 4) v.x = (v.x & m) | x;
-          else if (q < 8) v.y = (v.y & m) | x;
-          else if (q < 12) v.z = (v.z & m) | x;
-          else v.w = (v.w & m) | x;
-        }
-        ob[i] = v;
-      }
-      if (body + (uint32_t)l < n) o0[body + l] = byte_at(body + l);
     }
   }
-  // requested positions: tile-relative offsets (pack_tile) + the tile's output offset;
-  // positions at or past the batch end (the last tile's share) take the total
-  if (a.pos) {
-    const uint64_t i0 = a.tile_first[T];
-    const uint64_t i1 = T + 1 < a.ntiles ? a.tile_first[T + 1] : a.npos + 1;
-    for (uint64_t i = i0 + l; i < i1; i += 64) {
-      if (T + 1 == a.ntiles && a.pos[i] >= a.nwords) a.pos_out[i] = total;
-      else a.pos_out[i] += off;
-    }
-  }
-  if (T + 1 == a.ntiles && l == 0 && a.total_out) *a.total_out = total;
+  (void)tid;
 }
 
 }  // namespace
-
-static int cu_count() {
-  static int ncu = 0;
-  if (ncu == 0) {
-    int dev = 0, v = 0;
-    ncu = (hipGetDevice(&dev) == hipSuccess &&
-           hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-           v > 0) ? v : 256;
-  }
-  return ncu;
-}
 
 hipError_t launch_pack_tiles(const PackTileArgs& a, hipStream_t stream) {
   if (a.ntiles == 0) return hipSuccess;
@@ -1502,18 +900,9 @@ hipError_t launch_pack_tiles(const PackTileArgs& a, hipStream_t stream) {
   return hipGetLastError();
 }
 
-hipError_t launch_pack_direct(const PackTileArgs& a, hipStream_t stream) {
-  if (a.ntiles == 0) return hipSuccess;
-  if (a.ntiles >= (1ull << 31)) return hipErrorInvalidValue;
-  // persistent workgroups take tiles by ticket until none is left: as many as fit on the device
-  const uint64_t grid = (uint64_t)cu_count() * CPK_PACKD_WPE;
-  pack_direct_kernel<<<(unsigned)(a.ntiles < grid ? a.ntiles : grid), 256, 0, stream>>>(a);
-  return hipGetLastError();
-}
-
 hipError_t launch_pack_place(const PackTileArgs& a, hipStream_t stream) {
   if (a.ntiles == 0) return hipSuccess;
-  pack_place_kernel<<<(unsigned)((a.ntiles + 3) / 4), 256, 0, stream>>>(a);
+  pack_place_kernel<<<(unsigned)pack_place_groups(a.ntiles), 256, 0, stream>>>(a);
   return hipGetLastError();
 }
 

@@ -1797,6 +1797,7 @@ unpack_tiles_kernel(UnpackArgs a) {
   __syncthreads();
   const uint64_t t = (uint64_t)blockIdx.x * 4 + wv;
   if (t >= a.ntiles) return;
+  if (a.debug_skip & 512) return;  // diagnostic: the launch alone
   // batches of very long messages (whose look-backs reach back to the previous occupancy round):
   // the phases later tiles wait on (chain 0, the entry, the descriptors) ahead of other waves'
   // expansions in the SIMD's issue arbitration (C4 unpack_tiles 4.51 -> 4.21 ms; no gain on C2)
