@@ -36,12 +36,6 @@ __device__ __forceinline__ int lane_id() {
 
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 
-// Number of set bits of `m` at lanes below this lane.
-__device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
-  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                   __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-
 __device__ __forceinline__ uint32_t readlane32(uint32_t v, int l) {
   return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
 }
@@ -62,13 +56,6 @@ __device__ __forceinline__ uint32_t shfl32(uint32_t v, int src) {
 }
 __device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
   return ((uint64_t)shfl32((uint32_t)(v >> 32), src) << 32) | shfl32((uint32_t)v, src);
-}
-
-// Exclusive prefix sum over the wave of small values (0 <= v < 16) via 4 ballots.
-__device__ __forceinline__ uint32_t wave_excl_sum_small(uint32_t v, uint32_t* total) {
-  uint64_t b0 = ballot(v & 1), b1 = ballot(v & 2), b2 = ballot(v & 4), b3 = ballot(v & 8);
-  *total = (uint32_t)(__popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2) + 8 * __popcll(b3));
-  return mbcnt64(b0) + 2 * mbcnt64(b1) + 4 * mbcnt64(b2) + 8 * mbcnt64(b3);
 }
 
 // Inclusive wave scans by DPP: row_shr 1/2/4/8 inside each 16-lane row, then row_bcast:15 and
@@ -114,26 +101,6 @@ __device__ __forceinline__ uint64_t wave_incl_sum64(uint64_t v) {
 }
 __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
   return readlane64(wave_incl_sum64(v), 63);
-}
-
-// Tag byte of a word: bit i set <=> byte i non-zero (serialize-packed.c++:332-350), by SWAR.
-__device__ __forceinline__ uint32_t word_tag(uint64_t x) {
-  const uint64_t lo7 = 0x7f7f7f7f7f7f7f7full;
-  uint64_t m = (((x & lo7) + lo7) | x) & 0x8080808080808080ull;
-  return (uint32_t)(((m >> 7) * 0x0102040810204080ull) >> 56);
-}
-
-// Non-zero bytes of x packed to the low end, in byte order.
-__device__ __forceinline__ uint64_t compact_nonzero(uint64_t x) {
-  uint64_t out = 0;
-  uint32_t c = 0;
-#pragma unroll
-  for (int b = 0; b < 8; b++) {
-    uint64_t v = (x >> (8 * b)) & 0xff;
-    out |= v << (8 * c);
-    c += v != 0;
-  }
-  return out;
 }
 
 // Cross-lane hand-off through LDS inside one wave: the wave's LDS instructions execute in
@@ -382,209 +349,6 @@ __device__ __forceinline__ uint64_t lookback(const uint64_t* desc, uint64_t t, u
     j -= 64 * K;
   }
   return excl;
-}
-
-__device__ __forceinline__ uint64_t stamp_now() {
-  // no s_waitcnt: a phase ends where the wave gets to, memory still in flight (forcing the wait
-  // at every mark serialised the loads the phases are meant to overlap)
-  asm volatile("" ::: "memory");
-  const uint64_t t = __builtin_amdgcn_s_memtime();
-  asm volatile("" ::: "memory");
-  return t;
-}
-
-// ---------------------------------------------------------------------------------------------
-// Two-level decoupled look-back.
-//
-// Tiles are grouped 64 to a group.  Every tile publishes its aggregate (AGG) in desc[t]; the
-// group's last tile combines the group's 64 aggregates in order and publishes the group
-// aggregate in gdesc[g] (an arrival ticket instead -- whichever tile counts last -- measured
-// slower: the winner's extra round trip made the group aggregates later), and publishes the
-// group's inclusive prefix there once it knows its own.  A tile then needs one
-// hop over the tiles before it in its group and, unless an inclusive prefix is found there, one
-// hop over up to 64 group descriptors (4096 tiles): with thousands of tiles in flight the
-// inclusive front no longer has to crawl one window per fabric round trip.
-//
-// Combination (segmented when seg_bit != 0): a value carrying seg_bit restarts the sum (its
-// aggregate counts only from a message start inside the tile / group).
-constexpr int kGroup = 64;
-
-__device__ __forceinline__ uint64_t seg_combine(uint64_t before, uint64_t after, uint64_t seg_bit) {
-  // value of (before ++ after)
-  if (seg_bit && (after & seg_bit)) return after;
-  return (before & seg_bit) | ((before & ~seg_bit) + (after & ~seg_bit));
-}
-
-// Each lane loads its descriptor and polls it (only lanes whose entry is not ready) until
-// ready, sleeping between polls.
-__device__ __forceinline__ uint64_t load_ready(const uint64_t* p, bool use, uint32_t* err) {
-  if (!use) return kDescIncl;
-  uint64_t d = load_agent(p);
-  uint32_t spins = 0;
-  while ((d & kDescFlags) == 0) {
-    if (++spins >= kSpinLimit) {
-      raise_error(err, kErrInternal);
-      return kDescIncl;
-    }
-    __builtin_amdgcn_s_sleep(2);
-    d = load_agent(p);
-  }
-  return d;
-}
-
-// Sum (segmented) of lanes 0..k of v, in lane order = distance order (lane 0 nearest): i.e.
-// value of entries (k, ..., 1, 0) concatenated oldest first.
-__device__ __forceinline__ uint64_t reduce_nearest(uint64_t v, int k, uint64_t seg_bit) {
-  const int l = lane_id();
-  // the nearest stop with seg bit among lanes <= k: everything farther is dropped
-  const uint64_t segs = seg_bit ? ballot(l <= k && (v & seg_bit)) : 0;
-  const int s = segs ? lowest_bit(segs) : k;  // farthest lane that contributes
-  const uint64_t contrib = (l <= s) ? (v & ~seg_bit) : 0;
-  const uint64_t sum = wave_sum64(contrib);
-  return (segs ? seg_bit : 0) | sum;
-}
-
-// Publishes tile t's aggregate; the group's last tile also combines the group's aggregates (it
-// waits for its in-group predecessors, all running in the same round of the persistent order)
-// and publishes the group aggregate.  gdesc[g] has that single writer (AGG here, then INCL in
-// publish_incl), so no ticket atomics or CAS are needed.
-__device__ __forceinline__ void publish_agg(uint64_t* desc, uint64_t* gdesc, uint32_t* gcnt,
-                                            uint64_t t, uint64_t ntiles, uint64_t agg,
-                                            uint64_t seg_bit, uint32_t* err) {
-  (void)gcnt;
-  const int l = lane_id();
-  if (l == 0) store_agent(desc + t, kDescAgg | agg);
-  const uint64_t g = t / kGroup;
-  const uint64_t g0 = g * kGroup;
-  const bool last_of_group = (t + 1) % kGroup == 0 || t + 1 == ntiles;
-  if (!last_of_group) return;
-  const uint32_t n_in = (uint32_t)(t - g0 + 1);
-  // lane i = tile t - i (lane 0: this tile's own aggregate)
-  const bool use = l > 0 && (uint32_t)l < n_in;
-  const uint64_t d = l == 0 ? (kDescAgg | agg) : load_ready(desc + (t - (uint64_t)(use ? l : 0)),
-                                                            use, err);
-  const bool stop = use && (d & kDescFlags) == kDescIncl;
-  const uint64_t sb = ballot(stop);
-  const int k = sb ? lowest_bit(sb) : (int)n_in - 1;
-  const uint64_t v = reduce_nearest((l == 0 || use) ? (d & kDescValue) : 0, k, seg_bit);
-  if (l == 0) {
-    const uint64_t nv = sb ? (kDescIncl | (v & ~seg_bit)) : (kDescAgg | v);
-    store_agent(gdesc + g, nv);
-  }
-}
-
-// Exclusive prefix of tile t (after publish_agg).  Publishes nothing.
-__device__ __forceinline__ uint64_t lookback2(const uint64_t* desc, const uint64_t* gdesc,
-                                              uint64_t t, uint64_t seg_bit, uint32_t* err,
-                                              uint64_t* dbg = nullptr) {
-  // dbg (diagnostic builds only): [0] look-backs that went past the group, [1] group windows
-  // read, [2] cycles in the in-group hop, [3] cycles in the group hops
-  const uint64_t t0 = dbg ? stamp_now() : 0;
-  const int l = lane_id();
-  const uint64_t g = t / kGroup;
-  const int j = (int)(t - g * kGroup);  // predecessors inside the group
-  uint64_t excl = 0;                    // value of everything after the stop found so far
-  {
-    const bool use = l < j;
-    const uint64_t d = load_ready(desc + (t - 1 - (uint64_t)(use ? l : 0)), use, err);
-    const bool stop = use && (((d & kDescFlags) == kDescIncl) || (seg_bit && (d & seg_bit)));
-    const uint64_t sb = ballot(stop);
-    const int k = sb ? lowest_bit(sb) : j - 1;
-    if (j > 0) excl = reduce_nearest(use ? (d & kDescValue) : 0, k, seg_bit);
-    if (dbg) dbg[2] += stamp_now() - t0;
-    if (sb || g == 0) return excl & ~seg_bit;
-    if (excl & seg_bit) return excl & ~seg_bit;
-  }
-  const uint64_t t1 = dbg ? stamp_now() : 0;
-  if (dbg) dbg[0]++;
-  // group-level: groups g-1, g-2, ...
-  int64_t G = (int64_t)g - 1;
-  while (G >= 0) {
-    if (dbg) dbg[1]++;
-    const bool use = G - l >= 0;
-    if (dbg) {  // diagnostic: group descriptors not yet published at the first read
-      const uint64_t d0 = use ? load_agent(gdesc + (G - l)) : kDescIncl;
-      dbg[1] += 1000 * (uint64_t)__popcll(ballot((d0 & kDescFlags) == 0));
-    }
-    const uint64_t d = load_ready(gdesc + (use ? G - l : 0), use, err);
-    const bool stop = !use || ((d & kDescFlags) == kDescIncl) || (seg_bit && (d & seg_bit));
-    const uint64_t sb = ballot(stop);
-    const int k = sb ? lowest_bit(sb) : 63;
-    const uint64_t v = reduce_nearest(use ? (d & kDescValue) : 0, k, seg_bit);
-    excl = seg_combine(v, excl, seg_bit);
-    if (sb) break;
-    G -= 64;
-  }
-  if (dbg) dbg[3] += stamp_now() - t1;
-  return excl & ~seg_bit;
-}
-
-// After lookback2: publish tile t's inclusive value (and the group's, from its last tile).
-__device__ __forceinline__ void publish_incl(uint64_t* desc, uint64_t* gdesc, uint64_t t,
-                                             uint64_t ntiles, uint64_t incl) {
-  if (lane_id() != 0) return;
-  store_agent(desc + t, kDescIncl | incl);
-  const uint64_t g = t / kGroup;
-  if ((t + 1) % kGroup == 0 || t + 1 == ntiles) store_agent(gdesc + g, kDescIncl | incl);
-}
-
-// Diagnostic phase stamps (env CPK_STAMPS=1 selects a separately instantiated kernel; the
-// production kernels contain no stamp).  Lane 0 adds per-phase s_memtime deltas into its own
-// debug buffer, never into outputs.
-template <bool ON>
-struct Stamps {
-  // deltas accumulate in registers; flush() adds them to the debug buffer once (a global atomic
-  // per mark would put its own round trip into every measured phase)
-  unsigned long long* buf;
-  uint64_t last;
-  uint64_t acc[kStampSlots];
-  __device__ __forceinline__ void start(unsigned long long* b) {
-    if constexpr (ON) {
-      buf = b;
-      for (int i = 0; i < kStampSlots; i++) acc[i] = 0;
-      last = stamp_now();
-    }
-  }
-  __device__ __forceinline__ void restart() {
-    if constexpr (ON) last = stamp_now();
-  }
-  __device__ __forceinline__ void mark(int slot) {
-    if constexpr (ON) {
-      const uint64_t now = stamp_now();
-      acc[slot] += now - last;
-      last = now;
-    }
-  }
-  __device__ __forceinline__ void flush() {
-    if constexpr (ON) {
-      unsigned long long* row = buf + kStampSlots * (blockIdx.x & (kStampRows - 1));
-      if (lane_id() == 0 && buf)
-        for (int i = 0; i < kStampSlots; i++)
-          if (acc[i]) atomicAdd(row + i, (unsigned long long)acc[i]);
-    }
-  }
-};
-
-// Blocks of `threads` threads the whole GPU keeps resident for kernel `fn`: the occupancy API per
-// CU, capped by what the kernel's SGPR allocation allows (the API over-reports by one block per
-// CU for SGPR-heavy kernels on ROCm 7.2: MI355X_MICROARCH.md, "Occupancy API one block/CU high";
-// 800 SGPRs per SIMD, a wave holds ceil(sgprs/16)*16 + 16), minus `margin`, times the CU count.
-// Persistent kernels size their grid with it so that every wave of the grid runs concurrently
-// (a tile only ever waits on lower tiles).
-inline unsigned resident_blocks(const void* fn, int threads, int margin, int sgprs = 112) {
-  int dev = 0, cus = 0, per_cu = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return 256;
-  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-    cus = 256;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, 0) != hipSuccess)
-    per_cu = 1;
-  const int waves_per_block = (threads + 63) / 64;
-  const int sgpr_waves = 800 / (((sgprs + 15) / 16) * 16 + 16);    // per SIMD
-  const int sgpr_blocks = sgpr_waves * 4 / waves_per_block;         // 4 SIMDs per CU
-  if (per_cu > sgpr_blocks) per_cu = sgpr_blocks;
-  per_cu -= margin;
-  if (per_cu < 1) per_cu = 1;
-  return (unsigned)(per_cu * cus);
 }
 
 }  // namespace cpk

@@ -58,12 +58,6 @@ constexpr int kB = (int)kUnpackTileBytes;  // 4096
 constexpr int kPad = 16;
 constexpr int kDead = 1 << 24;  // chain ran into the end of the batch
 
-#ifndef CPK_PRIO
-#define CPK_PRIO 0  // 1: raised wave priority until the tile's descriptors are out, every batch
-#endif
-#ifndef CPK_PIPE
-#define CPK_PIPE 0  // 1: plain-tile batches read the next batch's record bytes ahead
-#endif
 
 
 #ifdef CPK_DIAG
@@ -653,24 +647,22 @@ __device__ __forceinline__ void run_jobs(const UnpackArgs& a, const RunJob& job,
   }
 }
 
-#ifndef CPK_SHORT_RUN
-#define CPK_SHORT_RUN 4  // runs of at most this many words are written by their own lane
-#endif
-// Runs of a batch: a short run (at most CPK_SHORT_RUN words, zero or raw from the staged tile --
+constexpr uint32_t kShortRunGeneral = 4;  // runs of at most this many words: their own lane
+// Runs of a batch: a short run (at most kShortRunGeneral words, zero or raw from the staged tile --
 // most runs of dense data, where a zero or raw stretch rarely lasts) is written by its own lane,
 // all such lanes together, one word per step; longer runs and raw runs outside the staged bytes
 // go through run_jobs (the whole wave per run, coalesced).
 __device__ __forceinline__ void run_jobs_batch(const UnpackArgs& a, RunJob job, const uint8_t* d,
                                                uint64_t dbase, uint32_t dlen) {
-  if (CPK_SHORT_RUN > 0 && a.words) {
+  if (a.words) {
     const bool in_lds = !job.raw || (job.src >= dbase && job.src - dbase + 8ull * job.n + 4 <= dlen);
-    const bool sh = job.n != 0 && job.n <= (uint32_t)CPK_SHORT_RUN && in_lds;
+    const bool sh = job.n != 0 && job.n <= kShortRunGeneral && in_lds;
     if (ballot(sh)) {
       const uint32_t n = sh ? job.n : 0u;
       const uint32_t o0 = (uint32_t)(job.src - dbase);
       const uint32_t* const d32 = (const uint32_t*)d;
 #pragma unroll
-      for (uint32_t k = 0; k < (uint32_t)CPK_SHORT_RUN; k++) {
+      for (uint32_t k = 0; k < kShortRunGeneral; k++) {
         if (!ballot(k < n)) break;
         if (k < n) {
           uint64_t v = 0;
@@ -1115,93 +1107,9 @@ __device__ __forceinline__ uint64_t wait_nonzero64(const uint64_t* p, uint32_t* 
   return readlane64(v, 0);
 }
 
-// The look-back of a flat stream decode: the nearest INCL within 64 tiles, then tile by tile
-// towards t - 1 the true exit -- each tile's AGG when its true entry is its optimistic one (the
-// predecessor's chain-0 exit), its desc2 when it is the second candidate -- and the words.  A
-// tile matching neither is waited for (its INCL); so is a missing descriptor.
-__device__ uint64_t lookback_flat(const UnpackArgs& a, uint64_t t, uint32_t* xprev) {
-  const int l = lane_id();
-  uint32_t spins = 0;
-  for (;;) {
-    const int64_t u = (int64_t)t - 1 - l;  // lane l: tile u, nearest first
-    // before tile 0: an inclusive zero whose exit enters tile 0 at byte 0
-    const uint64_t dv = u >= 0 ? load_agent(a.desc + u) : (kDescIncl | kOkBit);
-    const uint64_t sb = ballot((dv & kDescFlags) == kDescIncl);
-    const int k = sb ? lowest_bit(sb) : 64;
-    const uint64_t nb = ballot(l < k && (dv & kDescFlags) == 0);
-    const uint64_t* wait_on = nullptr;
-    uint64_t want = 0;  // 0: non-zero; kDescIncl: INCL
-    if (nb) {
-      CPK_DIAG_ONLY(diag_add(27, 1));
-      wait_on = a.desc + (t - 1 - lowest_bit(nb));
-    } else if (k == 64) {
-      CPK_DIAG_ONLY(diag_add(26, 1));
-      wait_on = a.desc + (t - 64);
-      want = kDescIncl;
-    } else {
-      const uint64_t d2 = (u >= 1 && l < k) ? load_agent(a.desc2 + u) : 0;
-      const uint32_t xq = (u >= 1 && l < k) ? (load_agent32(a.x0p + u - 1) & 0x7fffffffu) : 0;
-      const uint64_t dk = readlane64(dv, k);
-      uint32_t X = desc_exit(dk);
-      uint64_t acc = dk & kWordsMask;
-      int stuck = -1;
-      bool need2 = false;
-      for (int j = k - 1; j >= 0; j--) {
-        const uint64_t dj = readlane64(dv, j);
-        const uint32_t E = X >= (uint32_t)kDead ? (uint32_t)kB : X - (uint32_t)kB;
-        const uint32_t xqj = readlane32(xq, j);
-        const uint32_t E1 = xqj >= (uint32_t)kDead ? (uint32_t)kB : xqj - (uint32_t)kB;
-        if (E == E1) {
-          X = desc_exit(dj);
-          acc += dj & kWordsMask;
-          continue;
-        }
-        const uint64_t d2j = readlane64(d2, j);
-        if (d2j == 0) {
-          stuck = j;
-          need2 = true;
-          break;
-        }
-        if (d2j != kD2None && E == (uint32_t)((d2j >> kD2EntryShift) & 0x1fffu)) {
-          X = desc_exit(d2j);
-          acc += d2j & kD2WordsMask;
-          continue;
-        }
-        CPK_DIAG_ONLY(diag_add(22, 1); diag_add(23, E < 16); diag_add(24, E >= 64);
-                      diag_add(25, d2j == kD2None));
-        stuck = j;
-        break;
-      }
-      if (stuck < 0) {
-        *xprev = X;
-        return acc;
-      }
-      wait_on = (need2 ? a.desc2 : a.desc) + (t - 1 - stuck);
-      want = need2 ? 0 : kDescIncl;
-    }
-    if (l == 0) {
-      for (;;) {
-        const uint64_t v = load_agent(wait_on);
-        if (want ? (v & kDescFlags) == want : v != 0) break;
-        if (++spins >= kSpinLimit) break;
-        __builtin_amdgcn_s_sleep(1);
-      }
-    }
-    spins = uniform32(spins);
-    if (spins >= kSpinLimit) {
-      raise_error(a.err, kErrInternal);
-      *xprev = (uint32_t)kB;
-      return 0;
-    }
-  }
-}
-
-#ifndef CPK_FLAT_SCAN
-#define CPK_FLAT_SCAN 1  // 0: the serial flat look-back (one window, waits for the INCL 64 back)
-#endif
 constexpr int kFlatWindows = 16;
 
-// Flat look-back by composition (CPK_FLAT_SCAN).  A tile's true entry is one of two candidates
+// Flat look-back by composition.  A tile's true entry is one of two candidates
 // when the look-back can resolve it: a (E1, the entry the predecessor's chain-0 exit gives: the
 // tile's AGG holds its exit and words) or b (E2, its desc2 candidate).  So each tile is a transfer
 // function from {a, b} to the state its exit gives the next tile ({a, b} or fail) plus words, and
@@ -1801,7 +1709,7 @@ unpack_tiles_kernel(UnpackArgs a) {
   // batches of very long messages (whose look-backs reach back to the previous occupancy round):
   // the phases later tiles wait on (chain 0, the entry, the descriptors) ahead of other waves'
   // expansions in the SIMD's issue arbitration (C4 unpack_tiles 4.51 -> 4.21 ms; no gain on C2)
-  if (CPK_PRIO || a.prio) __builtin_amdgcn_s_setprio(2);
+  if (a.prio) __builtin_amdgcn_s_setprio(2);
   CPK_DIAG_ONLY(uint64_t ck[7]; uint64_t wk[7]; ck[0] = clock64(); wk[0] = wall_clock64());
   // the header launch is done: its scan descriptors go back to zero for the next call
   for (uint64_t i = t + a.ntiles * (uint64_t)l; i < a.hdr_nblocks; i += 64 * a.ntiles)
@@ -1967,7 +1875,7 @@ unpack_tiles_kernel(UnpackArgs a) {
     uint32_t xprev = xp;
     CPK_DIAG_ONLY(ck[4] = clock64(); wk[4] = wall_clock64());
     if (!(a.debug_skip & 8)) {
-      if constexpr (FLAT) excl = CPK_FLAT_SCAN ? lookback_flat_scan(a, t, &xprev) : lookback_flat(a, t, &xprev);
+      if constexpr (FLAT) excl = lookback_flat_scan(a, t, &xprev);
       else excl = lookback_tiles(a, t, &xprev);
     }
     CPK_DIAG_ONLY(ck[5] = clock64(); wk[5] = wall_clock64());
@@ -1998,7 +1906,7 @@ unpack_tiles_kernel(UnpackArgs a) {
 
   // ---- expansion -------------------------------------------------------------------------
   if (a.debug_skip & 256) return;  // diagnostic: + the entry and the look-back
-  if (CPK_PRIO || a.prio) __builtin_amdgcn_s_setprio(0);
+  if (a.prio) __builtin_amdgcn_s_setprio(0);
   expand_records(a, A, d, aux, dep_tab, tm, excl, win, mfirst, mlast, msw);
   // a fused single-tile batch: this wave is the whole call -- its error word for the host, last:
   // its stores done, then a system-scope release
