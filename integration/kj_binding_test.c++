@@ -13,7 +13,11 @@
 //      PackedFdMessageReader message(fd) (borrowed int fd, then an owned kj::OwnFd after a
 //      MallocMessageBuilder write), writePackedMessage over an unbuffered kj::OutputStream,
 //      PackedMessageReader over kj::FdInputStream, getRoot<AnyPointer>() walked to the two people
-//      the sample writes (ids 123 / 456, names, emails, phone counts).
+//      the sample writes (ids 123 / 456, names, emails, phone counts);
+//   4. the RoundTrip tests of serialize-packed-test.c++:225-585 restated schema-free (AnyPointer):
+//      forced segment counts 1/2/3/7/10 (its TestMessageBuilder), lazy one-byte reads and scratch
+//      space, two messages from one stream, the all-zero message in at most 7 bytes, and a
+//      5023-byte text field (raw runs over 255 words).
 //
 //   kj_binding_test <tests/golden dir>     -> prints "binding ok: N checks", exit 0
 #include <capnp/any.h>
@@ -279,6 +283,181 @@ void addressbook(const std::string& dir) {
   }
 }
 
+// ---- serialize-packed-test.c++:225-585, schema-free --------------------------------------------
+// The reference's round trips build TestAllTypes (test.capnp) messages; here the same shapes are
+// built through capnp::AnyPointer / AnyStruct: a root struct with data, text, blobs, nested
+// structs and lists (many separately allocated objects), an all-zero struct, and a 5023-byte
+// text field (raw runs past the 255-word cap).
+
+// serialize-packed-test.c++:225-254 TestMessageBuilder: minimum-size segments until the desired
+// count, then one large segment (so a message of enough objects has exactly that many segments).
+class SegmentCountBuilder final : public capnp::MallocMessageBuilder {
+ public:
+  explicit SegmentCountBuilder(uint n)
+      : capnp::MallocMessageBuilder(0, capnp::AllocationStrategy::FIXED_SIZE), left_(n) {}
+  kj::ArrayPtr<capnp::word> allocateSegment(uint minimumSize) override {
+    if (left_ <= 1) {
+      if (left_ == 1) --left_;
+      else over_ = true;
+      return capnp::MallocMessageBuilder::allocateSegment(capnp::SUGGESTED_FIRST_SEGMENT_WORDS);
+    }
+    --left_;
+    return capnp::MallocMessageBuilder::allocateSegment(minimumSize);
+  }
+  bool exact() const { return left_ == 0 && !over_; }
+
+ private:
+  uint left_;
+  bool over_ = false;
+};
+
+// the stand-in for initTestMessage (test-util.c++): more than ten separately allocated objects
+void fill_message(capnp::MessageBuilder& b) {
+  auto root = b.getRoot<capnp::AnyPointer>().initAsAnyStruct(6, 8);
+  auto data = root.getDataSection();
+  for (size_t i = 0; i < data.size(); i++) data[i] = (kj::byte)((i % 3) ? i * 37 + 1 : 0);
+  auto ptrs = root.getPointerSection();
+  ptrs[0].setAs<capnp::Text>("foo");
+  ptrs[1].setAs<capnp::Text>("a text field long enough to make a raw run of several words");
+  const kj::byte blob[] = {0, 1, 2, 0, 0, 0, 0, 0, 7, 8, 9, 10, 11, 12, 13, 0, 0, 0, 0, 0, 0, 0, 0,
+                           0, 255, 254, 0, 0, 0, 0, 0, 1};
+  ptrs[2].setAs<capnp::Data>(kj::arrayPtr(blob, sizeof blob));
+  auto s1 = ptrs[3].initAsAnyStruct(2, 2);
+  s1.getDataSection()[0] = 5;
+  s1.getPointerSection()[0].setAs<capnp::Text>("nested");
+  auto s2 = s1.getPointerSection()[1].initAsAnyStruct(1, 1);
+  s2.getDataSection()[3] = 0x80;
+  s2.getPointerSection()[0].setAs<capnp::Text>("deeper");
+  auto ls = ptrs[4].initAsListOfAnyStruct(2, 1, 5);
+  for (uint i = 0; i < 5; i++) {
+    ls[i].getDataSection()[i] = (kj::byte)(i + 1);
+    ls[i].getPointerSection()[0].setAs<capnp::Text>(i % 2 ? "odd" : "even element");
+  }
+  auto l8 = ptrs[5].initAs<capnp::List<uint64_t>>(20);
+  for (uint i = 0; i < 20; i++) l8.set(i, i % 4 == 0 ? 0 : 0x0101010101010101ull * i + i);
+  ptrs[6].setAs<capnp::Text>("bar");
+  ptrs[7].setAs<capnp::Text>("baz");
+}
+
+// the segments of a builder read back through a PackedMessageReader from `in`
+void check_builder_segments(capnp::MessageReader& r, capnp::MessageBuilder& b,
+                            const std::string& name) {
+  auto segs = b.getSegmentsForOutput();
+  for (uint i = 0; i < segs.size(); i++) {
+    auto s = r.getSegment(i);
+    check(s.size() == segs[i].size() &&
+              memcmp(s.begin(), segs[i].begin(), s.size() * sizeof(capnp::word)) == 0,
+          name + ": segment " + std::to_string(i));
+  }
+  check(r.getSegment(segs.size()) == nullptr, name + ": segment count");
+}
+
+// one RoundTrip* test: writePackedMessage, computeUnpackedSizeInWords against
+// computeSerializedSizeInWords, then a PackedMessageReader over a whole buffer, over a buffer
+// handed out one byte at a time (the Lazy tests: TestPipe(1)) and with a scratch space (the
+// ScratchSpace tests)
+std::vector<kj::byte> round_trip(capnp::MessageBuilder& b, const std::string& name) {
+  kj::VectorOutputStream out;
+  cpk_kj::writePackedMessage(out, b);
+  auto bytes = out.getArray();
+  std::vector<kj::byte> packed(bytes.begin(), bytes.end());
+  check(capnp::computeSerializedSizeInWords(b) ==
+            cpk_kj::computeUnpackedSizeInWords(kj::arrayPtr(packed.data(), packed.size())),
+        name + ": computeUnpackedSizeInWords == computeSerializedSizeInWords");
+  {
+    kj::ArrayInputStream in(kj::arrayPtr(packed.data(), packed.size()));
+    cpk_kj::PackedMessageReader r(in);
+    check_builder_segments(r, b, name);
+  }
+  {
+    FragmentedInput in(kj::arrayPtr(packed.data(), packed.size()), 1);
+    cpk_kj::PackedMessageReader r(in);
+    check_builder_segments(r, b, name + " lazy");
+    check(in.remaining() == 0, name + " lazy: consumed");
+  }
+  {
+    kj::ArrayInputStream in(kj::arrayPtr(packed.data(), packed.size()));
+    capnp::word scratch[1024];
+    cpk_kj::PackedMessageReader r(in, capnp::ReaderOptions(), kj::arrayPtr(scratch, 1024));
+    check_builder_segments(r, b, name + " scratch");
+  }
+  return packed;
+}
+
+void reference_round_trips() {
+  // RoundTrip, RoundTripOddSegmentCount (7), RoundTripEvenSegmentCount (10), and 2 and 3
+  for (uint n : {1u, 2u, 3u, 7u, 10u}) {
+    SegmentCountBuilder b(n);
+    fill_message(b);
+    check(b.exact() && b.getSegmentsForOutput().size() == n,
+          "segment count " + std::to_string(n) + " forced");
+    round_trip(b, "RoundTrip " + std::to_string(n) + " segments");
+  }
+  // RoundTripTwoMessages: two messages back to back on one stream, two readers in turn
+  {
+    SegmentCountBuilder b1(1), b2(1);
+    fill_message(b1);
+    auto r2 = b2.getRoot<capnp::AnyPointer>().initAsAnyStruct(0, 1);
+    r2.getPointerSection()[0].setAs<capnp::Text>("Second message.");
+    kj::VectorOutputStream out;
+    cpk_kj::writePackedMessage(out, b1);
+    cpk_kj::writePackedMessage(out, b2);
+    auto bytes = out.getArray();
+    check(capnp::computeSerializedSizeInWords(b1) + capnp::computeSerializedSizeInWords(b2) ==
+              cpk_kj::computeUnpackedSizeInWords(bytes),
+          "RoundTripTwoMessages: computeUnpackedSizeInWords");
+    kj::ArrayInputStream in(bytes);
+    {
+      cpk_kj::PackedMessageReader r(in);
+      check_builder_segments(r, b1, "RoundTripTwoMessages: first");
+    }
+    {
+      cpk_kj::PackedMessageReader r(in);
+      auto t = r.getRoot<capnp::AnyPointer>().getAs<capnp::AnyStruct>().getPointerSection()[0];
+      check(std::string(t.getAs<capnp::Text>().cStr()) == "Second message.",
+            "RoundTripTwoMessages: second");
+    }
+    check(in.tryGetReadBuffer().size() == 0, "RoundTripTwoMessages: consumed");
+  }
+  // RoundTripAllZero (1 segment): "Segment table packs to 2 bytes. Root pointer packs to 3 bytes.
+  // Content packs to 2 bytes (zero span)" -- at most 7 bytes; then the 3- and 2-segment shapes
+  // with two nested all-zero structs (initStructField().initStructField())
+  {
+    SegmentCountBuilder b(1);
+    b.getRoot<capnp::AnyPointer>().initAsAnyStruct(6, 20);
+    auto packed = round_trip(b, "RoundTripAllZero");
+    check(packed.size() <= 7, "RoundTripAllZero: at most 7 bytes (" +
+                                  std::to_string(packed.size()) + ")");
+  }
+  for (uint n : {3u, 2u}) {
+    SegmentCountBuilder b(n);
+    auto root = b.getRoot<capnp::AnyPointer>().initAsAnyStruct(6, 20);
+    root.getPointerSection()[0].initAsAnyStruct(6, 20).getPointerSection()[0].initAsAnyStruct(6, 20);
+    check(b.exact() && b.getSegmentsForOutput().size() == n,
+          "all-zero segment count " + std::to_string(n) + " forced");
+    round_trip(b, "RoundTripAllZero " + std::to_string(n) + " segments");
+  }
+  // RoundTripHugeString: a 5023-byte text field of 'x' (raw runs over 255 words), 1, 3 and 2
+  // segments
+  for (uint n : {1u, 3u, 2u}) {
+    std::string huge(5023, 'x');
+    SegmentCountBuilder b(n);
+    auto root = b.getRoot<capnp::AnyPointer>().initAsAnyStruct(6, 20);
+    root.getPointerSection()[0].setAs<capnp::Text>(huge.c_str());
+    // (the 2- and 3-segment shapes: objects after the text spill into further segments)
+    if (n > 1) root.getPointerSection()[1].initAsAnyStruct(1, 1).getPointerSection()[0]
+                   .setAs<capnp::Text>("after");
+    check(!(n > 1) || b.exact(), "huge string segment count " + std::to_string(n));
+    round_trip(b, "RoundTripHugeString " + std::to_string(n) + " segments");
+    kj::VectorOutputStream out;
+    cpk_kj::writePackedMessage(out, b);
+    kj::ArrayInputStream in(out.getArray());
+    cpk_kj::PackedMessageReader r(in);
+    auto t = r.getRoot<capnp::AnyPointer>().getAs<capnp::AnyStruct>().getPointerSection()[0];
+    check(std::string(t.getAs<capnp::Text>().cStr()) == huge, "RoundTripHugeString text");
+  }
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -301,6 +480,8 @@ int main(int argc, char** argv) {
   fixture(dir, "binary", "packed");
   fixture(dir, "segmented", "segmented-packed");
   addressbook(dir);
-  std::printf("binding ok: %d checks (%d KATs, 2 fixtures, addressbook)\n", checks, k);
+  reference_round_trips();
+  std::printf("binding ok: %d checks (%d KATs, 2 fixtures, addressbook, the RoundTrip tests of "
+              "serialize-packed-test.c++:225-585)\n", checks, k);
   return 0;
 }

@@ -2,7 +2,7 @@
 # Instruction attribution of the unpack tile kernel by phase: one rocprofv3 counter pass (SQ
 # instruction and cycle counters + kernel trace) of tools/ablate.py per CPK_DEBUG_SKIP value in
 # SKIPS (diagnostic only: outputs are meaningless with bits set).
-#   gpurun -- 'SKIPS="0 4 16 32 48" bash tools/gpu_ablate_pmc.sh TAG c2'
+#   gpurun -- 'SKIPS="0 4 16 32 48" bash tools/gpu_ablate_pmc.sh TAG c2'  (PMC: another counter set)
 set -o pipefail
 TAG=${1:-abp}
 CFG=${2:-c2}
@@ -11,7 +11,7 @@ mkdir -p "$R/gpurun_out"
 export TMPDIR=/tmp
 cd /tmp
 for s in ${SKIPS:-0}; do
-  CPK_DEBUG_SKIP=$s timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT \
+  CPK_DEBUG_SKIP=$s timeout -s KILL 120 rocprofv3 --pmc ${PMC:-SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT} \
     --kernel-trace --output-format csv -d "$R/gpurun_out/${TAG}_s$s" -o run \
     -- python3 "$R/tools/ablate.py" $CFG > "$R/gpurun_out/${TAG}_s$s.log" 2>&1 \
     || { echo "skip $s failed"; tail -5 "$R/gpurun_out/${TAG}_s$s.log"; exit 1; }
