@@ -54,7 +54,7 @@ struct PackTileArgs {
 // counts (kPlaceGroup tiles per workgroup), arena pieces -> out
 hipError_t launch_pack_tiles(const PackTileArgs& a, hipStream_t stream);
 hipError_t launch_pack_place(const PackTileArgs& a, hipStream_t stream);
-constexpr uint64_t kPackPlaceGroup = 16;
+constexpr uint64_t kPackPlaceGroup = 64;
 inline uint64_t pack_place_groups(uint64_t ntiles) {
   return (ntiles + kPackPlaceGroup - 1) / kPackPlaceGroup;
 }

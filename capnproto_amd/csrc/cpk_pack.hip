@@ -779,11 +779,16 @@ pack_tile_kernel(PackTileArgs a) {
 //    zero at rest).  Then the tiles whose bytes wait in the arena are copied to their offsets --
 //    one wave per tile, 16-byte stores -- with the count byte of a run the next tile closed, and
 //    the requested positions become output offsets.
-constexpr int kPlaceGroup = (int)kPackPlaceGroup;  // tiles per workgroup (lane l < 16 of wave 0:
-                                                   // tile 16g + l)
+constexpr int kPlaceGroup = (int)kPackPlaceGroup;  // tiles per workgroup (lane l of wave 0:
+                                                   // tile 64g + l)
 
 __global__ __launch_bounds__(256) void pack_place_kernel(PackTileArgs a) {
   __shared__ uint64_t s_off[kPlaceGroup];
+  __shared__ uint64_t s_piece[kPlaceGroup];
+  __shared__ uint32_t s_n[kPlaceGroup];
+  __shared__ uint32_t s_list[kPlaceGroup];  // group-relative indices of the tiles in the arena
+  __shared__ uint32_t s_narena;
+  __shared__ uint64_t s_pos[2];  // the group's requested positions: [s_pos[0], s_pos[1])
   const int tid = (int)threadIdx.x;
   const int l = lane_id();
   const int w = (int)uniform32(threadIdx.x >> 6);
@@ -794,6 +799,11 @@ __global__ __launch_bounds__(256) void pack_place_kernel(PackTileArgs a) {
     const bool in = l < kPlaceGroup && T < a.ntiles;
     const uint64_t n = in ? a.tile_bytes[T] : 0ull;
     const uint64_t dT = in ? load_agent(a.desc + T) : 0ull;
+    const uint64_t piece = in ? a.tpiece[T] : ~0ull;
+    // the group's positions: from its first tile's first to the next group's first
+    const bool pl = a.pos && l < 2;
+    const uint64_t pT = T0 + (uint64_t)l * kPlaceGroup;
+    const uint64_t pf = pl ? (pT < a.ntiles ? a.tile_first[pT] : a.npos + 1) : 0ull;
     const bool incl = in && (dT & kDescFlags) == kDescIncl;
     const uint64_t inc = wave_incl_sum64(n);  // bytes of the group's tiles up to this one
     const uint64_t gsum = readlane64(inc, kPlaceGroup - 1);
@@ -812,20 +822,43 @@ __global__ __launch_bounds__(256) void pack_place_kernel(PackTileArgs a) {
         if (l == 0) store_agent(a.gdesc + g, kDescIncl | (base + gsum));
       }
     }
-    if (in) s_off[l] = base + inc - n;
+    const uint64_t off = base + inc - n;
+    const bool arena = in && piece != ~0ull && n != 0 && off + n <= a.out_capacity;
+    const uint64_t am = ballot(arena);
+    if (in) {
+      s_off[l] = off;
+      s_n[l] = (uint32_t)n;
+      s_piece[l] = piece;
+      if (off + n > a.out_capacity) raise_error(a.err, kErrCapacity);
+    }
+    if (arena) s_list[__popcll(am & ((1ull << l) - 1ull))] = (uint32_t)l;
+    if (l == 0) s_narena = (uint32_t)__popcll(am);
+    if (pl) s_pos[l] = pf;
     if (in && T + 1 == a.ntiles && a.total_out) *a.total_out = base + inc;
   }
   __syncthreads();
+  // requested positions: tile-relative offsets (pack_tile) + the tile's output offset; a position
+  // belongs to the tile holding its word, positions at or past the batch end (the last tile's
+  // share) take the total
+  if (a.pos) {
+    const uint64_t i1 = s_pos[1];
+    for (uint64_t i = s_pos[0] + (uint64_t)tid; i < i1; i += 256) {
+      const uint64_t p = a.pos[i];
+      const uint64_t T = min(p / kPackTileWords, a.ntiles - 1);
+      const uint32_t j = (uint32_t)(T - T0);
+      if (j >= (uint32_t)kPlaceGroup) continue;  // (unsorted positions: not this group's)
+      if (T + 1 == a.ntiles && p >= a.nwords) a.pos_out[i] = s_off[j] + s_n[j];
+      else a.pos_out[i] += s_off[j];
+    }
+  }
   // the tiles in the arena: one wave per tile
-  for (int j = w; j < kPlaceGroup; j += 4) {
-    const uint64_t T = T0 + (uint64_t)j;
-    if (T >= a.ntiles) break;
+  const uint32_t na = s_narena;
+  for (uint32_t q = (uint32_t)w; q < na; q += 4) {
+    const uint32_t j = s_list[q];
+    const uint64_t T = T0 + j;
     const uint64_t off = s_off[j];
-    const uint32_t n = (uint32_t)a.tile_bytes[T];
-    const uint64_t piece = a.tpiece[T];
-    if (off + n > a.out_capacity) {
-      if (l == 0) raise_error(a.err, kErrCapacity);
-    } else if (piece != ~0ull && n) {
+    const uint32_t n = s_n[j];
+    {
       // the previous tile's count byte that this tile finishes (the previous tile may have left
       // it out, having written its bytes itself)
       if (T > 0 && l == 0) {
@@ -835,7 +868,7 @@ __global__ __launch_bounds__(256) void pack_place_kernel(PackTileArgs a) {
       // count byte patched by the next tile (position, value) -- wave-uniform
       const uint32_t hole = T + 1 < a.ntiles ? a.thole[T] : 0xffffffffu;
       const uint32_t pv = hole != 0xffffffffu ? a.tpatch[T + 1] : 0u;
-      const uint8_t* const src = a.arena + piece;
+      const uint8_t* const src = a.arena + s_piece[j];
       uint8_t* const o0 = a.out + off;
       const uint64_t A0 = (uint64_t)(uintptr_t)o0;
       const uint64_t A1 = A0 + n;
@@ -875,16 +908,6 @@ __global__ __launch_bounds__(256) void pack_place_kernel(PackTileArgs a) {
           ob[i] = v;
         }
         if (body + (uint32_t)l < n) o0[body + l] = byte_at(body + l);
-      }
-    }
-    // requested positions: tile-relative offsets (pack_tile) + the tile's output offset;
-    // positions at or past the batch end (the last tile's share) take the total
-    if (a.pos) {
-      const uint64_t i0 = a.tile_first[T];
-      const uint64_t i1 = T + 1 < a.ntiles ? a.tile_first[T + 1] : a.npos + 1;
-      for (uint64_t i = i0 + l; i < i1; i += 64) {
-        if (T + 1 == a.ntiles && a.pos[i] >= a.nwords) a.pos_out[i] = off + n;
-        else a.pos_out[i] += off;
       }
     }
   }

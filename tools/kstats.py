@@ -14,6 +14,6 @@ for d in sys.argv[1:]:
         n = r["Name"]
         if "cpk::" not in n or "copy_kernel" in n or "gen_" in n or "fill_kernel" in n:
             continue
-        short = n.split("(")[0].replace("void ", "").replace("cpk::(anonymous namespace)::", "")
+        short = n.replace("void ", "").replace("cpk::(anonymous namespace)::", "").split("(")[0]
         out.append(f"{short}={float(r['AverageNs']) / 1e3:.1f}")
     print(d.rstrip("/").split("/")[-1], " ".join(out))
