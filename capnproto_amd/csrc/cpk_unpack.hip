@@ -1509,11 +1509,7 @@ __device__ __forceinline__ void expand_lean(const UnpackArgs& a, uint64_t A, con
       // bytes p .. p + 12: tag, up to 8 data bytes, count byte
       const uint32_t q = p >> 2, sh = p & 3u;
       const uint32_t q0 = d32[q], q1 = d32[q + 1], q2 = d32[q + 2], q3 = d32[q + 3];
-      // a raw run's first word: bytes p + 10 .. p + 17 (read for every lane, used by 0xff records
-      // whose word lies in the staged bytes)
-      const uint32_t rb = p + 10u, rq = rb >> 2, rs = rb & 3u;
-      const uint32_t rqc = rq < kStaged / 4 - 2 ? rq : kStaged / 4 - 3;
-      const uint32_t r0 = d32[rqc], r1 = d32[rqc + 1], r2 = d32[rqc + 2];
+      const uint32_t rb = p + 10u;  // a raw run's first word: bytes p + 10 .. p + 17
       const uint32_t b0w = __builtin_amdgcn_alignbyte(q1, q0, sh);  // bytes p .. p+3
       const uint32_t b1w = __builtin_amdgcn_alignbyte(q2, q1, sh);  // p+4 .. p+7
       const uint32_t b2w = __builtin_amdgcn_alignbyte(q3, q2, sh);  // p+8 .. p+11
@@ -1525,16 +1521,29 @@ __device__ __forceinline__ void expand_lean(const UnpackArgs& a, uint64_t A, con
       uint32_t cnt = z ? ((b0w >> 8) & 0xffu) : 0u;
       cnt = f ? ((b2w >> 8) & 0xffu) : cnt;
       const uint32_t w = act ? 1u + cnt : 0u;
-      const uint32_t inc = wave_incl_sum32(w);
-      const uint32_t o = inc - w;  // words of the batch before the record
-      const uint32_t btot = readlane32(inc, 63);
+      // words of the batch before the record: a batch of single-word records (no run) needs no
+      // scan -- the active lanes are a prefix
+      const uint64_t runs = ballot(act && cnt != 0);
+      uint32_t o = (uint32_t)l, btot = (uint32_t)__popcll(ballot(act));
+      if (runs) {
+        const uint32_t inc = wave_incl_sum32(w);
+        o = inc - w;
+        btot = readlane32(inc, 63);
+      }
       const uint64_t msb = ballot(is_ms);
       const uint32_t wlo = __builtin_amdgcn_perm(dhi, dlo, (uint32_t)sel);
       const uint32_t whi = __builtin_amdgcn_perm(dhi, dlo, (uint32_t)(sel >> 32));
       const uint64_t word = ((uint64_t)whi << 32) | wlo;
-      const uint64_t rw = f ? (((uint64_t)__builtin_amdgcn_alignbyte(r2, r1, rs) << 32) |
-                               __builtin_amdgcn_alignbyte(r1, r0, rs))
-                            : 0ull;
+      // a raw run's first word (only a batch with a raw run of words reads it)
+      uint64_t rw = 0;
+      if (ballot(f && cnt != 0)) {
+        const uint32_t rq = rb >> 2, rs = rb & 3u;
+        const uint32_t rqc = rq < kStaged / 4 - 2 ? rq : kStaged / 4 - 3;
+        const uint32_t r0 = d32[rqc], r1 = d32[rqc + 1], r2 = d32[rqc + 2];
+        rw = f ? (((uint64_t)__builtin_amdgcn_alignbyte(r2, r1, rs) << 32) |
+                  __builtin_amdgcn_alignbyte(r1, r0, rs))
+               : 0ull;
+      }
       // the run's first word is in the staged bytes (always for a zero run)
       const bool inl = !f || rb + 12u <= kStaged;  // (its three dwords unclamped)
       uint64_t* wp;  // the record's word
