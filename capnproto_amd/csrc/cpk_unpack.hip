@@ -1031,6 +1031,7 @@ __device__ uint64_t lookback_tiles(const UnpackArgs& a, uint64_t t, uint32_t* xp
   for (;;) {
     const int64_t idx = base - l;
     const bool in = l < width;
+    CPK_DIAG_ONLY(diag_add(22, 1));
     // before tile 0: an inclusive zero whose exit enters tile 0 at byte 0
     const uint64_t dv = !in ? 0ull : (idx >= 0 ? load_agent(a.desc + idx) : (kDescIncl | kOkBit));
     const uint64_t stt = dv & kDescFlags;
@@ -1060,6 +1061,7 @@ __device__ uint64_t lookback_tiles(const UnpackArgs& a, uint64_t t, uint32_t* xp
     }
     // one lane polls the blocking descriptor (sleeping between polls), then the window is read
     // again from the nearest tile
+    CPK_DIAG_ONLY(diag_add(want_incl ? 24 : 23, 1); const uint32_t sp0 = uniform32(spins));
     if (l == 0) {
       for (;;) {
         const uint64_t f = load_agent(wait_on) & kDescFlags;
@@ -1069,6 +1071,7 @@ __device__ uint64_t lookback_tiles(const UnpackArgs& a, uint64_t t, uint32_t* xp
       }
     }
     spins = uniform32(spins);
+    CPK_DIAG_ONLY(diag_add(25, spins - sp0));
     if (spins >= kSpinLimit) {
       raise_error(a.err, kErrInternal);
       break;
@@ -2011,9 +2014,10 @@ hipError_t launch_unpack_stage(int stage, const UnpackArgs& a, hipStream_t strea
 //  14 tiles whose optimistic entry's exit is not their chain-0 exit (no ok bit)
 //  16..21 clock cycles (s_memtime) per phase: staging and message window, chain 0, waiting for
 //  the predecessor's chain-0 exit, the optimistic entry, the look-back, the expansion
-//  22..27 flat look-back events: stuck (entry matches no candidate), ... with entry < 16, ... with
-//  entry >= 64, ... with no second candidate, waits for an INCL (no INCL within reach, or an entry
-//  matching no candidate), waits for a descriptor not published yet
+//  22..25 message look-back: windows read, waits for a descriptor not published yet, waits for
+//  an INCL (an AGG without the ok bit), polls
+//  26/27 flat look-back: waits for an INCL (no INCL within reach, or an entry matching no
+//  candidate), waits for a descriptor not published yet
 //  28/29 composed flat look-back: windows read before an INCL wait, windows read to resolve
 extern "C" int cpk_debug_diag(uint64_t* out, int reset) {
   if (hipDeviceSynchronize() != hipSuccess) return 10;

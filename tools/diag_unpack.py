@@ -22,7 +22,7 @@ NAMES = ["tiles", "walk0_trips", "walk0_lane_steps", "rewalk_trips", "rewalk_lan
          "settle_rounds", "enter_calls", "merge_steps", "merge_capped", "entry_mismatch",
          "opt_walked", "has_start", "f_cand", "f_used", "not_ok", "-",
          "clk_stage", "clk_chain0", "clk_wait_x0p", "clk_entry", "clk_lookback", "clk_expand",
-         "stuck", "stuck_e16", "stuck_e64", "stuck_nod2", "incl_waits", "unpublished",
+         "lb_windows", "lb_wait_unpub", "lb_wait_incl", "lb_polls", "incl_waits", "unpublished",
          "win_before_wait", "win_resolved"]
 
 L = capnproto_amd.load_library()
