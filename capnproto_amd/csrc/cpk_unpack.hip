@@ -722,11 +722,14 @@ __device__ __forceinline__ void load_starts(const UnpackArgs& a, int64_t mw, Msg
   w.ok = 0;
 }
 
-// Packed bytes [A, A + kB + kPad) of the batch (zero past the end) in 16-byte pieces per lane:
-// loaded into registers first (stage_load) so that other independent loads can be issued before
-// the wave waits for them, then written to LDS (stage_store).
+// Packed bytes [A - kPre, A + kB + kPad) of the batch (zero outside it) in 16-byte pieces per
+// lane: loaded into registers first (stage_load) so that other independent loads can be issued
+// before the wave waits for them, then written to LDS (stage_store; d[-kPre] is byte A - kPre).
+// The kPre bytes before the tile are the predecessor's last bytes: the walk through them guesses
+// the tile's entry.
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-constexpr int kStageVecs = (kB + kPad + 1023) / 1024;
+constexpr int kPre = 64;
+constexpr int kStageVecs = (kPre + kB + kPad + 1023) / 1024;
 struct Staged {
   u32x4 v[kStageVecs];
 };
@@ -736,7 +739,7 @@ __device__ __forceinline__ void stage_store(const Staged& sg, uint8_t* d) {
 #pragma unroll
   for (int k = 0; k < kStageVecs; k++) {
     const int o = 16 * (64 * k + l);
-    if (o < kB + kPad) *(u32x4*)(d + o) = sg.v[k];
+    if (o < kPre + kB + kPad) *(u32x4*)(d - kPre + o) = sg.v[k];
   }
   lane_handoff();  // other lanes read these bytes next
 }
@@ -749,14 +752,17 @@ __device__ __forceinline__ void stage_load(const UnpackArgs& a, uint64_t A, Stag
   for (int k = 0; k < kStageVecs; k++) {
     const int o = 16 * (64 * k + l);
     sg.v[k] = (u32x4){0, 0, 0, 0};
-    if (o < kB + kPad) {
+    if (o < kPre + kB + kPad) {
+      // bytes [b, b + 16) of the batch, b = A - kPre + o (may be negative: tile 0's prefix)
+      const int64_t b = (int64_t)A - kPre + o;
       u32x4 v = {0, 0, 0, 0};
-      if (aligned && A + o + 16 <= P) {
-        v = *(const u32x4*)(a.packed + A + o);
+      if (aligned && b >= 0 && (uint64_t)b + 16 <= P) {
+        v = *(const u32x4*)(a.packed + b);
       } else {
         uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0;
         for (int i = 0; i < 16; i++) {
-          const uint32_t bv = (A + o + i < P) ? (uint32_t)a.packed[A + o + i] : 0u;
+          const bool inb = b + i >= 0 && (uint64_t)(b + i) < P;
+          const uint32_t bv = inb ? (uint32_t)a.packed[b + i] : 0u;
           const uint32_t sv = bv << (8 * (i & 3));
           if (i < 4) q0 |= sv;
           else if (i < 8) q1 |= sv;
@@ -768,12 +774,6 @@ __device__ __forceinline__ void stage_load(const UnpackArgs& a, uint64_t A, Stag
       sg.v[k] = v;
     }
   }
-}
-
-__device__ __forceinline__ void stage_tile(const UnpackArgs& a, uint64_t A, uint8_t* d) {
-  Staged sg;
-  stage_load(a, A, sg);
-  stage_store(sg, d);
 }
 
 // Message-start bitmap of tile [A, A + kB) into ms[64] (bit = tile-relative byte; the batch end
@@ -866,25 +866,47 @@ __device__ __forceinline__ uint64_t make_dep(uint32_t tag) {
 // Tile descriptors (desc[t], zero until published).  A tile's exit is the first position of its
 // chain at or past the tile end; its words are those of its records (message starts excepted,
 // below).  States:
-//   AGG   the tile's exit and words for its optimistic entry -- the one the predecessor's chain 0
-//         leads to (x0p[t - 1], published as soon as the predecessor has settled chain 0);
+//   AGG   the tile's exit and words for its guessed entry, with that entry: the guess is where the
+//         chain through the 64 bytes before the tile lands in it (chains synchronise within a
+//         few records), so it needs nothing from the predecessor tile -- no wait before the AGG;
 //   INCL  its true exit and the inclusive words of the message at the tile end.
-// The ok bit says the exit is the tile's chain-0 exit: then the next tile's optimistic entry is
-// its true one, provided this tile's own entry was.  A tile holding a message start publishes
-// INCL at once: its exit and the words after its last start do not depend on its entry.
+// An AGG is right when its entry is where its predecessor's (right) exit leads: the look-back
+// checks that on neighbouring descriptors.  A guess can be wrong (a raw run longer than the
+// kPre bytes: they parse as garbage records), and a wrong AGG would hold every later tile's
+// look-back until its own look-back published INCL -- tile after tile, serially, where guesses
+// fail often (C4: 5 % of the tiles, 4.2 -> 19.9 ms).  So a tile also finalises its AGG from the
+// entry its predecessor's base-chain exit gives (x0p[t - 1]; that chain ran the predecessor's
+// whole tile, so it is wrong about as rarely as the old chain-0 guesses): right away if x0p is
+// published by then, else when its look-back first has to wait anyway.  A look-back meeting a
+// wrong tentative AGG waits for the final one (not for an INCL); a wrong final one, for the INCL.
+// A tile holding a message start publishes INCL at once: its exit and the words after its last
+// start do not depend on its entry.
+// (The flat stream decode keeps the scheme its composed look-back is built on: the optimistic
+// entry is where the predecessor's chain 0 leads (x0p[t - 1]), and the ok bit says the exit is the
+// tile's chain-0 exit, so the next tile's optimistic entry is its true one.)
 constexpr uint64_t kOkBit = 1ull << 61;
 constexpr int kExitShift = 48;                       // bits 48-60: exit - kB
-constexpr uint64_t kWordsMask = (1ull << kExitShift) - 1;
+constexpr int kEntryShift = 35;                      // bits 35-47: an AGG's guessed entry
+constexpr uint64_t kWordsMask = (1ull << kEntryShift) - 1;  // (a message of < 2^35 words)
 constexpr uint32_t kExitDead = 0x1fff;               // the chain ran past the batch end
 
 __device__ __forceinline__ uint64_t make_desc(uint64_t state, uint32_t exit, uint32_t x0,
-                                              uint64_t words) {
+                                              uint64_t words, uint32_t entry = 0) {
   const uint32_t e = exit >= (uint32_t)kDead ? kExitDead : exit - (uint32_t)kB;
-  return state | (exit == x0 ? kOkBit : 0ull) | ((uint64_t)e << kExitShift) | (words & kWordsMask);
+  return state | (exit == x0 ? kOkBit : 0ull) | ((uint64_t)e << kExitShift) |
+         ((uint64_t)(entry & 0x1fffu) << kEntryShift) | (words & kWordsMask);
 }
 __device__ __forceinline__ uint32_t desc_exit(uint64_t d) {
   const uint32_t e = (uint32_t)(d >> kExitShift) & 0x1fffu;
   return e == kExitDead ? (uint32_t)kDead : e + (uint32_t)kB;
+}
+__device__ __forceinline__ uint32_t desc_entry(uint64_t d) {
+  return (uint32_t)(d >> kEntryShift) & 0x1fffu;
+}
+constexpr uint64_t kFinalBit = 1ull << 61;  // (message decode: the bit the flat decode's ok uses)
+__device__ __forceinline__ uint64_t make_agg(uint32_t exit, uint64_t words, uint32_t entry,
+                                             bool final) {
+  return (make_desc(kDescAgg, exit, ~0u, words, entry) & ~kOkBit) | (final ? kFinalBit : 0ull);
 }
 
 // Entry of a tile from its predecessor's exit (predecessor-relative), clipped at the tile's first
@@ -1015,57 +1037,72 @@ __device__ __forceinline__ uint64_t clip_below(uint64_t tm0, uint32_t fms, int s
 
 // Exclusive prefix of tile t -- words of the message at the tile start before this tile -- and
 // (*xprev) the true exit of tile t - 1, from the descriptors of tiles t - 1, t - 2, ...: up to the
-// nearest INCL, every AGG on the way must be right.  Tile j's AGG is right when tile j - 1's
-// exit (as published, and itself right) has the ok bit; the farthest tile without it makes every
-// nearer one wrong, so the wave then waits for the tile right after it to publish INCL (it
-// resolves its own entry the same way) and starts over.  Waits are only ever for lower tiles.
-// The first window of each pass is 16 tiles (one 128-byte line of descriptors: the nearest INCL
-// is usually a few tiles back, and these agent-scope reads go past the L2), later ones 64.
-__device__ uint64_t lookback_tiles(const UnpackArgs& a, uint64_t t, uint32_t* xprev) {
+// nearest INCL, every AGG on the way must be right -- its entry the one its predecessor's exit
+// (as published, and itself right) leads to.  The farthest AGG that is not makes every nearer one
+// wrong: the wave waits for that tile to publish its final AGG (if this one was its guess) or its
+// INCL, and starts over.  Waits are only ever for lower tiles; before its first wait the wave runs
+// on_wait (the tile finalises its own AGG).  The first window of each pass is 16 tiles (one
+// 128-byte line of descriptors: the nearest INCL is usually a few tiles back, and these
+// agent-scope reads go past the L2), later ones 64.
+template <class OnWait>
+__device__ uint64_t lookback_tiles(const UnpackArgs& a, uint64_t t, uint32_t* xprev,
+                                   OnWait on_wait) {
   const int l = lane_id();
   int64_t base = (int64_t)t - 1;  // nearest tile of the window
   uint64_t acc = 0;
   uint32_t xfirst = (uint32_t)kB;
   uint32_t spins = 0;
   int width = 16;
+  uint64_t carry = 0;  // descriptor of the previous window's farthest tile (an AGG) to check
+  bool has_carry = false;
   for (;;) {
     const int64_t idx = base - l;
     const bool in = l < width;
     CPK_DIAG_ONLY(diag_add(22, 1));
     // before tile 0: an inclusive zero whose exit enters tile 0 at byte 0
-    const uint64_t dv = !in ? 0ull : (idx >= 0 ? load_agent(a.desc + idx) : (kDescIncl | kOkBit));
+    const uint64_t dv = !in ? 0ull : (idx >= 0 ? load_agent(a.desc + idx) : kDescIncl);
     const uint64_t stt = dv & kDescFlags;
     const uint64_t sb = ballot(in && stt == kDescIncl);
     const int k = sb ? lowest_bit(sb) : 64;
     const uint64_t nb = ballot(in && stt == 0);
     const int nl = nb ? lowest_bit(nb) : 64;
     const uint64_t* wait_on = nullptr;
-    bool want_incl = false;
+    int want = 0;  // 0: published, 1: final AGG or INCL, 2: INCL
     if (nl < k) {
       wait_on = a.desc + (base - nl);
     } else {
       const int kk = k < width ? k : width - 1;
-      const bool first = base == (int64_t)t - 1;
-      const uint64_t fb = ballot(l <= kk && (l >= 1 || !first) && !(dv & kOkBit));
-      if (fb) {
-        wait_on = a.desc + (base - highest_bit(fb) + 1);
-        want_incl = true;
+      // entry each tile's predecessor (the next lane) leads to; an AGG tile has no message start
+      const uint32_t ent = entry_from_exit(desc_exit(dv), (uint32_t)kB);
+      const uint32_t pent = shfl32(ent, l + 1 < 64 ? l + 1 : 63);
+      const uint64_t fb = ballot(l < kk && desc_entry(dv) != pent);
+      if (has_carry && desc_entry(carry) != readlane32(ent, 0)) {
+        wait_on = a.desc + (base + 1);
+        want = (carry & kFinalBit) ? 2 : 1;
+      } else if (fb) {
+        const int j = highest_bit(fb);
+        wait_on = a.desc + (base - j);
+        want = (readlane64(dv, j) & kFinalBit) ? 2 : 1;
       } else {
-        if (first) xfirst = desc_exit(readlane64(dv, 0));
+        if (base == (int64_t)t - 1) xfirst = desc_exit(readlane64(dv, 0));
         acc += wave_sum64(l <= kk ? (dv & kWordsMask) : 0ull);
         if (k < width) break;
+        carry = readlane64(dv, width - 1);
+        has_carry = true;
         base -= width;
         width = 64;
         continue;
       }
     }
+    on_wait();
     // one lane polls the blocking descriptor (sleeping between polls), then the window is read
-    // again from the nearest tile
-    CPK_DIAG_ONLY(diag_add(want_incl ? 24 : 23, 1); const uint32_t sp0 = uniform32(spins));
+    // again from the nearest tile (after a wrong AGG, from tile t - 1)
+    CPK_DIAG_ONLY(diag_add(want ? 24 : 23, 1); const uint32_t sp0 = uniform32(spins));
     if (l == 0) {
       for (;;) {
-        const uint64_t f = load_agent(wait_on) & kDescFlags;
-        if (want_incl ? f == kDescIncl : f != 0) break;
+        const uint64_t v = load_agent(wait_on);
+        const uint64_t f = v & kDescFlags;
+        if (want == 0 ? f != 0 : (f == kDescIncl || (want == 1 && (v & kFinalBit)))) break;
         if (++spins >= kSpinLimit) break;
         __builtin_amdgcn_s_sleep(1);
       }
@@ -1076,10 +1113,11 @@ __device__ uint64_t lookback_tiles(const UnpackArgs& a, uint64_t t, uint32_t* xp
       raise_error(a.err, kErrInternal);
       break;
     }
-    if (want_incl) {
+    if (want) {
       base = (int64_t)t - 1;
       acc = 0;
       width = 16;
+      has_carry = false;
     }
   }
   *xprev = xfirst;
@@ -1682,7 +1720,7 @@ __device__ __forceinline__ void expand_records(const UnpackArgs& a, uint64_t A, 
 template <bool FLAT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CPK_UNPACK_WPE))) void
 unpack_tiles_kernel(UnpackArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds_data[4][kB + kPad];
+  __shared__ __attribute__((aligned(16))) uint8_t lds_data[4][kPre + kB + kPad];
   // per wave 1 KiB: message starts while they are found, then chain 0 and the walked starts
   // while the entry's chain is traced, then the record list of a quarter tile
   __shared__ uint64_t lds_aux[4][kB / 32];
@@ -1726,7 +1764,7 @@ unpack_tiles_kernel(UnpackArgs a) {
   // the header launch is done: its scan descriptors go back to zero for the next call
   for (uint64_t i = t + a.ntiles * (uint64_t)l; i < a.hdr_nblocks; i += 64 * a.ntiles)
     a.hdr_desc[i] = 0;
-  uint8_t* const d = lds_data[wv];
+  uint8_t* const d = lds_data[wv] + kPre;
   uint64_t* const aux = lds_aux[wv];
   const uint64_t P = a.nbytes;
   const uint64_t A = t * kB;
@@ -1753,20 +1791,36 @@ unpack_tiles_kernel(UnpackArgs a) {
   // message start there, if any) and walks unmarked up to it: chains synchronise within a few
   // records, so the chain then usually enters the sub-tile where the true one does, and the
   // fixed point below has little left to re-walk.
+  // Lane 0 does the same through the kPre bytes before the tile (the predecessor's last bytes,
+  // from its last message start there if any): where it lands is the tile's guessed entry Eg,
+  // the start of the tile's base chain (the flat stream decode keeps chain 0, from byte 0).
+  const bool guess = !FLAT && t > 0;
   int e0 = st.s;
+  // first message start (the batch end counts), tile-relative; kB if none
+  const uint64_t msl = ballot(st.msw != 0);
+  const int fl = lowest_bit(msl);
+  const uint32_t fms = msl ? (uint32_t)(64 * fl + lowest_bit(readlane64(st.msw, fl))) : (uint32_t)kB;
 #if CPK_PREWALK > 0
   {
-    const uint64_t pm = shfl64(st.msw, l > 0 ? l - 1 : 0);
-    if (l > 0 && st.s < st.pend && !(a.debug_skip & 4)) {
+    uint64_t pm = shfl64(st.msw, l > 0 ? l - 1 : 0);
+    if (l == 0) {
+      const uint64_t s0 = readlane64(win.start, 0);  // message mfirst - 1: the last start before A
+      pm = (s0 != ~0ull && s0 + kPre >= A && s0 < A) ? 1ull << (s0 + kPre - A) : 0ull;
+    }
+    if ((l > 0 || guess) && st.s < st.pend && !(a.debug_skip & 4)) {
       const uint64_t wn = pm & ~mask_lt(64 - CPK_PREWALK);
       int q = wn ? st.s - 64 + highest_bit(wn) : st.s - CPK_PREWALK;
       while (q < st.s) q += step_len(d[q], d[q + 9]);
       // (a message start in the sub-tile before the landing point restarts the chain there)
       const int fm = st.msw ? st.s + lowest_bit(st.msw) : 0x7fffffff;
       e0 = q < fm ? q : fm;
+      // (the base chain starts at or before the tile's first message start, where every chain
+      // restarts, and inside the tile)
+      if (l == 0 && e0 > (int)fms) e0 = (int)fms;
     }
   }
 #endif
+  const uint32_t Eg = guess ? (uint32_t)readlane32((uint32_t)e0, 0) : 0u;
 #ifdef CPK_DIAG
   int dn = 0, dit[3] = {0, 0, 0};
   if (e0 < st.pend && !(a.debug_skip & 4)) sx = walk(d, st, e0, 0, &chain, &runm, &dn);
@@ -1782,7 +1836,7 @@ unpack_tiles_kernel(UnpackArgs a) {
   uint64_t tm0 = 0;
   int out = st.end;
   const bool settled =
-      (a.debug_skip & 4) ? true : settle(d, st, chain, sx, 0, e, tm0, out, runm, diag_it);
+      (a.debug_skip & 4) ? true : settle(d, st, chain, sx, (int)Eg, e, tm0, out, runm, diag_it);
   CPK_DIAG_ONLY(diag_add(5, dit[0]));
   uint32_t x0 = readlane32((uint32_t)out, 63);
   // Flat streams (stream split): inside long raw stretches (text) the chain from the tile's first
@@ -1820,10 +1874,6 @@ unpack_tiles_kernel(UnpackArgs a) {
     win.ok = 0;
   }
 
-  // first message start (the batch end counts), tile-relative; kB if none
-  const uint64_t msl = ballot(st.msw != 0);
-  const int fl = lowest_bit(msl);
-  const uint32_t fms = msl ? (uint32_t)(64 * fl + lowest_bit(readlane64(st.msw, fl))) : (uint32_t)kB;
   // a message starting in the tile: exit and words after the last start are entry-independent
   const uint64_t msin = tm0 & st.msw;
   const int lastms = highest_bit(msin);
@@ -1844,6 +1894,70 @@ unpack_tiles_kernel(UnpackArgs a) {
     if (!has_start) {  // (tile 0 without a message start: bytes before the first message)
       const uint64_t w = readlane32(wave_incl_sum32(mask_words(d, st.s, tm0, runm)), 63);
       if (l == 0) store_agent(a.desc + t, make_desc(kDescIncl, x0, x0, w));
+    }
+  } else if constexpr (!FLAT) {
+    // the guessed entry's AGG, at once (a tile with a message start published its INCL already)
+    uint32_t xE = x0;
+    uint64_t runs = runm, w = 0;
+    if (!has_start) {
+      w = readlane32(wave_incl_sum32(mask_words(d, st.s, tm0, runm)), 63);
+      if (l == 0) store_agent(a.desc + t, make_agg(x0, w, Eg, false));
+    }
+    CPK_DIAG_ONLY(ck[3] = clock64(); wk[3] = wall_clock64());
+    // the final AGG: for the entry the predecessor's base-chain exit gives
+    bool fin = has_start;
+    uint32_t Eo = Eg, xO = x0;
+    uint64_t tmO = tm0, runsO = runm, wO = w;
+    auto finalize = [&](bool block) {
+      if (fin) return;
+      uint32_t xp = 0;
+      if (block) {
+        xp = wait_nonzero32(a.x0p + t - 1, a.err);
+      } else {
+        if (l == 0) xp = load_agent32(a.x0p + t - 1);
+        xp = readlane32(xp, 0);
+        if (!xp) return;
+      }
+      Eo = entry_from_exit(xp & 0x7fffffffu, fms);
+      if (Eo != Eg) {
+        runsO = runm;
+        xO = x0;
+        if (Eo < fms)
+          tmO = enter_chain(d, aux, st, tm0, (int)Eo, (int)fms, x0, &xO, &runsO);
+        else
+          tmO = clip_below(tm0, fms, st.s, &xO);
+        wO = readlane32(wave_incl_sum32(mask_words(d, st.s, tmO, runsO)), 63);
+      }
+      if (l == 0) store_agent(a.desc + t, make_agg(xO, wO, Eo, true));
+      fin = true;
+    };
+    finalize(false);
+    CPK_DIAG_ONLY(ck[4] = clock64(); wk[4] = wall_clock64());
+    uint32_t xprev = (uint32_t)kB + Eg;
+    if (!(a.debug_skip & 8)) excl = lookback_tiles(a, t, &xprev, [&]() { finalize(true); });
+    CPK_DIAG_ONLY(ck[5] = clock64(); wk[5] = wall_clock64());
+    const uint32_t E = entry_from_exit(xprev, fms);
+    CPK_DIAG_ONLY(diag_add(9, E != Eg); diag_add(10, fin && Eo != Eg); diag_add(14, fin && E != Eo));
+    if (E == Eg) {
+    } else if (fin && E == Eo) {
+      tm = tmO;
+      runs = runsO;
+      xE = xO;
+      w = wO;
+    } else {
+      // neither guess: the predecessor's chain does not lead where they did
+      if (E < fms)
+        tm = enter_chain(d, aux, st, tm0, (int)E, (int)fms, x0, &xE, &runs);
+      else
+        tm = clip_below(tm0, fms, st.s, &xE);
+      if (!has_start) w = readlane32(wave_incl_sum32(mask_words(d, st.s, tm, runs)), 63);
+    }
+    if (!has_start && l == 0) store_agent(a.desc + t, make_desc(kDescIncl, xE, x0, excl + w));
+    if (a.stamps && l == 0 && t < 1024) {  // diagnostic dump (CPK_STAMPS=1)
+      a.stamps[4 * t] = E | ((uint64_t)Eg << 32);
+      a.stamps[4 * t + 1] = xE | ((uint64_t)x0 << 32);
+      a.stamps[4 * t + 2] = excl;
+      a.stamps[4 * t + 3] = w | ((uint64_t)fms << 32) | ((uint64_t)has_start << 63);
     }
   } else {
     // optimistic entry: where the predecessor's chain 0 leads (a tile with a message start
@@ -1887,8 +2001,7 @@ unpack_tiles_kernel(UnpackArgs a) {
     uint32_t xprev = xp;
     CPK_DIAG_ONLY(ck[4] = clock64(); wk[4] = wall_clock64());
     if (!(a.debug_skip & 8)) {
-      if constexpr (FLAT) excl = lookback_flat_scan(a, t, &xprev);
-      else excl = lookback_tiles(a, t, &xprev);
+      excl = lookback_flat_scan(a, t, &xprev);
     }
     CPK_DIAG_ONLY(ck[5] = clock64(); wk[5] = wall_clock64());
     const uint32_t E = entry_from_exit(xprev, fms);
