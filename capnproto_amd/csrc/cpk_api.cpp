@@ -591,9 +591,10 @@ cpk_status unpack_common(cpk_ctx* ctx, uint32_t mode, const uint8_t* d_packed, u
   a.hdr_nblocks = mode == 0 && !fuse ? cpk::header_scan_blocks(n) : 0;
   a.desc2 = s.desc2;
   a.hdr_fuse = fuse ? 1u : 0u;
-  // messages of >= 256 tiles on average: the look-back reaches back to the previous occupancy
-  // round, and the waves ahead of it in the issue arbitration publish sooner
-  a.prio = (mode != 2 && n && P / n >= 256 * B) ? 1u : 0u;
+  // messages of >= 4 tiles on average: most tiles look back over AGGs (no message start of their
+  // own), and the waves ahead of the expansions in the issue arbitration publish sooner (C2
+  // unpack_tiles 225.9 -> 222.6 us, C4 unchanged; on every batch: C5 9.36 -> 9.72 ms)
+  a.prio = (mode != 2 && n && P / n >= 4 * B) ? 1u : 0u;
   a.err_host = fuse ? ctx->err_host : nullptr;
   ctx->fused_last = a.err_host != nullptr;
   a.hdr_limit = limit;
