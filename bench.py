@@ -515,8 +515,9 @@ def summarize(res, world, copy_gbps):
             "read_only_frac": round(rd / HBM_PEAK_GBS, 4),
             "measured_copy_GBps": round(copy_gbps, 1) if copy_gbps else None,
             "measured_copy_kernel": "copy_kernel (cpk_stream.hip): 16 B/lane streaming copy, "
-                                    "best of a sweep over loads in flight (4, 8), cache policy "
-                                    "and grid size, read + write bytes, 1 GiB each way",
+                                    "best of a sweep over loads in flight per lane (4, 8, 16), "
+                                    "default or non-temporal access, grid-strided or contiguous "
+                                    "blocks, and grid size; read + write bytes, 1 GiB each way",
             "frac_of_measured_copy": round(rt / copy_gbps, 4) if copy_gbps else None,
             "dominant_kernel": {
                 "kernel": dom,
@@ -634,8 +635,10 @@ def main():
             "roofline": s["roofline"],
             "cpu_baseline": cb,
             "kernels": {"pack": "framing + pack_tile (tiles whose offset is known in time write "
-                                "straight out, the rest to a bounded slot pool) + pack_place "
-                                "(look-back offsets, slot copies) (capnproto_amd/csrc/cpk_pack.hip)",
+                                "straight out; sparse tiles take an exact-size piece of a byte "
+                                "arena, dense ones wait for their offset) + pack_place (group "
+                                "scan of the tile byte counts, arena copies, requested positions) "
+                                "(capnproto_amd/csrc/cpk_pack.hip)",
                         "unpack": "header (+ word-offset scan, tile_first, scratch zeroing) + "
                                   "unpack_tiles (capnproto_amd/csrc/cpk_unpack.hip)",
                         "knobs": knobs},
