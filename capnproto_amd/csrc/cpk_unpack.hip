@@ -647,6 +647,11 @@ __device__ __forceinline__ void run_jobs(const UnpackArgs& a, const RunJob& job,
   }
 }
 
+// A raw run crossing into the next tile (text: runs of up to 2 KiB): its words ending at most
+// kRunSplit bytes into the next tile are written by the run's own tile (from its staged bytes
+// and kPad), the rest by the next tile, which stages those bytes itself (run_tail) -- rather
+// than every crossing run being read whole again from global memory, from another XCD's L2.
+constexpr uint32_t kRunSplit = (uint32_t)kPad - 4u;
 constexpr uint32_t kShortRunGeneral = 4;  // runs of at most this many words: their own lane
 // Runs of a batch: a short run (at most kShortRunGeneral words, zero or raw from the staged tile --
 // most runs of dense data, where a zero or raw stretch rarely lasts) is written by its own lane,
@@ -1646,21 +1651,16 @@ __device__ __forceinline__ void expand_lean(const UnpackArgs& a, uint64_t A, con
                      __builtin_amdgcn_alignbyte(x1, x0, s3);
           }
         } else {
-          // past the staged bytes: unaligned 8-byte loads from the batch, all of a 256-word
-          // block issued before its stores (clamped indices: no load left outstanding)
-          const uint8_t* const s8 = a.packed + A + sj;
-          for (uint32_t kb = k0; kb < nj; kb += 256) {
-            uint64_t v[4];
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-              const uint32_t k = kb + 64 * i + l;
-              __builtin_memcpy(&v[i], s8 + 8ull * (k < nj ? k : nj - 1), 8);
-            }
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-              const uint32_t k = kb + 64 * i + l;
-              dst[k < nj ? k : nj - 1] = v[i];
-            }
+          // a raw run leaving the staged bytes: its words whose bytes are staged (ending at most
+          // kRunSplit bytes into the next tile) from LDS; the rest the next tile writes from its
+          // own staged bytes (run_tail) -- this record neither ends nor breaks its message
+          const uint32_t kin = sj + 12u <= kStaged ? (kStaged - 4u - sj) / 8u : 0u;
+          const uint32_t ke = nj < kin ? nj : kin;
+          for (uint32_t k = k0 + l; k < ke; k += 64) {
+            const uint32_t ob = sj + 8u * k, qq = ob >> 2, s3 = ob & 3u;
+            const uint32_t x0 = d32[qq], x1 = d32[qq + 1], x2 = d32[qq + 2];
+            dst[k] = ((uint64_t)__builtin_amdgcn_alignbyte(x2, x1, s3) << 32) |
+                     __builtin_amdgcn_alignbyte(x1, x0, s3);
           }
         }
       }
@@ -1675,6 +1675,29 @@ __device__ __forceinline__ void expand_lean(const UnpackArgs& a, uint64_t A, con
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+}
+
+// The words of the raw run this tile's entry E lies behind (the predecessor's last record, a
+// raw run when E > kRunSplit) that end more than kRunSplit bytes into the tile: the predecessor
+// left them (lean expansion) or wrote them too (same values).  Not for a run that ends or breaks
+// its message, whose record handle_record writes whole, nor for a message the lean path would
+// not take (header refused, output too small).
+__device__ __forceinline__ void run_tail(const UnpackArgs& a, uint64_t A, const uint8_t* d,
+                                         uint32_t E, uint64_t excl, const MsgWin& win) {
+  const int l = lane_id();
+  const uint64_t mbase = readlane64(win.base, 0), mtot = readlane64(win.total, 0);
+  const uint64_t mend = readlane64(win.end, 0);
+  const uint32_t n = (E - kRunSplit + 7u) / 8u;  // words ending past byte kRunSplit
+  if (!readlane32(win.ok, 0) || mbase + mtot > a.words_capacity || excl >= mtot ||
+      A + E >= mend || excl < n)
+    return;
+  const uint32_t* const d32 = (const uint32_t*)d;
+  for (uint32_t j = (uint32_t)l; j < n; j += 64) {
+    const uint32_t ob = E - 8u * j - 8u, qq = ob >> 2, s3 = ob & 3u;  // bytes [ob, ob + 8)
+    const uint32_t x0 = d32[qq], x1 = d32[qq + 1], x2 = d32[qq + 2];
+    a.words[mbase + excl - 1u - j] = ((uint64_t)__builtin_amdgcn_alignbyte(x2, x1, s3) << 32) |
+                                     __builtin_amdgcn_alignbyte(x1, x0, s3);
   }
 }
 
@@ -1890,6 +1913,7 @@ unpack_tiles_kernel(UnpackArgs a) {
 
   // ---- the tile's entry and the words before it ------------------------------------------
   uint64_t tm = tm0, excl = 0;
+  uint32_t Ein = 0;  // the tile's true entry
   if (t == 0 || fms == 0) {
     if (!has_start) {  // (tile 0 without a message start: bytes before the first message)
       const uint64_t w = readlane32(wave_incl_sum32(mask_words(d, st.s, tm0, runm)), 63);
@@ -1937,6 +1961,7 @@ unpack_tiles_kernel(UnpackArgs a) {
     if (!(a.debug_skip & 8)) excl = lookback_tiles(a, t, &xprev, [&]() { finalize(true); });
     CPK_DIAG_ONLY(ck[5] = clock64(); wk[5] = wall_clock64());
     const uint32_t E = entry_from_exit(xprev, fms);
+    Ein = E;
     CPK_DIAG_ONLY(diag_add(9, E != Eg); diag_add(10, fin && Eo != Eg); diag_add(14, fin && E != Eo));
     if (E == Eg) {
     } else if (fin && E == Eo) {
@@ -2032,6 +2057,7 @@ unpack_tiles_kernel(UnpackArgs a) {
   // ---- expansion -------------------------------------------------------------------------
   if (a.debug_skip & 256) return;  // diagnostic: + the entry and the look-back
   if (a.prio) __builtin_amdgcn_s_setprio(0);
+  if (!FLAT && a.mode == 0 && a.words && Ein > kRunSplit) run_tail(a, A, d, Ein, excl, win);
   expand_records(a, A, d, aux, dep_tab, tm, excl, win, mfirst, mlast, msw);
   // a fused single-tile batch: this wave is the whole call -- its error word for the host, last:
   // its stores done, then a system-scope release
