@@ -696,12 +696,15 @@ struct MsgWin {
   uint32_t ok;       // header accepted
 };
 
-__device__ __forceinline__ void load_win(const UnpackArgs& a, int64_t mw, MsgWin& w) {
+// Lanes from nl on load lane 0's entry again (the same lines, not more of them) and hold the
+// defaults of a missing entry.
+__device__ __forceinline__ void load_win(const UnpackArgs& a, int64_t mw, MsgWin& w,
+                                         int nl = 64) {
   // every load unconditional, from a clamped index (entries past the batch select their defaults
   // afterwards): loads under branches each got their own wait, three round trips in a row
   const int64_t m = mw + lane_id();
-  const bool v = m >= 0 && (uint64_t)m < a.nmsgs;
-  const uint64_t mc = v ? (uint64_t)m : 0;
+  const bool v = m >= 0 && (uint64_t)m < a.nmsgs && lane_id() < nl;
+  const uint64_t mc = v ? (uint64_t)m : (mw >= 0 && (uint64_t)mw < a.nmsgs ? (uint64_t)mw : 0);
   const uint64_t mn = mc + 1 <= a.nmsgs ? mc + 1 : a.nmsgs;
   const uint64_t* const wo = a.word_off ? a.word_off : a.in_off;
   const int32_t* const hs = a.hdr_status ? a.hdr_status : (const int32_t*)a.in_off;
@@ -793,21 +796,24 @@ __device__ __forceinline__ uint64_t tile_msg_starts(const UnpackArgs& a, uint64_
   const uint64_t P = a.nbytes;
   ms[l] = 0;
   MsgWin w2;
+  // the first window is 8 entries (a tile holds a few messages; the lines of 64 entries are
+  // fetched again by the tiles of other XCDs sharing them), all 64 when 7 messages start in it
+  int nl = first ? 8 : 64;
   if (first) {
-    load_win(a, (int64_t)mfirst - 1, w2);
+    load_win(a, (int64_t)mfirst - 1, w2, nl);
     *first = w2;
   } else {
     load_starts(a, (int64_t)mfirst - 1, w2);
   }
   uint64_t mlast;
   for (;;) {
-    const bool in = l > 0 && w2.start >= A && w2.start < A + kB;
+    const bool in = l > 0 && l < nl && w2.start >= A && w2.start < A + kB;
     if (in) {
       const uint64_t r = w2.start - A;
       atomicOr((unsigned long long*)&ms[r >> 6], 1ull << (r & 63));
     }
     const uint64_t inm = ballot(in);
-    if (inm != (~0ull << 1)) {
+    if (inm != (nl == 64 ? (~0ull << 1) : (((1ull << nl) - 1) & ~1ull))) {
       mlast = (uint64_t)(w2.mw + 1 + __popcll(inm));
       if (nms_after) {
         // message mlast is the window lane after the last one in the tile (a missing entry
@@ -816,6 +822,12 @@ __device__ __forceinline__ uint64_t tile_msg_starts(const UnpackArgs& a, uint64_
         *nms_after = (int)((nx < P ? nx : P) - A);
       }
       break;
+    }
+    if (nl < 64) {  // the first window again, whole
+      nl = 64;
+      load_win(a, w2.mw, w2);
+      *first = w2;
+      continue;
     }
     // 63 starts in this window: continue with the next
     if (first) load_win(a, w2.mw + 63, w2);
