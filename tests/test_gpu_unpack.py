@@ -262,3 +262,61 @@ def test_text_messages_many_tiles(codec, oracle):
         m = cases.flat_message(rng, 1, [n], "text")
         msgs.append(oracle.pack_flat(m)[0])
     check_against_oracle(codec, oracle, msgs)
+
+
+def _raw_run_message(oracle, rng, p0, c, tail_words, nwords_delta=0, cut=None):
+    """A packed message whose raw run record (0xff, 8 data bytes, count c, 8c raw bytes) starts at
+    packed byte p0 of the message: 2-byte filler records before it, tail_words more after it.
+    nwords_delta < 0 makes the segment table claim fewer words (the run then overshoots); cut
+    truncates the packed bytes.  Returns the packed bytes."""
+    body_words = lambda nfill: nfill + 1 + c + tail_words
+    head = oracle.pack_chunk(np.array([0], "<u8"))  # placeholder size for the table word
+    nfill = max(0, (p0 - len(head)) // 2)
+    for _ in range(3):  # the table word's packed size depends on the word count
+        nw = body_words(nfill) + nwords_delta
+        head = oracle.pack_chunk(np.frombuffer(np.array([0, nw], "<u4").tobytes(), "<u8"))
+        nfill = max(0, (p0 - len(head)) // 2)
+    body = bytearray()
+    for _ in range(nfill):
+        body += bytes([0x01, int(rng.integers(1, 256))])
+    if (p0 - len(head)) % 2:
+        body[-2:] = bytes([0x03]) + rng.integers(1, 256, 2, dtype=np.uint8).tobytes()
+    body += bytes([0xff]) + rng.integers(1, 256, 8, dtype=np.uint8).tobytes() + bytes([c])
+    body += rng.integers(0, 256, 8 * c, dtype=np.uint8).tobytes()
+    for _ in range(tail_words):
+        body += bytes([0x01, int(rng.integers(1, 256))])
+    m = head + bytes(body)
+    return m[:cut] if cut is not None else m
+
+
+def test_raw_runs_across_tiles(codec, oracle):
+    """Raw runs crossing a 4 KiB tile boundary of the batch: the run's own tile writes the words
+    staged with it, the next tile the rest from its own bytes (run_tail) -- except for a run that
+    ends or breaks its message (its last record, a run overshooting the message's words, a
+    message cut inside the run), whose tile writes it whole.  A valid message follows each case
+    so that a stray write past a failing message shows; the next tile's guessed entry (the 64
+    bytes before it are raw bytes) is wrong for most of them."""
+    rng = np.random.default_rng(5)
+    after = oracle.pack_flat(cases.flat_message(rng, 1, [300], "mixed"))[0]
+    for p0 in (4090, 4080, 4070, 4050, 3900, 3000, 2100):
+        for c in (1, 2, 5, 40, 255):
+            batches = [
+                [_raw_run_message(oracle, rng, p0, c, 20), after],        # run in the middle
+                [_raw_run_message(oracle, rng, p0, c, 0), after],         # the message's last
+                [_raw_run_message(oracle, rng, p0, c, 0, -1), after],     # overshoot
+                [_raw_run_message(oracle, rng, p0, c, 10, -8), after],    # overshoot, then more
+            ]
+            full = _raw_run_message(oracle, rng, p0, c, 0)
+            batches.append([full[: p0 + 10 + 4 * c], after])             # cut inside the run
+            for msgs in batches:
+                check_against_oracle(codec, oracle, msgs)
+    # two tiles in a row each entered inside a run, runs of 255 words back to back
+    for k in range(4):
+        nw = 4 * 256
+        body = bytearray()
+        for _ in range(4):
+            body += bytes([0xff]) + rng.integers(1, 256, 8, dtype=np.uint8).tobytes() + bytes([255])
+            body += rng.integers(0, 256, 8 * 255, dtype=np.uint8).tobytes()
+        head = oracle.pack_chunk(np.frombuffer(np.array([0, nw], "<u4").tobytes(), "<u8"))
+        pad = oracle.pack_flat(cases.flat_message(rng, 1, [17 * k], "mixed"))[0]
+        check_against_oracle(codec, oracle, [pad, head + bytes(body), after])
