@@ -282,7 +282,7 @@ def measure_copy(codec, nbytes=1 << 31, reps=6):
     sweep = {}
     names = {0: "x4", 1: "x8", 2: "x16"}
     for form in (0, 1, 2, 4, 5, 6, 8, 9, 10, 12, 13, 14):
-      for g in (2048, 4096, 8192, 16384):
+      for g in (1024, 2048, 4096, 8192, 16384, 32768):
         blocks = (form << 24) | g
 
         def run():
@@ -303,6 +303,19 @@ def measure_copy(codec, nbytes=1 << 31, reps=6):
         sweep[f"{tag}/{g}"] = round(gbps, 1)
         best = max(best, gbps)
     ok = torch.equal(a, b)
+    # the runtime's own device-to-device copy (hipMemcpyAsync: ROCclr's blit kernel), for scale
+    b.zero_()
+    with torch.cuda.stream(s):
+        b.copy_(a)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(reps):
+            b.copy_(a)
+        e1.record(s)
+        torch.cuda.synchronize()
+    sweep["runtime_d2d_copy"] = round(2 * nbytes / (e0.elapsed_time(e1) / reps * 1e-3) / 1e9, 1)
+    ok = ok and torch.equal(a, b)
     del a, b
     torch.cuda.empty_cache()
     if not ok:
