@@ -1075,9 +1075,13 @@ __device__ uint64_t lookback_tiles(const UnpackArgs& a, uint64_t t, uint32_t* xp
   for (;;) {
     const int64_t idx = base - l;
     const bool in = l < width;
-    CPK_DIAG_ONLY(diag_add(22, 1));
+    CPK_DIAG_ONLY(diag_add(22, 1); const uint64_t lt0 = wall_clock64());
     // before tile 0: an inclusive zero whose exit enters tile 0 at byte 0
     const uint64_t dv = !in ? 0ull : (idx >= 0 ? load_agent(a.desc + idx) : kDescIncl);
+#ifdef CPK_DIAG
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (width == 16) diag_add(15, wall_clock64() - lt0);  // the first window's read, 10 ns ticks
+#endif
     const uint64_t stt = dv & kDescFlags;
     const uint64_t sb = ballot(in && stt == kDescIncl);
     const int k = sb ? lowest_bit(sb) : 64;

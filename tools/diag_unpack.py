@@ -20,7 +20,7 @@ from bench import CONFIGS  # noqa: E402
 
 NAMES = ["tiles", "walk0_trips", "walk0_lane_steps", "rewalk_trips", "rewalk_lane_steps",
          "settle_rounds", "enter_calls", "merge_steps", "merge_capped", "entry_mismatch",
-         "opt_walked", "has_start", "f_cand", "f_used", "not_ok", "-",
+         "opt_walked", "has_start", "f_cand", "f_used", "not_ok", "lb_first_read_ticks",
          "clk_stage", "clk_chain0", "clk_wait_x0p", "clk_entry", "clk_lookback", "clk_expand",
          "lb_windows", "lb_wait_unpub", "lb_wait_incl", "lb_polls", "incl_waits", "unpublished",
          "win_before_wait", "win_resolved"]
