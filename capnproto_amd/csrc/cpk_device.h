@@ -138,7 +138,6 @@ __device__ __forceinline__ void frame_message(const uint64_t* __restrict__ words
     if (status) status[i] = 6;  // CPK_ERR_BAD_FRAMING
     return;
   }
-  mark_chunk(bits, tstarts, w0);
   const uint64_t nw = w1 - w0;
   const uint32_t* t32 = (const uint32_t*)(words + w0);
   const uint64_t nseg = (uint64_t)t32[0] + 1;
@@ -149,16 +148,30 @@ __device__ __forceinline__ void frame_message(const uint64_t* __restrict__ words
     for (uint64_t s = 0; s < nseg && total <= nw; s++) total += t32[s + 1];
     ok = total == nw;
   }
+  // the chunk starts gathered per bitmap word: one atomic per word touched (the message start and
+  // its table end usually share one), not one per start
+  uint64_t cw = w0 >> 6, cm = 1ull << (w0 & 63);
+  auto mark = [&](uint64_t p) {
+    if ((p >> 6) != cw) {
+      atomicOr(bits + cw, (unsigned long long)cm);
+      cw = p >> 6;
+      cm = 0;
+    }
+    cm |= 1ull << (p & 63);
+    if (p % kPackTileWords == 0) tstarts[p / kPackTileWords] = 1;
+  };
+  if (w0 % kPackTileWords == 0 && w0) tstarts[w0 / kPackTileWords] = 1;  // (tile 0: none)
   if (!ok) {
     st = 6;  // CPK_ERR_BAD_FRAMING: packed as one chunk
   } else {
     uint64_t p = w0 + tw;
-    if (p < w1) mark_chunk(bits, tstarts, p);
+    if (p < w1) mark(p);
     for (uint64_t s = 0; s + 1 < nseg; s++) {
       p += t32[s + 1];
-      if (p < w1) mark_chunk(bits, tstarts, p);
+      if (p < w1) mark(p);
     }
   }
+  atomicOr(bits + cw, (unsigned long long)cm);
   if (status) status[i] = st;
 }
 
