@@ -476,9 +476,19 @@ pack_tile_kernel(PackTileArgs a) {
   const bool first_sync = sum_fsw(sm[0]) == 0;
   // the tile's entry budget (| 0x100: the run is a raw run), waited for only when the tile's
   // first word goes on with the stretch the previous tile ended in
+#ifdef CPK_DIAG
+  uint64_t pwait = 0;  // (diagnostic) wall ticks wave 0 waited for the previous tile's exit budget
+#endif
   auto tile_entry = [&]() -> uint32_t {
     if (first_sync || T == 0) return 0u;
+#ifdef CPK_DIAG
+    const uint64_t w0c = wall_clock64();
+    const uint32_t v = wait_nonzero32(a.state + T - 1, a.err) & 0x1ffu;
+    pwait += wall_clock64() - w0c;
+    return v;
+#else
     return wait_nonzero32(a.state + T - 1, a.err) & 0x1ffu;
+#endif
   };
   const bool last_sync = sum_sync(sm[kWv - 1]);  // the exit went out before barrier A
   uint32_t bT = 0, bw = 0;
@@ -745,7 +755,7 @@ pack_tile_kernel(PackTileArgs a) {
     for (int k = 0; k < 5; k++) g_ptimeline[8 * T + k] = pk[k];
     g_ptimeline[8 * T + 5] = pout;
     g_ptimeline[8 * T + 6] = agg;
-    g_ptimeline[8 * T + 7] = __builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_ID
+    g_ptimeline[8 * T + 7] = pwait;  // wave 0's wait for the previous tile's exit budget
   }
 #endif
   if (a.frame_mode) {

@@ -64,6 +64,8 @@ def ptimeline(name):
     for k, nm in enumerate(["analysis", "emission", "decision", "copy_out"]):
         v = w[:, k + 1] - w[:, k]
         print(f"  {nm:9s} mean {v.mean():7.3f} us  [{pct(v)}]", flush=True)
+    bw = a[:, 7] / 100.0
+    print(f"  budget wait (wave 0) mean {bw.mean():.3f} us [{pct(bw)}] share waiting {np.mean(bw > 0):.3f}", flush=True)
     for o, nm in ((1, "in_time"), (2, "slot"), (3, "waited")):
         sel = a[:, 5] == o
         if sel.any():
