@@ -175,6 +175,21 @@ __device__ __forceinline__ void frame_message(const uint64_t* __restrict__ words
   if (status) status[i] = st;
 }
 
+// Workgroup b's tile-order index when consecutive tiles should share an XCD: workgroups are
+// dealt to the 8 XCDs round robin (b % 8 -- for speed only, nothing relies on it), so the j-th
+// workgroup of XCD x takes index (j / C) * 8C + x * C + j % C -- chunks of C consecutive indices
+// per XCD, a round of 8C over all of them.  (Deadlock-free as the plain order is: a tile waits
+// only on lower indices, all within its own round or before it, and a round of 8C workgroups is
+// far below the resident ones.)
+template <uint64_t C>
+__device__ __forceinline__ uint64_t xcd_order(uint64_t b, uint64_t G) {
+  constexpr uint64_t R = 8 * C;
+  const uint64_t full = (G / R) * R;
+  if (b >= full) return b;
+  const uint64_t x = b & 7, j = b >> 3;
+  return (j / C) * R + x * C + (j % C);
+}
+
 // Workgroup barrier ordering LDS only: __syncthreads also releases global memory at workgroup
 // scope, which waits for every outstanding vector memory operation -- stores, and loads issued
 // ahead for later use.
