@@ -140,12 +140,16 @@ __device__ __forceinline__ void frame_message(const uint64_t* __restrict__ words
   }
   const uint64_t nw = w1 - w0;
   const uint32_t* t32 = (const uint32_t*)(words + w0);
-  const uint64_t nseg = (uint64_t)t32[0] + 1;
+  // the table's first word in one load: the segment count and the first segment's size (a
+  // one-segment message needs no further load)
+  const uint64_t h0 = words[w0];
+  const uint64_t nseg = (uint64_t)(uint32_t)h0 + 1;
   const uint64_t tw = nseg / 2 + 1;
+  auto seg_size = [&](uint64_t s) -> uint64_t { return s == 0 ? (h0 >> 32) : t32[s + 1]; };
   bool ok = tw <= nw;
   if (ok) {
     uint64_t total = tw;
-    for (uint64_t s = 0; s < nseg && total <= nw; s++) total += t32[s + 1];
+    for (uint64_t s = 0; s < nseg && total <= nw; s++) total += seg_size(s);
     ok = total == nw;
   }
   // the chunk starts gathered per bitmap word: one atomic per word touched (the message start and
@@ -167,7 +171,7 @@ __device__ __forceinline__ void frame_message(const uint64_t* __restrict__ words
     uint64_t p = w0 + tw;
     if (p < w1) mark(p);
     for (uint64_t s = 0; s + 1 < nseg; s++) {
-      p += t32[s + 1];
+      p += seg_size(s);
       if (p < w1) mark(p);
     }
   }

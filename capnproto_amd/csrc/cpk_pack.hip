@@ -483,6 +483,9 @@ pack_tile_kernel(PackTileArgs a) {
 #endif
   auto tile_entry = [&]() -> uint32_t {
     if (first_sync || T == 0) return 0u;
+#ifdef CPK_ABLATE_NOENTRY
+    return 0u;  // (ablation only: wrong bytes) no wait for the previous tile's exit budget
+#endif
 #ifdef CPK_DIAG
     const uint64_t w0c = wall_clock64();
     const uint32_t v = wait_nonzero32(a.state + T - 1, a.err) & 0x1ffu;
@@ -643,8 +646,13 @@ pack_tile_kernel(PackTileArgs a) {
     uint32_t o = woff + loff;  // tile byte offset of the lane's next record
     const uint32_t lbase = (uint32_t)(kWW * w + kK * l);
     uint64_t sel_next = sel_tab[etags[0] & 0xffu];
+#ifdef CPK_ABLATE_EMIT
+    constexpr int kEmitK = CPK_ABLATE_EMIT;  // (ablation only: wrong bytes) words emitted per lane
+#else
+    constexpr int kEmitK = kK;
+#endif
 #pragma unroll
-    for (int k = 0; k < kK; k++) {
+    for (int k = 0; k < kEmitK; k++) {
       const uint32_t lo = xlo[k], hi = xhi[k];
       const uint32_t tg = (etags[k >> 2] >> (8 * (k & 3))) & 0xffu;
       const uint64_t sel = sel_next;
@@ -855,12 +863,14 @@ __global__ __launch_bounds__(256) void pack_place_kernel(PackTileArgs a) {
   if (a.pos) {
     const uint64_t i1 = s_pos[1];
     for (uint64_t i = s_pos[0] + (uint64_t)tid; i < i1; i += 256) {
+      // both loads issued before either is waited for (the tile-relative offset does not wait
+      // for the position)
       const uint64_t p = a.pos[i];
+      const uint64_t rel = a.pos_out[i];
       const uint64_t T = min(p / kPackTileWords, a.ntiles - 1);
       const uint32_t j = (uint32_t)(T - T0);
       if (j >= (uint32_t)kPlaceGroup) continue;  // (unsorted positions: not this group's)
-      if (T + 1 == a.ntiles && p >= a.nwords) a.pos_out[i] = s_off[j] + s_n[j];
-      else a.pos_out[i] += s_off[j];
+      a.pos_out[i] = (T + 1 == a.ntiles && p >= a.nwords) ? s_off[j] + s_n[j] : rel + s_off[j];
     }
   }
   // the tiles in the arena: one wave per tile

@@ -21,7 +21,7 @@ for v in ${VARIANTS:-base}; do
 import csv, sys
 rows = list(csv.DictReader(open(sys.argv[1])))
 print("==", sys.argv[2], " ".join(f'{r["Name"].replace("(anonymous namespace)::", "").split("(")[0].split("::")[-1][:22]}={float(r["AverageNs"])/1e3:.1f}'
-      for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:9] if "cpk" in r["Name"]))
+      for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:9] if "cpk" in r["Name"] and "copy_kernel" not in r["Name"] and "gen_" not in r["Name"]))
 PY
   done
 done
