@@ -180,7 +180,10 @@ __device__ __forceinline__ uint32_t sum_exit(uint32_t s) { return (s >> 16) & 0x
 // and the nearest inclusive prefix is usually a few tiles back), then 64 per round trip.
 // wait == false: gives up (false) when one before the nearest inclusive prefix has not
 // published its byte count yet, or after 272 predecessors (one round trip instead: C3 pack_tile
-// 2.18 -> 3.05 ms, fewer tiles resolve in time and more wait).
+// 2.18 -> 3.05 ms, fewer tiles resolve in time and more wait).  wait == true re-reads the blocked
+// window with every lane; measured and not kept: one lane polling the blocking descriptor (C2 /
+// C3 / C4 pack_tile +5 / +6 / +9 %), 128 or 256 tiles per round trip (C3 +7 / +15 %), the 64
+// nearest tiles read again beside a blocked window or beside every far one (C2 +5 / +12 %).
 __device__ __forceinline__ bool pack_lookback(const uint64_t* desc, uint64_t t, uint64_t* out,
                                               bool wait, uint32_t* err) {
   const int l = lane_id() + (int)opaque_zero();  // (addresses not hoisted out of the caller's loop)
