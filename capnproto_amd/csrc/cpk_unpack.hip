@@ -1799,7 +1799,7 @@ unpack_tiles_kernel(UnpackArgs a) {
   // the phases later tiles wait on (chain 0, the entry, the descriptors) ahead of other waves'
   // expansions in the SIMD's issue arbitration (C4 unpack_tiles 4.51 -> 4.21 ms; no gain on C2)
   if (a.prio) __builtin_amdgcn_s_setprio(2);
-  CPK_DIAG_ONLY(uint64_t ck[7]; uint64_t wk[7]; ck[0] = clock64(); wk[0] = wall_clock64());
+  CPK_DIAG_ONLY(uint64_t ck[7]; uint64_t wk[7]; uint64_t wflat = 0; ck[0] = clock64(); wk[0] = wall_clock64());
   // the header launch is done: its scan descriptors go back to zero for the next call
   for (uint64_t i = t + a.ntiles * (uint64_t)l; i < a.hdr_nblocks; i += 64 * a.ntiles)
     a.hdr_desc[i] = 0;
@@ -2021,7 +2021,10 @@ unpack_tiles_kernel(UnpackArgs a) {
     }
     if (FLAT && !has_start) {
       // flat stream: the exit and words for the entry the predecessor's AGG exit gives
+      CPK_DIAG_ONLY(const uint64_t wa0 = wall_clock64());
       const uint64_t dp = wait_nonzero64(a.desc + t - 1, a.err);
+      // (diagnostic) AGG published, predecessor's AGG seen: ticks after the tile's start
+      CPK_DIAG_ONLY(wflat = (wa0 - wk[0]) | ((wall_clock64() - wk[0]) << 32));
       const uint32_t E2 = entry_from_exit(desc_exit(dp), fms);
       uint64_t d2 = kD2None;
       if (E2 != Eopt && E2 <= (uint32_t)kB) {
@@ -2091,7 +2094,7 @@ unpack_tiles_kernel(UnpackArgs a) {
   for (int k = 0; k < 6; k++) diag_add(16 + k, ck[k + 1] - ck[k]);
   if (l == 0 && t < (uint64_t)kTimelineTiles) {
     for (int k = 0; k < 7; k++) g_timeline[8 * t + k] = wk[k];
-    g_timeline[8 * t + 7] = __builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_ID
+    g_timeline[8 * t + 7] = FLAT ? wflat : __builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_ID
   }
 #endif
 }

@@ -129,6 +129,32 @@ def timeline(name, ntiles):
     gap = w[1:, 2] - w[:-1, 2]  # x0p publish: tile t's minus tile t - 1's
     print(f"  x0p publish t minus t-1 us [{pct(gap)}]  se values {np.unique(se)[:8]} cu {np.unique(cu)[:16]}",
           flush=True)
+def flat_entry_detail():
+    """Flat decode: where the slow entries go -- AGG publication (wa: ticks after the tile's
+    start) and the predecessor's AGG seen (wb), from slot 7 of the diagnostic timeline."""
+    if tl is None:
+        return
+    import numpy as np
+    a = np.frombuffer(tl, dtype=np.uint64).reshape(TL_N, 8).astype(np.int64)
+    ok = a[:, 0] > 0
+    idx = np.nonzero(ok)[0]
+    a = a[ok]
+    wa = (a[:, 7] & 0xffffffff) / 100.0
+    wb = (a[:, 7] >> 32) / 100.0
+    ent = (a[:, 4] - a[:, 3]) / 100.0
+    pct = lambda v: " ".join(f"{q}:{np.percentile(v, q):.2f}" for q in (10, 50, 90, 99))
+    print(f"  flat: AGG published at [{pct(wa)}] us; waited for predecessor's AGG [{pct(wb - wa)}] us;"
+          f" after it [{pct((a[:, 4] - a[:, 0]) / 100.0 - wb)}] us", flush=True)
+    slow = np.argsort(-ent)[:12]
+    t0 = a[:, 0].min()
+    for j in slow:
+        t = idx[j]
+        print(f"   slow entry tile {t} (t%4={t % 4}) entry {ent[j]:.1f} start {(a[j, 0] - t0) / 100:.1f}"
+              f" agg@{wa[j]:.1f} pred_agg_seen@{wb[j]:.1f} chain0 {(a[j, 2] - a[j, 1]) / 100:.1f}", flush=True)
+    w4 = np.array([ent[(idx % 4) == k].mean() for k in range(4)])
+    print("  flat: entry mean by wave", " ".join(f"{x:.2f}" for x in w4), flush=True)
+
+
 codec = capnproto_amd.Codec(0)
 buf = (C.c_uint64 * 32)()
 for name in sys.argv[2:]:
@@ -149,6 +175,7 @@ for name in sys.argv[2:]:
         codec.sync()
         assert L.cpk_debug_diag(buf, 1) == 0
         timeline(name, 1 << 30)
+        flat_entry_detail()
         t = max(buf[0], 1)
         print(name, "messages", int(res[4].item()), "tiles", buf[0], " ".join(
             f"{NAMES[k]}={buf[k] / t:.3f}" for k in range(1, len(NAMES)) if NAMES[k] != "-"), flush=True)
