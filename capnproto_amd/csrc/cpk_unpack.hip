@@ -946,6 +946,9 @@ __device__ __forceinline__ uint32_t mask_words(const uint8_t* d, int s, uint64_t
   return w;
 }
 
+#ifndef CPK_ENTER_CHAIN_C
+#define CPK_ENTER_CHAIN_C 1
+#endif
 // The chain entered at tile byte E (0 < E < fms) replaces chain 0's record starts before the
 // point where it meets chain 0.  Lane 0 walks it record by record (one LDS round trip per
 // record) for up to kMergeCap records; a chain still running beside chain 0 then (interleaved
@@ -995,6 +998,14 @@ __device__ uint64_t enter_chain(const uint8_t* d, uint64_t* aux, const SubTile& 
     int xB = kDead;
     // (B's records are clipped at the first message start after the tile, as chain 0's are)
     if (notA) xB = walk(d, st, st.s + lowest_bit(notA), tm0, &chB);
+#if CPK_ENTER_CHAIN_C
+    // a third chain C from the first byte neither chain starts a record at (walked until it meets
+    // chain 0 or B): text parsed as records runs as several interleaved chains
+    const uint64_t notAB = notA & ~chB;
+    uint64_t chC = 0;
+    int xC = kDead;
+    if (notAB) xC = walk(d, st, st.s + lowest_bit(notAB), tm0 | chB, &chC);
+#endif
     for (int k = 0; k < 2 * kB && p < fms && p < kB; k++) {
       const int j = p >> 6, b = p & 63;
       if ((readlane64(tm0, j) >> b) & 1) break;
@@ -1004,9 +1015,17 @@ __device__ uint64_t enter_chain(const uint8_t* d, uint64_t* aux, const SubTile& 
         cur = j;
       }
       const uint64_t Bj = readlane64(chB, j);
+#if CPK_ENTER_CHAIN_C
+      const uint64_t Cj = readlane64(chC, j);
+#endif
       if ((Bj >> b) & 1) {
         fm |= Bj & ~mask_lt(b);
         p = (int)readlane32((uint32_t)xB, j);
+#if CPK_ENTER_CHAIN_C
+      } else if ((Cj >> b) & 1) {
+        fm |= Cj & ~mask_lt(b);
+        p = (int)readlane32((uint32_t)xC, j);
+#endif
       } else {
         fm |= 1ull << b;
         p += step_len(d[p], d[p + 9]);
