@@ -77,7 +77,10 @@ __device__ __forceinline__ void diag_trips(int k, int n) {
 #else
 #define CPK_DIAG_ONLY(x)
 #endif
-constexpr int kMergeCap = 48;               // entry-walk records before the jump walk
+#ifndef CPK_MERGE_CAP
+#define CPK_MERGE_CAP 8
+#endif
+constexpr int kMergeCap = CPK_MERGE_CAP;               // entry-walk records before the jump walk
 
 // status codes (include/cpk.h)
 constexpr int32_t kOK = 0, kEOF = 1, kOvershoot = 2, kTooMany = 3, kTooLarge = 4, kInvalid = 5;
@@ -946,14 +949,21 @@ __device__ __forceinline__ uint32_t mask_words(const uint8_t* d, int s, uint64_t
   return w;
 }
 
-#ifndef CPK_ENTER_CHAIN_C
-#define CPK_ENTER_CHAIN_C 1
+// Chains beside chain 0 that enter_chain's jump walk follows: chain k of a sub-tile starts at
+// its first byte neither chain 0 nor chains 1 .. k-1 start a record at (text parsed as records
+// runs as several interleaved chains).  Stream split with the lane-0 walk capped at 48 records:
+// 16.0 / 14.3 / 13.6 ms with 1 / 2 / 3 chains; capped at 16: 13.5 ms with 3, 13.3 with 4, 15.7
+// with 6 (registers: C2 unpack_tiles 225 -> 257 us); 4 chains capped at 8: 13.2 ms.  The message
+// decode is unchanged within noise (C2 / C4 unpack_tiles 225 / 4370 -> 220 / 4351 us).
+#ifndef CPK_ENTER_CHAINS
+#define CPK_ENTER_CHAINS 4
 #endif
+constexpr int kEnterChains = CPK_ENTER_CHAINS;
 // The chain entered at tile byte E (0 < E < fms) replaces chain 0's record starts before the
 // point where it meets chain 0.  Lane 0 walks it record by record (one LDS round trip per
 // record) for up to kMergeCap records; a chain still running beside chain 0 then (interleaved
-// chains that meet late, or never) is continued by all lanes in step, jumping along each
-// sub-tile's second chain B (from its first byte chain 0 does not start a record at).  Returns
+// chains that meet late, or never) is continued by all lanes in step, jumping along the
+// sub-tiles' other chains (kEnterChains of them) where it meets one of them.  Returns
 // the lane's true record-start mask; *exit is chain 0's exit when the chains meet (or the walk
 // reaches the first message start, where every chain restarts), else where the entry's chain
 // leaves the tile.  *runs gains the run records of the walked starts.
@@ -993,19 +1003,19 @@ __device__ uint64_t enter_chain(const uint8_t* d, uint64_t* aux, const SubTile& 
     fm = readlane64(fm, 0);
     const uint64_t vm = st.vend <= st.s ? 0ull : (st.vend >= st.s + 64 ? ~0ull
                                                                      : mask_lt(st.vend - st.s));
-    const uint64_t notA = ~tm0 & vm;
-    uint64_t chB = 0;
-    int xB = kDead;
-    // (B's records are clipped at the first message start after the tile, as chain 0's are)
-    if (notA) xB = walk(d, st, st.s + lowest_bit(notA), tm0, &chB);
-#if CPK_ENTER_CHAIN_C
-    // a third chain C from the first byte neither chain starts a record at (walked until it meets
-    // chain 0 or B): text parsed as records runs as several interleaved chains
-    const uint64_t notAB = notA & ~chB;
-    uint64_t chC = 0;
-    int xC = kDead;
-    if (notAB) xC = walk(d, st, st.s + lowest_bit(notAB), tm0 | chB, &chC);
-#endif
+    // (the chains' records are clipped at the first message start after the tile, as chain 0's
+    // are; each is walked until it meets chain 0 or an earlier one)
+    uint64_t ch[kEnterChains];
+    int xc[kEnterChains];
+    uint64_t taken = tm0, left = ~tm0 & vm;
+#pragma unroll
+    for (int c = 0; c < kEnterChains; c++) {
+      ch[c] = 0;
+      xc[c] = kDead;
+      if (left) xc[c] = walk(d, st, st.s + lowest_bit(left), taken, &ch[c]);
+      taken |= ch[c];
+      left &= ~ch[c];
+    }
     for (int k = 0; k < 2 * kB && p < fms && p < kB; k++) {
       const int j = p >> 6, b = p & 63;
       if ((readlane64(tm0, j) >> b) & 1) break;
@@ -1014,19 +1024,17 @@ __device__ uint64_t enter_chain(const uint8_t* d, uint64_t* aux, const SubTile& 
         fm = 0;
         cur = j;
       }
-      const uint64_t Bj = readlane64(chB, j);
-#if CPK_ENTER_CHAIN_C
-      const uint64_t Cj = readlane64(chC, j);
-#endif
-      if ((Bj >> b) & 1) {
-        fm |= Bj & ~mask_lt(b);
-        p = (int)readlane32((uint32_t)xB, j);
-#if CPK_ENTER_CHAIN_C
-      } else if ((Cj >> b) & 1) {
-        fm |= Cj & ~mask_lt(b);
-        p = (int)readlane32((uint32_t)xC, j);
-#endif
-      } else {
+      bool jumped = false;
+#pragma unroll
+      for (int c = 0; c < kEnterChains; c++) {
+        const uint64_t Cj = readlane64(ch[c], j);
+        if (!jumped && ((Cj >> b) & 1)) {
+          fm |= Cj & ~mask_lt(b);
+          p = (int)readlane32((uint32_t)xc[c], j);
+          jumped = true;
+        }
+      }
+      if (!jumped) {
         fm |= 1ull << b;
         p += step_len(d[p], d[p + 9]);
       }
