@@ -31,6 +31,11 @@ struct cpk_ctx {
   // message, chunk offsets), [4] cpk_split_packed_stream (call state, record-head map)
   void* stage[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
   size_t stage_size[5] = {0, 0, 0, 0, 0};
+  // the stream split's record-head map (in stage[4]) as last laid out: its memory and extent
+  // (a reallocation always changes the size: a new allocation at the old address is caught)
+  void* split_map = nullptr;
+  size_t split_map_size = 0;
+  uint64_t split_map_words = 0;
   // measurement hooks: [0] pack (tile, scan, placement), [1] unpack (the tile kernel after the
   // header launch), [2] the unpack tile kernel alone
   bool timing = false;
@@ -520,8 +525,9 @@ cpk_status unpack_common(cpk_ctx* ctx, uint32_t mode, const uint8_t* d_packed, u
                          uint64_t* d_words, uint64_t cap, uint64_t* d_word_off_out,
                          int32_t* d_status, uint64_t* d_size_out, uint64_t limit,
                          hipStream_t stream, uint64_t* d_in_end = nullptr,
-                         uint64_t* d_rec_pos = nullptr, bool store_free = false) {
-  if (!ctx || (!d_in_off && n) || (!d_packed && P) || (!d_status && n))
+                         uint64_t* d_rec_pos = nullptr, bool store_free = false,
+                         const uint64_t* d_rec_gen = nullptr) {
+  if (!ctx || (!d_in_off && n) || (!d_packed && P) || (!d_status && n) || (d_rec_pos && !d_rec_gen))
     return CPK_ERR_INVALID_ARGUMENT;
   if (hipSetDevice(ctx->device) != hipSuccess) return CPK_ERR_HIP;
   if (order_streams(ctx, stream) != CPK_OK) return CPK_ERR_HIP;
@@ -580,6 +586,7 @@ cpk_status unpack_common(cpk_ctx* ctx, uint32_t mode, const uint8_t* d_packed, u
   a.size_out = d_size_out;
   a.in_end = d_in_end;
   a.rec_pos = d_rec_pos;
+  a.rec_gen = d_rec_gen;
   a.mode = mode;
   a.ntiles = ntiles;
   a.desc = s.desc;
@@ -910,29 +917,41 @@ cpk_status cpk_split_packed_stream(cpk_ctx* ctx, const uint8_t* d_packed, uint64
   const uint64_t limit = limits ? limits->traversal_limit_words : 8ull * 1024 * 1024;
   hipStream_t s = (hipStream_t)stream;
   if (order_streams(ctx, s) != CPK_OK) return CPK_ERR_HIP;
-  // the record-head map (one u64 per output word) and 8 words of call state: in_off[2],
-  // word_off[2], meta[4] (stop byte, stop word, decode status)
+  // (record positions share their u64 with the call's generation: kRecGenShift bits)
+  if (nbytes >> cpk::kRecGenShift) return CPK_ERR_INVALID_ARGUMENT;
+  // the record-head map (one u64 per output word) after 16 words of state: in_off[2],
+  // word_off[2], meta[4] (stop byte, stop word, decode status), the map's generation and fill
+  // flag (kept from call to call)
   const uint64_t rp_bytes = align16(words_capacity * 8 + 128);
   cpk_status st = ensure(&ctx->stage[4], &ctx->stage_size[4],
                          rp_bytes + cpk::split_scratch_bytes(words_capacity));
   if (st != CPK_OK) return st;
   uint64_t* state = (uint64_t*)ctx->stage[4];
-  uint64_t* rec_pos = state + 8;
   uint64_t* meta = state + 4;
+  uint64_t* genw = state + 8;
+  uint32_t* fillw = (uint32_t*)(state + 9);
+  uint64_t* rec_pos = state + 16;
   void* split_scr = (char*)ctx->stage[4] + rp_bytes;
+  // the map is filled when its memory or extent is new to it (the scratch after it moves with
+  // the extent) or the generation wraps; otherwise the generation moves on and old entries stop
+  // counting
+  const bool fresh = ctx->split_map != ctx->stage[4] || ctx->split_map_size != ctx->stage_size[4] ||
+                     ctx->split_map_words != words_capacity;
   hipError_t e = cpk::launch_set_u64x4(state, 0, nbytes, 0, words_capacity, s);
   if (e == hipSuccess) e = cpk::launch_set_u64x4(meta, 0, 0, CPK_ERR_PREMATURE_EOF, 0, s);
-  if (e == hipSuccess && words_capacity)
-    e = cpk::launch_fill(rec_pos, words_capacity * 8, 0xff, s);
+  if (e == hipSuccess) e = cpk::launch_split_gen(genw, fillw, fresh, rec_pos, words_capacity * 8, s);
   if (e != hipSuccess) return CPK_ERR_HIP;
+  ctx->split_map = ctx->stage[4];
+  ctx->split_map_size = ctx->stage_size[4];
+  ctx->split_map_words = words_capacity;
   if (nbytes) {
     // the whole stream as one flat chunk of up to words_capacity words, stopping at the first
     // record the input cuts (prefix mode: meta[0..1] = where it stopped)
     st = unpack_common(ctx, 1, d_packed, nbytes, state, 1, state + 2, d_words, words_capacity,
-                       nullptr, (int32_t*)(meta + 2), meta + 1, 0, s, meta, rec_pos);
+                       nullptr, (int32_t*)(meta + 2), meta + 1, 0, s, meta, rec_pos, false, genw);
     if (st != CPK_OK) return st;
   }
-  return hip_status(cpk::launch_split_walk(d_packed, nbytes, d_words, rec_pos, meta, max_msgs,
+  return hip_status(cpk::launch_split_walk(d_packed, nbytes, d_words, rec_pos, genw, meta, max_msgs,
                                            limit, words_capacity, split_scr, d_msg_word_off,
                                            d_msg_in_off, d_status, d_nmsgs, s));
 }

@@ -92,7 +92,10 @@ struct UnpackArgs {
   int32_t* status;
   uint64_t* size_out;           // mode 2
   uint64_t* in_end;             // optional: packed byte where each message actually ends
-  uint64_t* rec_pos;            // optional: packed byte of the record whose head is word i
+  uint64_t* rec_pos;            // optional: packed byte of the record whose head is word i,
+                                // tagged with the call's generation (rec_tag below)
+  const uint64_t* rec_gen;      // with rec_pos: the call's generation (device word; the tag is
+                                // gen << kRecGenShift)
   uint32_t mode;                // 0 messages, 1 exact-size chunks (flat-packed), 2 size only
   uint64_t ntiles;
   uint64_t* desc;               // ntiles tile descriptors (cpk_unpack.hip), zeroed
@@ -117,6 +120,14 @@ struct UnpackArgs {
   uint32_t prio;                // batches of very long messages: raised wave priority (cpk_unpack.hip)
 };
 constexpr uint64_t kUnpackFuseMsgs = 256;
+
+// The stream split's record-head map holds (gen << kRecGenShift) | packed byte for a record head,
+// anything else elsewhere: an entry counts only with the call's generation, so the map is filled
+// (0xff bytes: generation 0xffffff, never a call's) only when its layout changes or the
+// generation counter wraps, not on every call (the fill of a 3.55 GiB stream's map: 0.61 ms).
+constexpr int kRecGenShift = 40;
+constexpr uint64_t kRecPosMask = (1ull << kRecGenShift) - 1;
+constexpr uint64_t kRecGenMax = 1ull << 23;
 
 // Unpack stages (launch_unpack_stage), in launch order: the tile kernel is the only one.
 constexpr int kUnpackTiles = 0;
@@ -157,8 +168,13 @@ hipError_t launch_set_u64x4(uint64_t* dst, uint64_t v0, uint64_t v1, uint64_t v2
 // The message chain over the decoded words, block-parallel (cpk_stream.hip); scratch holds
 // split_scratch_bytes(words_capacity).
 uint64_t split_scratch_bytes(uint64_t words_capacity);
+// The split's generation (device word genw): the next one, or 1 when `force` (a new map layout)
+// or on wrap-around, which also sets *fill; then the map is filled where *fill says so.
+hipError_t launch_split_gen(uint64_t* genw, uint32_t* fill, bool force, uint64_t* rec_pos,
+                            uint64_t nbytes, hipStream_t stream);
 hipError_t launch_split_walk(const uint8_t* packed, uint64_t nbytes, const uint64_t* words,
-                             const uint64_t* rec_pos, const uint64_t* meta, uint64_t max_msgs,
+                             const uint64_t* rec_pos, const uint64_t* rec_gen,
+                             const uint64_t* meta, uint64_t max_msgs,
                              uint64_t limit, uint64_t words_capacity, void* scratch,
                              uint64_t* msg_word_off, uint64_t* msg_in_off, int32_t* status,
                              uint64_t* nmsgs, hipStream_t stream);

@@ -82,18 +82,26 @@ struct Flat {
   const uint8_t* packed;
   uint64_t nbytes;
   const uint64_t* rec_pos;
+  const uint64_t* rec_gen;  // (device) the call's generation: rec_pos entries of other calls
+                            // (or of none) do not count
   const uint64_t* meta;  // (device) where the flat decode stopped: packed byte, word, status
   uint64_t Bc, Tc;  // packed byte / word where the flat decode stopped
+  uint64_t gen;
   bool capped;      // ... because the output was full, not because the input ended
 
   __device__ void load() {
     Bc = meta[0];
     Tc = meta[1];
+    gen = *rec_gen;
     capped = (int32_t)meta[2] != sEOF && Bc < nbytes;
   }
 
   // packed byte of the record whose head is word x (x <= Tc); kNone inside a run
-  __device__ uint64_t head(uint64_t x) const { return x == Tc ? Bc : rec_pos[x]; }
+  __device__ uint64_t head(uint64_t x) const {
+    if (x == Tc) return Bc;
+    const uint64_t v = rec_pos[x];
+    return (v >> kRecGenShift) == gen ? (v & kRecPosMask) : kNone;
+  }
 
   // A read that has to end at word x > Tc meets the record at Bc first: the reference checks a
   // raw run's count against the read before it needs the run's bytes (serialize-packed.c++:
@@ -308,7 +316,7 @@ __global__ __launch_bounds__(64) void split_spec_kernel(Flat F, const uint64_t* 
       bool cand = false;
       uint64_t hp = kNone;
       if (p < lim) {
-        hp = F.rec_pos[p];
+        hp = F.head(p);  // (p < Tc)
         if (hp != kNone && (uint32_t)words[p] < 511) {
           uint64_t x = 0, hx = 0, single = 0;
           if (message_at(F, words, p, limit, &x, &hx, &single) == sOK) {
@@ -832,8 +840,40 @@ uint64_t split_scratch_bytes(uint64_t words_capacity) {
   return nb * (sizeof(SplitBlock) + 8ull * kSplitList) + 64;
 }
 
+__global__ void split_gen_kernel(uint64_t* genw, uint32_t* fill, int force) {
+  uint64_t g = force ? 1 : *genw + 1;
+  if (g >= kRecGenMax) {
+    g = 1;
+    force = 1;
+  }
+  *genw = g;
+  *fill = force ? 1u : 0u;
+}
+
+// the map fill when split_gen_kernel asks for it (a grid of 4096 blocks that exit at once
+// otherwise)
+__global__ void fill_if_kernel(uint64_t* __restrict__ p, uint64_t nw, const uint32_t* fill) {
+  if (!*fill) return;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nw;
+       i += (uint64_t)gridDim.x * blockDim.x)
+    p[i] = ~0ull;
+}
+
+hipError_t launch_split_gen(uint64_t* genw, uint32_t* fill, bool force, uint64_t* rec_pos,
+                            uint64_t nbytes, hipStream_t stream) {
+  split_gen_kernel<<<1, 1, 0, stream>>>(genw, fill, force ? 1 : 0);
+  const uint64_t nw = nbytes / 8;
+  if (nw) {
+    uint64_t blocks = (nw + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    fill_if_kernel<<<(unsigned)blocks, 256, 0, stream>>>(rec_pos, nw, fill);
+  }
+  return hipGetLastError();
+}
+
 hipError_t launch_split_walk(const uint8_t* packed, uint64_t nbytes, const uint64_t* words,
-                             const uint64_t* rec_pos, const uint64_t* meta, uint64_t max_msgs,
+                             const uint64_t* rec_pos, const uint64_t* rec_gen,
+                             const uint64_t* meta, uint64_t max_msgs,
                              uint64_t limit, uint64_t words_capacity, void* scratch,
                              uint64_t* msg_word_off, uint64_t* msg_in_off, int32_t* status,
                              uint64_t* nmsgs, hipStream_t stream) {
@@ -841,6 +881,7 @@ hipError_t launch_split_walk(const uint8_t* packed, uint64_t nbytes, const uint6
   F.packed = packed;
   F.nbytes = nbytes;
   F.rec_pos = rec_pos;
+  F.rec_gen = rec_gen;
   F.meta = meta;
   const uint64_t nb = words_capacity / kSplitBlock + 1;
   SplitBlock* blocks = (SplitBlock*)scratch;

@@ -580,7 +580,7 @@ __device__ __forceinline__ int32_t handle_record(const UnpackArgs& a_unused, con
   if (st == kOK && !mi.fits) st = kCap;
   if (mi.fits && !trunc1) {
     if (a.words) a.words[mi.base + wb] = word;  // (NULL: a skip, nothing stored)
-    if (a.rec_pos) a.rec_pos[mi.base + wb] = pabs;
+    if (a.rec_pos) a.rec_pos[mi.base + wb] = pabs | (*a.rec_gen << kRecGenShift);
     uint64_t n = cnt;
     if (over) n = mi.total - wb - 1;
     if (trunc3) {
@@ -1666,7 +1666,7 @@ __device__ __forceinline__ void expand_lean(const UnpackArgs& a, uint64_t A, con
       if (put) {
         wp[0] = word;
         if (cnt != 0 && inl) wp[1] = rw;
-        if (a.rec_pos) a.rec_pos[wp - a.words] = A + p;
+        if (a.rec_pos) a.rec_pos[wp - a.words] = (A + p) | (*a.rec_gen << kRecGenShift);
       }
       if (ballot(special)) {
         const uint64_t mbase = msb ? shfl64(win.base, wl) : cbase;

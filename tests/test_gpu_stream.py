@@ -239,6 +239,39 @@ def test_split_limit_and_cut_in_later_blocks(codec):
     assert torch.equal(w2[:mw], words[:mw])
 
 
+def test_split_map_generations(codec):
+    """Back-to-back splits of different streams into one output extent: the record-head map is
+    filled only when its layout changes, so each call's heads must count and the previous
+    call's must not (generation-tagged entries) -- including a call after a cut stream and after
+    a call of another extent, which refills the map."""
+    import torch
+
+    n = 1 << 14
+    streams = [_mixed_stream(codec, n, seed) for seed in (21, 22, 23)]
+    cap = max(s[4] for s in streams) + 16
+    for k in (0, 1, 2, 0, 1):
+        words, off, packed, poff, total, nbytes = streams[k]
+        w2, woff, ioff, status, cnt = codec.split_packed_stream(packed, cap, n + 1, nbytes=nbytes)
+        codec.sync()
+        assert int(cnt.item()) == n and int(status[n].item()) == P.OK, k
+        assert torch.equal(woff[:n + 1], off) and torch.equal(ioff[:n + 1], poff), k
+        assert torch.equal(w2[:total], words[:total]), k
+    # a cut stream, then another extent (the map refilled), then the first extent again
+    words, off, packed, poff, total, nbytes = streams[2]
+    m = n // 2
+    cut = int(poff[m].item()) + 5
+    w2, woff, ioff, status, cnt = codec.split_packed_stream(packed, cap, n + 1, nbytes=cut)
+    codec.sync()
+    assert int(cnt.item()) == m and int(status[m].item()) == P.PREMATURE_EOF
+    for c in (cap + 4096, cap):
+        words, off, packed, poff, total, nbytes = streams[1]
+        w2, woff, ioff, status, cnt = codec.split_packed_stream(packed, c, n + 1, nbytes=nbytes)
+        codec.sync()
+        assert int(cnt.item()) == n and int(status[n].item()) == P.OK
+        assert torch.equal(woff[:n + 1], off) and torch.equal(ioff[:n + 1], poff)
+        assert torch.equal(w2[:total], words[:total])
+
+
 def test_split_messages_longer_than_blocks(codec):
     """Messages of 150 Ki words, longer than the split's 64 Ki-word blocks, between runs of small
     ones: blocks a message passes over take the in-order pass's serial path between windows it
