@@ -165,7 +165,9 @@ cpk_status cpk_unpack_messages(cpk_ctx* ctx, const uint8_t* d_packed, uint64_t t
  *                                  failure for the next message (PREMATURE_EOF, RUN_OVERSHOOT,
  *                                  TOO_MANY_SEGMENTS, MESSAGE_TOO_LARGE) or CPK_ERR_CAPACITY
  *                                  when it does not fit words_capacity.
- * The three arrays need max_msgs + 1 entries.  limits may be NULL (reference defaults). */
+ * The three arrays need max_msgs + 1 entries.  limits may be NULL (reference defaults).
+ * nbytes < 2^40 (CPK_ERR_INVALID_ARGUMENT otherwise: record positions share a word with the
+ * call's generation). */
 cpk_status cpk_split_packed_stream(cpk_ctx* ctx, const uint8_t* d_packed, uint64_t nbytes,
                                    uint64_t* d_words, uint64_t words_capacity, uint64_t max_msgs,
                                    uint64_t* d_msg_word_off, uint64_t* d_msg_in_off,
