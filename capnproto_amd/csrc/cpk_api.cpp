@@ -557,7 +557,7 @@ cpk_status unpack_common(cpk_ctx* ctx, uint32_t mode, const uint8_t* d_packed, u
     if (n == 0) return hip_status(cpk::launch_fill(d_word_off_out, 8, 0, stream));
     if ((st = ensure_hdr_desc(ctx, n)) != CPK_OK) return st;
     if (!fuse) {
-      e = cpk::launch_unpack_header(d_packed, d_in_off, n, limit, d_word_off_out, s.hdr_status,
+      e = cpk::launch_unpack_header(d_packed, P, d_in_off, n, limit, d_word_off_out, s.hdr_status,
                                     d_status, ctx->hdr_desc, ctx->err, tf, stream);
       if (e != hipSuccess) return CPK_ERR_HIP;
     }

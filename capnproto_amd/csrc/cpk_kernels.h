@@ -146,7 +146,8 @@ unsigned long long* debug_stamps(int which);
 // descriptors `desc` -- header_scan_blocks(n) u64 -- are zero on entry and cleared again by the
 // tile kernel through UnpackArgs::hdr_desc); word_off gets n + 1 entries.
 uint64_t header_scan_blocks(uint64_t n);
-hipError_t launch_unpack_header(const uint8_t* packed, const uint64_t* in_off, uint64_t n,
+hipError_t launch_unpack_header(const uint8_t* packed, uint64_t P, const uint64_t* in_off,
+                                uint64_t n,
                                 uint64_t limit, uint64_t* word_off, int32_t* hdr_status,
                                 int32_t* status, uint64_t* desc, uint32_t* err,
                                 const TileFirstJob& tf, hipStream_t stream);

@@ -132,20 +132,16 @@ __device__ int32_t decode_exact(const uint8_t* b, uint64_t& p, uint64_t end, uin
 
 // 1. Message headers (serialize.c++:202-242): the flat size of message m in words (segment
 // table + segments), 0 when the header fails (its status says why).
-__device__ __forceinline__ uint64_t header_words(const uint8_t* __restrict__ packed,
-                                                 const uint64_t* __restrict__ in_off, uint64_t m,
-                                                 uint64_t limit, int32_t* st_out) {
-  uint64_t p = in_off[m];
-  const uint64_t end = in_off[m + 1];
+// (v0, v1: the message's first 16 packed bytes, read by the caller when end - p >= 16)
+__device__ __forceinline__ uint64_t header_words_v(const uint8_t* __restrict__ packed, uint64_t p,
+                                                   uint64_t end, uint64_t v0, uint64_t v1,
+                                                   uint64_t limit, int32_t* st_out) {
   uint64_t first = 0;
   int32_t st;
   if (end - p >= 16) {
     // the first word's record (<= 10 bytes) from one 16-byte read: decode_exact's steps for
     // one word, with every byte present (a run record's count must be 0 -- it may not cross
     // word 1 -- so its raw bytes are never needed)
-    uint64_t v0, v1;
-    __builtin_memcpy(&v0, packed + p, 8);
-    __builtin_memcpy(&v1, packed + p + 8, 8);
     auto byte_at = [&](uint32_t k) -> uint32_t {
       return (uint32_t)((k < 8 ? v0 >> (8 * k) : v1 >> (8 * (k - 8))) & 0xff);
     };
@@ -187,6 +183,18 @@ __device__ __forceinline__ uint64_t header_words(const uint8_t* __restrict__ pac
   *st_out = st;
   return words;
 }
+__device__ __forceinline__ uint64_t header_words(const uint8_t* __restrict__ packed,
+                                                 const uint64_t* __restrict__ in_off, uint64_t m,
+                                                 uint64_t limit, int32_t* st_out) {
+  const uint64_t p = in_off[m];
+  const uint64_t end = in_off[m + 1];
+  uint64_t v0 = 0, v1 = 0;
+  if (end - p >= 16) {
+    __builtin_memcpy(&v0, packed + p, 8);
+    __builtin_memcpy(&v1, packed + p + 8, 8);
+  }
+  return header_words_v(packed, p, end, v0, v1, limit, st_out);
+}
 
 // One launch for the headers and their word offsets: blocks [0, nsb) each take kHdrBlock
 // messages (4 per thread), decode their headers and scan the flat sizes into word_off with a
@@ -197,12 +205,14 @@ __device__ __forceinline__ uint64_t header_words(const uint8_t* __restrict__ pac
 // Headers per thread: 1 for batches of up to kHdrSmall messages (each thread's two dependent
 // loads are the launch's latency: C2 10.1 -> 5.9 us), 4 above (fewer look-back blocks: C3 66.6 ->
 // 56.3 us).
+// (One block of 16 headers per thread for batches of up to 4096, no look-back: C2's header
+// launch 5.9 -> 34.7 us -- one CU decoding every header -- so not that.)
 constexpr uint64_t kHdrSmall = 1ull << 16;
 __host__ __device__ constexpr int hdr_per(uint64_t n) { return n <= kHdrSmall ? 1 : 4; }
 template <int kHdrPerThread>
 __global__ __launch_bounds__(256) void header_kernel(
-    const uint8_t* __restrict__ packed, const uint64_t* __restrict__ in_off, uint64_t n,
-    uint64_t limit, uint64_t* __restrict__ word_off, int32_t* __restrict__ hdr_status,
+    const uint8_t* __restrict__ packed, uint64_t P, const uint64_t* __restrict__ in_off,
+    uint64_t n, uint64_t limit, uint64_t* __restrict__ word_off, int32_t* __restrict__ hdr_status,
     int32_t* __restrict__ status, uint64_t* desc, uint32_t* err, TileFirstJob tf,
     uint32_t nsb) {
   if (run_tile_first(tf, nsb)) return;
@@ -215,13 +225,35 @@ __global__ __launch_bounds__(256) void header_kernel(
   const uint64_t m0 = b * kHdrBlock + (uint64_t)kHdrPerThread * threadIdx.x;
   uint64_t w[kHdrPerThread];
   uint64_t sum = 0;
+  // every message's offsets, then every message's first 16 bytes, all in flight before any is
+  // used (clamped indices and addresses, no branch: a load under a branch is waited for at the
+  // join) -- two round trips per thread whatever kHdrPerThread is (C5's header launch 218 -> 206
+  // us)
+  uint64_t hp[kHdrPerThread], he[kHdrPerThread], v0[kHdrPerThread], v1[kHdrPerThread];
+#pragma unroll
+  for (int k = 0; k < kHdrPerThread; k++) {
+    const uint64_t m = m0 + k < n ? m0 + k : n - 1;
+    hp[k] = in_off[m];
+    he[k] = in_off[m + 1];
+  }
+  const bool wide = P >= 16;  // (uniform: else no message has 16 bytes)
+#pragma unroll
+  for (int k = 0; k < kHdrPerThread; k++) {
+    const uint64_t q = (wide && he[k] - hp[k] >= 16) ? hp[k] : 0;
+    v0[k] = 0;
+    v1[k] = 0;
+    if (wide) {
+      __builtin_memcpy(&v0[k], packed + q, 8);
+      __builtin_memcpy(&v1[k], packed + q + 8, 8);
+    }
+  }
 #pragma unroll
   for (int k = 0; k < kHdrPerThread; k++) {
     const uint64_t m = m0 + k;
     w[k] = 0;
     if (m < n) {
       int32_t st;
-      w[k] = header_words(packed, in_off, m, limit, &st);
+      w[k] = header_words_v(packed, hp[k], he[k], v0[k], v1[k], limit, &st);
       hdr_status[m] = st;
       status[m] = st;
     }
@@ -2162,18 +2194,22 @@ uint64_t header_scan_blocks(uint64_t n) {
   return (n + blk - 1) / blk;
 }
 
-hipError_t launch_unpack_header(const uint8_t* packed, const uint64_t* in_off, uint64_t n,
-                                uint64_t limit, uint64_t* word_off, int32_t* hdr_status,
-                                int32_t* status, uint64_t* desc, uint32_t* err,
-                                const TileFirstJob& tf, hipStream_t stream) {
+hipError_t launch_unpack_header(const uint8_t* packed, uint64_t P, const uint64_t* in_off,
+                                uint64_t n, uint64_t limit, uint64_t* word_off,
+                                int32_t* hdr_status, int32_t* status, uint64_t* desc,
+                                uint32_t* err, const TileFirstJob& tf, hipStream_t stream) {
   const unsigned nb = (unsigned)header_scan_blocks(n);
   if (nb + tile_first_blocks(tf) == 0) return hipSuccess;
-  if (hdr_per(n) == 1)
-    hipLaunchKernelGGL(header_kernel<1>, dim3(nb + tile_first_blocks(tf)), dim3(256), 0, stream,
-                       packed, in_off, n, limit, word_off, hdr_status, status, desc, err, tf, nb);
-  else
-    hipLaunchKernelGGL(header_kernel<4>, dim3(nb + tile_first_blocks(tf)), dim3(256), 0, stream,
-                       packed, in_off, n, limit, word_off, hdr_status, status, desc, err, tf, nb);
+  const dim3 g(nb + tile_first_blocks(tf)), blk(256);
+  switch (hdr_per(n)) {
+    case 1:
+      hipLaunchKernelGGL(header_kernel<1>, g, blk, 0, stream, packed, P, in_off, n, limit,
+                         word_off, hdr_status, status, desc, err, tf, nb);
+      break;
+    default:
+      hipLaunchKernelGGL(header_kernel<4>, g, blk, 0, stream, packed, P, in_off, n, limit,
+                         word_off, hdr_status, status, desc, err, tf, nb);
+  }
   return hipGetLastError();
 }
 
