@@ -812,6 +812,12 @@ __global__ __launch_bounds__(256) void pack_place_kernel(PackTileArgs a) {
   __shared__ uint32_t s_list[kPlaceGroup];  // group-relative indices of the tiles in the arena
   __shared__ uint32_t s_narena;
   __shared__ uint64_t s_pos[2];  // the group's requested positions: [s_pos[0], s_pos[1])
+  // the count-byte handoffs around the group's tiles, read with the group's descriptors: thole
+  // of tiles T0 - 1 .. T0 + 63 (s_hole[j + 1]: tile T0 + j), tpatch of T0 .. T0 + 64, and the
+  // byte count of tile T0 - 1 (a tile's copy then waits on its source bytes alone)
+  __shared__ uint32_t s_hole[kPlaceGroup + 1];
+  __shared__ uint32_t s_patch[kPlaceGroup + 1];
+  __shared__ uint32_t s_nprev;
   const int tid = (int)threadIdx.x;
   const int l = lane_id();
   const int w = (int)uniform32(threadIdx.x >> 6);
@@ -823,6 +829,12 @@ __global__ __launch_bounds__(256) void pack_place_kernel(PackTileArgs a) {
     const uint64_t n = in ? a.tile_bytes[T] : 0ull;
     const uint64_t dT = in ? load_agent(a.desc + T) : 0ull;
     const uint64_t piece = in ? a.tpiece[T] : ~0ull;
+    const uint32_t th = in ? a.thole[T] : 0xffffffffu;
+    const uint32_t tp = in ? a.tpatch[T] : 0u;
+    const uint64_t T64 = T0 + kPlaceGroup;
+    const uint32_t th_m1 = (l == 0 && T0 > 0) ? a.thole[T0 - 1] : 0xffffffffu;
+    const uint32_t nb_m1 = (l == 0 && T0 > 0) ? (uint32_t)a.tile_bytes[T0 - 1] : 0u;
+    const uint32_t tp_64 = (l == kPlaceGroup - 1 && T64 < a.ntiles) ? a.tpatch[T64] : 0u;
     // the group's positions: from its first tile's first to the next group's first
     const bool pl = a.pos && l < 2;
     const uint64_t pT = T0 + (uint64_t)l * kPlaceGroup;
@@ -857,6 +869,15 @@ __global__ __launch_bounds__(256) void pack_place_kernel(PackTileArgs a) {
     if (arena) s_list[__popcll(am & ((1ull << l) - 1ull))] = (uint32_t)l;
     if (l == 0) s_narena = (uint32_t)__popcll(am);
     if (pl) s_pos[l] = pf;
+    if (l < kPlaceGroup) {
+      s_hole[l + 1] = th;
+      s_patch[l] = tp;
+    }
+    if (l == 0) {
+      s_hole[0] = th_m1;
+      s_nprev = nb_m1;
+    }
+    if (l == kPlaceGroup - 1) s_patch[kPlaceGroup] = tp_64;
     if (in && T + 1 == a.ntiles && a.total_out) *a.total_out = base + inc;
   }
   __syncthreads();
@@ -887,12 +908,13 @@ __global__ __launch_bounds__(256) void pack_place_kernel(PackTileArgs a) {
       // the previous tile's count byte that this tile finishes (the previous tile may have left
       // it out, having written its bytes itself)
       if (T > 0 && l == 0) {
-        const uint32_t ph = a.thole[T - 1], pp = a.tpatch[T];
-        if (ph != 0xffffffffu && pp) a.out[off - a.tile_bytes[T - 1] + ph] = (uint8_t)pp;
+        const uint32_t ph = s_hole[j], pp = s_patch[j];
+        const uint32_t nprev = j ? s_n[j - 1] : s_nprev;
+        if (ph != 0xffffffffu && pp) a.out[off - nprev + ph] = (uint8_t)pp;
       }
       // count byte patched by the next tile (position, value) -- wave-uniform
-      const uint32_t hole = T + 1 < a.ntiles ? a.thole[T] : 0xffffffffu;
-      const uint32_t pv = hole != 0xffffffffu ? a.tpatch[T + 1] : 0u;
+      const uint32_t hole = T + 1 < a.ntiles ? s_hole[j + 1] : 0xffffffffu;
+      const uint32_t pv = hole != 0xffffffffu ? s_patch[j + 1] : 0u;
       const uint8_t* const src = a.arena + s_piece[j];
       uint8_t* const o0 = a.out + off;
       const uint64_t A0 = (uint64_t)(uintptr_t)o0;
