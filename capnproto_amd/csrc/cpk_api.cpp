@@ -326,17 +326,15 @@ struct PackScratch {
   size_t total;
 };
 
-// Byte arena of a pack of N words: the packed bytes of the tiles whose offset is not known in time
-// wait there for the placement launch, each in a piece of exactly its size.  Half the unpacked
-// bytes (at least 8 MiB, at most the worst-case packed size or 8 GiB): a tile finding it full
-// waits for its offset instead.
-uint64_t pack_arena_bytes(uint64_t N, uint64_t ntiles) {
-  uint64_t cap = N * 4;
-  if (cap < (8ull << 20)) cap = 8ull << 20;
-  const uint64_t worst = N * 10 + 16 * ntiles;
-  if (cap > worst) cap = worst;
+// Byte arena of a pack of `ntiles` tiles: the packed bytes of the tiles whose offset is not known
+// in time wait there for the placement launch, each in a piece of exactly its size (rounded to 16
+// bytes).  Only a tile of at most kPackArenaTile packed bytes takes a piece, so ntiles pieces of
+// that size are all any batch can use (2 bytes per word; at most 8 GiB, past which a tile finding
+// it full waits for its offset instead).
+uint64_t pack_arena_bytes(uint64_t ntiles) {
+  uint64_t cap = ntiles * (uint64_t)cpk::kPackArenaTile;
   if (cap > (8ull << 30)) cap = 8ull << 30;
-  return (cap + 15) & ~15ull;
+  return cap;
 }
 
 // Pack scratch: the zeroed part (exit budgets polled by the next tile, the arena's fill counter,
@@ -356,7 +354,7 @@ PackScratch carve_pack(void* base, uint64_t N, uint64_t ntiles) {
   s.thole = c.take<uint32_t>(ntiles);
   s.tpatch = c.take<uint32_t>(ntiles);
   s.tpiece = c.take<uint64_t>(ntiles);
-  s.arena_cap = ntiles > 1 ? pack_arena_bytes(N, ntiles) : 0;
+  s.arena_cap = ntiles > 1 ? pack_arena_bytes(ntiles) : 0;
   s.arena = c.take<uint8_t>(s.arena_cap + 16);
   s.total = c.off;
   return s;
@@ -496,28 +494,51 @@ struct UnpackScratch {
   uint64_t* desc;
   uint32_t* x0p;
   uint64_t* desc2;
+  uint64_t* gdesc;
+  uint32_t* gate;
+  unsigned int* ticket;
   size_t zero_bytes;
   uint64_t* tile_first;
   uint64_t* tile_firstpos;
   int32_t* hdr_status;
+  uint64_t* tbits;
+  uint32_t* tegs;
+  uint64_t* texcl;
   size_t total;
 };
 
 // Unpack scratch: per message 4 B (header status), per 4 KiB tile 28 B (descriptor, chain-0
 // exit, first message and its start), and for a flat stream decode 8 B more (second-candidate
-// descriptor).  The tile descriptors and exits are zeroed (in the header / init launch).
-UnpackScratch carve_unpack(void* base, uint64_t ntiles, uint64_t n, bool flat = false) {
+// descriptor).  The split message decode adds per tile 524 B (chain 0's record-start bits, the
+// guessed entry, the words before the tile) and per 64-tile group 8 B (zeroed).  The tile
+// descriptors and exits are zeroed (in the header / init launch).
+UnpackScratch carve_unpack(void* base, uint64_t ntiles, uint64_t n, bool flat = false,
+                           bool split = false) {
   Carve c(base);
   UnpackScratch s;
   s.desc = c.take<uint64_t>(ntiles);
   s.x0p = c.take<uint32_t>(ntiles);
   s.desc2 = flat ? c.take<uint64_t>(ntiles) : nullptr;
+  s.gdesc = split ? c.take<uint64_t>(cpk::resolve_groups(ntiles)) : nullptr;
+  s.gate = split ? c.take<uint32_t>(4) : nullptr;
+  s.ticket = split ? (unsigned int*)(s.gate + 1) : nullptr;
   s.zero_bytes = c.off;
   s.tile_first = c.take<uint64_t>(ntiles);
   s.tile_firstpos = c.take<uint64_t>(ntiles);
   s.hdr_status = c.take<int32_t>(n);
+  s.tbits = split ? c.take<uint64_t>(ntiles * 64) : nullptr;
+  s.tegs = split ? c.take<uint32_t>(ntiles) : nullptr;
+  s.texcl = split ? c.take<uint64_t>(ntiles) : nullptr;
   s.total = c.off;
   return s;
+}
+
+// The split message decode (index, resolve, expand launches: cpk_unpack.hip) for message batches
+// of more than one tile, with CPK_UNPACK_SPLIT=1 (A/B; measured slower than the one-pass kernel,
+// DESIGN.md 3.2).
+bool unpack_split_enabled() {
+  static const bool v = getenv("CPK_UNPACK_SPLIT") && atoi(getenv("CPK_UNPACK_SPLIT")) != 0;
+  return v;
 }
 
 cpk_status unpack_common(cpk_ctx* ctx, uint32_t mode, const uint8_t* d_packed, uint64_t P,
@@ -535,10 +556,14 @@ cpk_status unpack_common(cpk_ctx* ctx, uint32_t mode, const uint8_t* d_packed, u
   const uint64_t ntiles = (P + B - 1) / B;
   // a flat stream decode (the stream split) carries second-candidate tile descriptors
   const bool flat = d_rec_pos != nullptr;
-  UnpackScratch probe = carve_unpack(nullptr, ntiles, n, flat);
+  // a message batch of several tiles decodes in three launches, no tile waiting on another (the
+  // stream readers' message ends, skips and the flat decode keep the one-pass kernel)
+  const bool split = mode == 0 && ntiles > 1 && !flat && !d_in_end && !store_free && d_words &&
+                     unpack_split_enabled();
+  UnpackScratch probe = carve_unpack(nullptr, ntiles, n, flat, split);
   cpk_status st = ensure(&ctx->scratch, &ctx->scratch_size, probe.total + 64);
   if (st != CPK_OK) return st;
-  UnpackScratch s = carve_unpack(ctx->scratch, ntiles, n, flat);
+  UnpackScratch s = carve_unpack(ctx->scratch, ntiles, n, flat, split);
   const uint64_t* word_off = d_word_off_in;
   hipError_t e = hipSuccess;
   cpk::TileFirstJob tf;  // each tile's first message, in the same launch as the headers
@@ -607,7 +632,42 @@ cpk_status unpack_common(cpk_ctx* ctx, uint32_t mode, const uint8_t* d_packed, u
   a.hdr_limit = limit;
   a.hdr_word_off = d_word_off_out;
   a.hdr_status_out = s.hdr_status;
+  a.phase = 0;
+  a.tbits = s.tbits;
+  a.tegs = s.tegs;
+  a.texcl = s.texcl;
+  a.gate = s.gate;
+  a.ticket = nullptr;
   TimedLaunch tl(ctx, 1, stream);
+  if (split) {
+    cpk::ResolveArgs r;
+    r.packed = d_packed;
+    r.nbytes = P;
+    r.ntiles = ntiles;
+    r.desc = s.desc;
+    r.x0p = s.x0p;
+    r.tbits = s.tbits;
+    r.tile_firstpos = s.tile_firstpos;
+    r.gdesc = s.gdesc;
+    r.ticket = s.ticket;
+    r.texcl = s.texcl;
+    r.gate = s.gate;
+    r.err = ctx->err;
+    TimedLaunch tk(ctx, 2, stream);
+    a.phase = 1;
+    e = cpk::launch_unpack_stage(cpk::kUnpackIndex, a, stream);
+    if (e == hipSuccess) e = cpk::launch_unpack_resolve(r, stream);
+    a.phase = 2;
+    a.hdr_nblocks = 0;  // (cleared by the index launch)
+    if (e == hipSuccess) e = cpk::launch_unpack_stage(cpk::kUnpackExpand, a, stream);
+    tk.done();
+    if (e != hipSuccess) {
+      (void)cpk::launch_fill(ctx->hdr_desc, 8 * cpk::header_scan_blocks(n), 0, stream);
+      return CPK_ERR_HIP;
+    }
+    tl.done();
+    return CPK_OK;
+  }
   for (int stage = cpk::kUnpackTiles; stage <= cpk::kUnpackTiles; stage++) {
     TimedLaunch tk(ctx, 2 + stage, stream);
     e = cpk::launch_unpack_stage(stage, a, stream);
@@ -722,7 +782,6 @@ cpk_status cpk_copy_ranges(cpk_ctx* ctx, const uint8_t* d_src, const uint64_t* d
   if (!ctx || (n && (!d_src || !d_src_off || !d_dst_off || !d_len || !d_dst)))
     return CPK_ERR_INVALID_ARGUMENT;
   if (hipSetDevice(ctx->device) != hipSuccess) return CPK_ERR_HIP;
-  if (n >= (1ull << 33)) return CPK_ERR_INVALID_ARGUMENT;
   return hip_status(cpk::launch_copy_ranges(d_src, d_src_off, d_dst_off, d_len, n, d_dst,
                                             (hipStream_t)stream));
 }

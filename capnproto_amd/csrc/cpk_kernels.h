@@ -9,6 +9,9 @@ namespace cpk {
 
 constexpr uint64_t kPackTileWords = 2048;       // words per workgroup tile (cpk_pack.hip)
 constexpr uint64_t kPackScratchBytes = 10 * kPackTileWords;  // a tile's packed bytes, worst case
+// pack tiles of at most this many packed bytes may leave them in the byte arena (cpk_pack.hip),
+// so the arena never needs more than this per tile
+constexpr uint32_t kPackArenaTile = 4096;
 constexpr uint64_t kUnpackTileBytes = 4096;     // packed bytes per unpack tile (>= 2050)
 
 struct PackTileArgs {
@@ -118,8 +121,38 @@ struct UnpackArgs {
   uint64_t* hdr_word_off;
   int32_t* hdr_status_out;
   uint32_t prio;                // batches of very long messages: raised wave priority (cpk_unpack.hip)
+  // The split message decode (cpk_unpack.hip, "Split decode"): phase 0 one pass (chain, look-back
+  // and expansion per tile); 1 the index launch (chain 0 per tile, published with its record-start
+  // bits); 2 the expansion launch (after the resolve launch).
+  uint32_t phase;
+  uint64_t* tbits;              // ntiles * 64: each tile's base-chain record starts (1 bit per byte)
+  uint32_t* tegs;               // ntiles: each tile's guessed entry
+  const uint64_t* texcl;        // ntiles: words of the tile's first message before the tile
+  const uint32_t* gate;         // non-zero: the resolve launch could not place every tile
+  unsigned int* ticket;         // tile tickets of a launch whose tiles wait (zeroed), else NULL
 };
 constexpr uint64_t kUnpackFuseMsgs = 256;
+
+// The resolve launch of the split message decode: every tile's words before it in its first
+// message, from the index launch's descriptors (a segmented scan over 64-tile groups; tiles whose
+// guessed entry was wrong re-traced from the true one).
+struct ResolveArgs {
+  const uint8_t* packed;
+  uint64_t nbytes;
+  uint64_t ntiles;
+  const uint64_t* desc;         // the index launch's tile descriptors
+  const uint32_t* x0p;          // ... and base-chain exits
+  const uint64_t* tbits;        // ... and record-start bits
+  const uint64_t* tile_firstpos;
+  uint64_t* gdesc;              // per 64-tile group look-back descriptors (zeroed)
+  unsigned int* ticket;         // group tickets (zeroed)
+  uint64_t* texcl;
+  uint32_t* gate;               // set when a tile's true exit is not its base-chain exit (zeroed)
+  uint32_t* err;
+};
+constexpr uint64_t kResolveGroup = 64;
+__host__ __device__ inline uint64_t resolve_groups(uint64_t ntiles) { return (ntiles + kResolveGroup - 1) / kResolveGroup; }
+hipError_t launch_unpack_resolve(const ResolveArgs& r, hipStream_t stream);
 
 // The stream split's record-head map holds (gen << kRecGenShift) | packed byte for a record head,
 // anything else elsewhere: an entry counts only with the call's generation, so the map is filled
@@ -129,8 +162,11 @@ constexpr int kRecGenShift = 40;
 constexpr uint64_t kRecPosMask = (1ull << kRecGenShift) - 1;
 constexpr uint64_t kRecGenMax = 1ull << 23;
 
-// Unpack stages (launch_unpack_stage), in launch order: the tile kernel is the only one.
+// Unpack stages (launch_unpack_stage): the one-pass tile kernel, or the split decode's index and
+// expansion launches (the resolve launch between them is launch_unpack_resolve).
 constexpr int kUnpackTiles = 0;
+constexpr int kUnpackIndex = 1;
+constexpr int kUnpackExpand = 2;
 
 uint32_t debug_skip();
 

@@ -50,7 +50,7 @@ constexpr uint32_t kCap = 9 * kTW;             // staging window (bytes)
 constexpr uint32_t kPadF = 16;                 // front pad: records straddling the window start
 constexpr int kSlotDw = (kPadF + kCap + 64) / 4;
 constexpr int kTrashDw = 64 + 4;               // lane l: dwords l .. l + 3
-constexpr uint32_t kArenaTile = 4096;          // tiles of at most this many bytes use the arena
+constexpr uint32_t kArenaTile = kPackArenaTile;  // tiles of at most this many bytes use the arena
 constexpr uint64_t kScr = kPackScratchBytes;    // scratch slot per tile (<= 10 B per word)
 static_assert(kScr >= 10 * kTW && kScr % 16 == 0, "a tile's bytes fit its scratch slot");
 

@@ -725,22 +725,14 @@ __global__ __launch_bounds__(256) void gather_kernel(const uint64_t* __restrict_
 }
 
 // ---- message placement for the batch exchange ------------------------------------------------
-// n byte ranges src[src_off[i], +len[i]) -> dst[dst_off[i], ...): one wave per range, the body
-// as 16-byte stores aligned on the destination, each from five aligned source dwords shifted by
-// v_alignbyte (the head and tail bytes one per lane).  Used by the multi-GPU gather to put
-// round-robin shards' messages at their global positions (capnproto_amd/shard.py).
-__global__ __launch_bounds__(256) void copy_ranges_kernel(const uint8_t* __restrict__ src,
-                                                          const uint64_t* __restrict__ src_off,
-                                                          const uint64_t* __restrict__ dst_off,
-                                                          const uint64_t* __restrict__ len,
-                                                          uint64_t n, uint8_t* __restrict__ dst) {
-  const uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (i >= n) return;
-  const uint32_t l = threadIdx.x & 63u;
-  const uint64_t nb = len[i];
-  if (nb == 0) return;
-  const uint8_t* const s0 = src + src_off[i];
-  uint8_t* const o0 = dst + dst_off[i];
+// n byte ranges src[src_off[i], +len[i]) -> dst[dst_off[i], ...): one wave per range (the waves
+// of a capped grid stride over the ranges, so any n launches), the body as 16-byte stores aligned
+// on the destination, each from five aligned source dwords shifted by v_alignbyte (the head and
+// tail bytes one per lane).  Used by the multi-GPU gather to put round-robin shards' messages at
+// their global positions (capnproto_amd/shard.py).
+constexpr uint64_t kCopyRangesMaxBlocks = 1u << 16;
+__device__ __forceinline__ void copy_range(const uint8_t* __restrict__ s0, uint8_t* __restrict__ o0,
+                                           uint64_t nb, uint32_t l) {
   const uint64_t A0 = (uint64_t)(uintptr_t)o0, A1 = A0 + nb;
   const uint64_t al = (A0 + 15) & ~15ull;
   const uint64_t head = (al < A1 ? al : A1) - A0;  // bytes before 16-byte alignment
@@ -768,14 +760,27 @@ __global__ __launch_bounds__(256) void copy_ranges_kernel(const uint8_t* __restr
   if (body + l < nb) o0[body + l] = s0[body + l];
 }
 
+__global__ __launch_bounds__(256) void copy_ranges_kernel(const uint8_t* __restrict__ src,
+                                                          const uint64_t* __restrict__ src_off,
+                                                          const uint64_t* __restrict__ dst_off,
+                                                          const uint64_t* __restrict__ len,
+                                                          uint64_t n, uint8_t* __restrict__ dst) {
+  const uint32_t l = threadIdx.x & 63u;
+  const uint64_t stride = (uint64_t)gridDim.x * 4;
+  for (uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < n; i += stride) {
+    const uint64_t nb = len[i];
+    if (nb) copy_range(src + src_off[i], dst + dst_off[i], nb, l);
+  }
+}
+
 }  // namespace
 
 hipError_t launch_copy_ranges(const uint8_t* src, const uint64_t* src_off,
                               const uint64_t* dst_off, const uint64_t* len, uint64_t n,
                               uint8_t* dst, hipStream_t stream) {
   if (n == 0) return hipSuccess;
-  copy_ranges_kernel<<<(unsigned)((n + 3) / 4), 256, 0, stream>>>(src, src_off, dst_off, len, n,
-                                                                   dst);
+  const uint64_t blocks = (n + 3) / 4 < kCopyRangesMaxBlocks ? (n + 3) / 4 : kCopyRangesMaxBlocks;
+  copy_ranges_kernel<<<(unsigned)blocks, 256, 0, stream>>>(src, src_off, dst_off, len, n, dst);
   return hipGetLastError();
 }
 

@@ -451,6 +451,24 @@ __device__ __forceinline__ uint64_t ff_heads(const uint8_t* d, int s) {
   return m;
 }
 
+// Positions j of the lane's sub-tile [s, s + 64) whose byte is 0x00 or 0xff: the run records'
+// tags among any record starts there (the split decode's expansion launch rebuilds the run mask
+// of chain 0 from these instead of walking the chain again).
+__device__ __forceinline__ uint64_t run_bytes(const uint8_t* d, int s) {
+  const uint32_t* const w = (const uint32_t*)(d + s);
+  uint64_t m = 0;
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    const uint32_t x = w[k], y = ~x;
+    const uint32_t z = ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x) & 0x80808080u;
+    const uint32_t f = ~(((y & 0x7f7f7f7fu) + 0x7f7f7f7fu) | y) & 0x80808080u;
+    // bits 7, 15, 23, 31 -> 0..3 (one multiply gathers them into bits 21-24)
+    const uint32_t nib = ((((z | f) >> 7) * 0x204081u) >> 21) & 15u;
+    m |= (uint64_t)nib << (4 * k);
+  }
+  return m;
+}
+
 struct Rec {
   uint32_t tag;
   int hb;       // tag + data bytes
@@ -1776,14 +1794,133 @@ __device__ __forceinline__ void run_tail(const UnpackArgs& a, uint64_t A, const 
   }
 }
 
+// Expansion of a tile in the middle of a message: no message start in the tile, and neither the
+// words of its records nor their bytes can reach the message's end (most tiles of long
+// messages).  Then no record can end or break its message, and the record batches need none of
+// expand_lean's per-record message logic: one wave-uniform word pointer, one store per record, the
+// runs' other words by the wave.  (Same stores as expand_lean for such a tile.)
+__device__ __forceinline__ void expand_simple(const UnpackArgs& a, const uint8_t* d, uint64_t* aux,
+                                              const uint64_t* dep_tab, uint64_t tm, uint64_t* wp) {
+  const int l = lane_id();
+  __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): as expand_lean
+  aux[l] = tm;
+  lane_handoff();
+  const uint16_t* const a16 = (const uint16_t*)aux;
+  const uint32_t tq01 = a16[l] | ((uint32_t)a16[64 + l] << 16);
+  const uint32_t tq23 = a16[128 + l] | ((uint32_t)a16[192 + l] << 16);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (the lists overwrite aux)
+  uint16_t* const list = (uint16_t*)aux;
+  const uint32_t* const d32 = (const uint32_t*)d;
+  constexpr uint32_t kStaged = (uint32_t)(kB + kPad);
+  for (int h = 0; h < 4; h++) {
+    const uint32_t hs = 16u * ((uint32_t)h & 1u);
+    uint32_t bits = ((h < 2 ? tq01 : tq23) >> hs) & 0xffffu;
+    const uint32_t c = __popc(bits);
+    const uint32_t Rin = wave_incl_sum32(c);
+    const uint32_t nh = readlane32(Rin, 63);
+    const uint32_t pbase = 1024u * (uint32_t)h + 16u * (uint32_t)l;
+    uint16_t* lp = list + (Rin - c);
+    while (bits) {
+      const uint32_t b = (uint32_t)__builtin_ctz(bits);
+      bits &= bits - 1;
+      *lp++ = (uint16_t)(pbase + b);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    for (uint32_t b0 = 0; b0 < nh; b0 += 64) {
+      const uint32_t rr = b0 + l;
+      const bool act = rr < nh;
+      const uint32_t p = list[act ? rr : nh - 1];
+      const uint32_t q = p >> 2, sh = p & 3u;
+      const uint32_t q0 = d32[q], q1 = d32[q + 1], q2 = d32[q + 2], q3 = d32[q + 3];
+      const uint32_t b0w = __builtin_amdgcn_alignbyte(q1, q0, sh);  // bytes p .. p+3
+      const uint32_t b1w = __builtin_amdgcn_alignbyte(q2, q1, sh);  // p+4 .. p+7
+      const uint32_t b2w = __builtin_amdgcn_alignbyte(q3, q2, sh);  // p+8 .. p+11
+      const uint32_t tag = b0w & 0xffu;
+      const uint64_t sel = dep_tab[tag];
+      const uint32_t dlo = __builtin_amdgcn_alignbyte(b1w, b0w, 1);
+      const uint32_t dhi = __builtin_amdgcn_alignbyte(b2w, b1w, 1);
+      const bool z = tag == 0, f = tag == 0xffu;
+      uint32_t cnt = z ? ((b0w >> 8) & 0xffu) : 0u;
+      cnt = f ? ((b2w >> 8) & 0xffu) : cnt;
+      const uint64_t runs = ballot(act && cnt != 0);
+      uint32_t o = (uint32_t)l, btot = (uint32_t)__popcll(ballot(act));
+      if (runs) {
+        const uint32_t w = act ? 1u + cnt : 0u;
+        const uint32_t inc = wave_incl_sum32(w);
+        o = inc - w;
+        btot = readlane32(inc, 63);
+      }
+      const uint32_t wlo = __builtin_amdgcn_perm(dhi, dlo, (uint32_t)sel);
+      const uint32_t whi = __builtin_amdgcn_perm(dhi, dlo, (uint32_t)(sel >> 32));
+      if (act) wp[o] = ((uint64_t)whi << 32) | wlo;
+      if (runs) {
+        // a run's first word with its record (a raw run's from the staged bytes when they hold
+        // it), the rest by the whole wave -- as expand_lean
+        const uint32_t rb = p + 10u;  // a raw run's first word: bytes p + 10 .. p + 17
+        const bool inl = !f || rb + 12u <= kStaged;
+        uint64_t rw = 0;
+        if (ballot(f && cnt != 0)) {
+          const uint32_t rq = rb >> 2, rs = rb & 3u;
+          const uint32_t rqc = rq < kStaged / 4 - 2 ? rq : kStaged / 4 - 3;
+          const uint32_t r0 = d32[rqc], r1 = d32[rqc + 1], r2 = d32[rqc + 2];
+          rw = f ? (((uint64_t)__builtin_amdgcn_alignbyte(r2, r1, rs) << 32) |
+                    __builtin_amdgcn_alignbyte(r1, r0, rs))
+                 : 0ull;
+        }
+        if (act && cnt != 0 && inl) wp[o + 1] = rw;
+        uint64_t lm = ballot(act && (cnt > 1u || (cnt != 0 && !inl)));
+        while (lm) {
+          const int j = lowest_bit(lm);
+          lm &= lm - 1;
+          const uint32_t k0 = readlane32(inl ? 1u : 0u, j);
+          const uint32_t nj = readlane32(cnt, j);
+          uint64_t* const dst = wp + readlane32(o, j) + 1;
+          const uint32_t sj = readlane32(rb, j);
+          if (!readlane32(f ? 1u : 0u, j)) {
+            for (uint32_t k = k0 + l; k < nj; k += 64) dst[k] = 0;
+          } else {
+            // (a raw run leaving the staged bytes: its words ending at most kRunSplit bytes into
+            // the next tile; the next tile writes the rest, run_tail)
+            const uint32_t kin = sj + 8u * nj + 4u <= kStaged
+                                     ? nj
+                                     : (sj + 12u <= kStaged ? (kStaged - 4u - sj) / 8u : 0u);
+            const uint32_t ke = nj < kin ? nj : kin;
+            for (uint32_t k = k0 + l; k < ke; k += 64) {
+              const uint32_t ob = sj + 8u * k, qq = ob >> 2, s3 = ob & 3u;
+              const uint32_t x0 = d32[qq], x1 = d32[qq + 1], x2 = d32[qq + 2];
+              dst[k] = ((uint64_t)__builtin_amdgcn_alignbyte(x2, x1, s3) << 32) |
+                       __builtin_amdgcn_alignbyte(x1, x0, s3);
+            }
+          }
+        }
+      }
+      wp += btot;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+}
+
 // Expansion of a tile's records given its true record-start masks (lane = sub-tile) and excl,
 // the words of the tile's first message before the tile: the lean path when the tile's window
 // allows it, else the general one.
 __device__ __forceinline__ void expand_records(const UnpackArgs& a, uint64_t A, const uint8_t* d,
                                                uint64_t* aux, const uint64_t* dep_tab, uint64_t tm,
                                                uint64_t excl, MsgWin& win, uint64_t mfirst,
-                                               uint64_t mlast, uint64_t msw) {
+                                               uint64_t mlast, uint64_t msw,
+                                               uint64_t tile_words = ~0ull) {
   const int l = lane_id();
+  // a tile in the middle of one accepted message (no start in it; its words and bytes short of
+  // the message's end; the message fits the output)
+  if (a.mode == 0 && a.words && a.word_off && !a.rec_pos && tile_words != ~0ull &&
+      ballot(msw != 0) == 0) {
+    const uint64_t cbase = readlane64(win.base, 0), ctot = readlane64(win.total, 0);
+    const uint64_t cend = readlane64(win.end, 0);
+    if (readlane32(win.ok, 0) && cbase + ctot <= a.words_capacity && excl + tile_words < ctot &&
+        A + (uint64_t)kB + 2050u < cend) {
+      expand_simple(a, d, aux, dep_tab, tm, a.words + cbase + excl);
+      return;
+    }
+  }
   bool fast = a.mode == 0 && mlast - (mfirst - 1) <= 63 && a.word_off && a.words;
   if (fast) {
     const int64_t m = win.mw + l;
@@ -1815,9 +1952,13 @@ __device__ __forceinline__ void expand_records(const UnpackArgs& a, uint64_t A, 
 #endif
 // FLAT: the flat stream decode's second-candidate descriptors and look-back are compiled in (a
 // variant of its own: their registers cost the other variant spills).
-template <bool FLAT>
+// PHASE (the split message decode, "Split decode" below): 0 one pass; 1 the index launch (stage,
+// chain 0, descriptors and record-start bits; no look-back, no expansion); 2 the expansion launch
+// (chain 0 from the index launch's bits, the tile's prefix from the resolve launch).
+template <bool FLAT, int PHASE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CPK_UNPACK_WPE))) void
 unpack_tiles_kernel(UnpackArgs a) {
+  static_assert(!FLAT || PHASE == 0, "the flat stream decode is one pass");
   __shared__ __attribute__((aligned(16))) uint8_t lds_data[4][kPre + kB + kPad];
   // per wave 1 KiB: message starts while they are found, then chain 0 and the walked starts
   // while the entry's chain is traced, then the record list of a quarter tile
@@ -1825,8 +1966,8 @@ unpack_tiles_kernel(UnpackArgs a) {
   __shared__ uint64_t dep_tab[256];
   const int l = lane_id();
   const int wv = (int)uniform32(threadIdx.x >> 6);  // wave-uniform (keeps tile math scalar)
-  dep_tab[threadIdx.x] = make_dep(threadIdx.x);
-  if (a.hdr_fuse) {
+  if (PHASE != 1) dep_tab[threadIdx.x] = make_dep(threadIdx.x);
+  if (PHASE == 0 && a.hdr_fuse) {
     // a single-tile batch of few messages: the header launch's work first, one message per
     // thread (serialize.c++:202-242 via header_words), the word offsets by one block scan
     __shared__ uint64_t s_hw[4];
@@ -1857,11 +1998,15 @@ unpack_tiles_kernel(UnpackArgs a) {
   // batches of very long messages (whose look-backs reach back to the previous occupancy round):
   // the phases later tiles wait on (chain 0, the entry, the descriptors) ahead of other waves'
   // expansions in the SIMD's issue arbitration (C4 unpack_tiles 4.51 -> 4.21 ms; no gain on C2)
-  if (a.prio) __builtin_amdgcn_s_setprio(2);
+  if (PHASE == 0 && a.prio) __builtin_amdgcn_s_setprio(2);
   CPK_DIAG_ONLY(uint64_t ck[7]; uint64_t wk[7]; uint64_t wflat = 0; ck[0] = clock64(); wk[0] = wall_clock64());
   // the header launch is done: its scan descriptors go back to zero for the next call
-  for (uint64_t i = t + a.ntiles * (uint64_t)l; i < a.hdr_nblocks; i += 64 * a.ntiles)
-    a.hdr_desc[i] = 0;
+  if (PHASE != 2)
+    for (uint64_t i = t + a.ntiles * (uint64_t)l; i < a.hdr_nblocks; i += 64 * a.ntiles)
+      a.hdr_desc[i] = 0;
+  // the expansion launch of a split decode whose resolve launch could not place every tile runs the
+  // one-pass look-back instead (wave-uniform)
+  const bool gated = PHASE == 2 && uniform32(*(const volatile uint32_t*)a.gate) != 0;
   uint8_t* const d = lds_data[wv] + kPre;
   uint64_t* const aux = lds_aux[wv];
   const uint64_t P = a.nbytes;
@@ -1882,8 +2027,22 @@ unpack_tiles_kernel(UnpackArgs a) {
     return;
   }
 
+  // first message start (the batch end counts), tile-relative; kB if none
+  const uint64_t msl = ballot(st.msw != 0);
+  const int fl = lowest_bit(msl);
+  const uint32_t fms = msl ? (uint32_t)(64 * fl + lowest_bit(readlane64(st.msw, fl))) : (uint32_t)kB;
+  uint64_t runm = 0, tm0 = 0;
+  uint32_t Eg = 0, x0 = 0;
+  bool settled = true;
+  int q0 = 0;  // where the tile's base chain starts
+  if constexpr (PHASE == 2) {
+    // chain 0 as the index launch left it (its run records are rebuilt only where needed)
+    tm0 = a.tbits[t * 64 + l];
+    Eg = t > 0 ? uniform32(a.tegs[t]) : 0u;
+    x0 = uniform32(a.x0p[t]) & 0x7fffffffu;
+  } else {
   // ---- chain 0 (entered at the tile's first byte): speculative walks, then the lane fixed point
-  uint64_t chain = 0, runm = 0;
+  uint64_t chain = 0;
   int sx = kDead;
   // Each lane's speculative chain starts CPK_PREWALK bytes before its sub-tile (at the last
   // message start there, if any) and walks unmarked up to it: chains synchronise within a few
@@ -1894,10 +2053,6 @@ unpack_tiles_kernel(UnpackArgs a) {
   // the start of the tile's base chain (the flat stream decode keeps chain 0, from byte 0).
   const bool guess = !FLAT && t > 0;
   int e0 = st.s;
-  // first message start (the batch end counts), tile-relative; kB if none
-  const uint64_t msl = ballot(st.msw != 0);
-  const int fl = lowest_bit(msl);
-  const uint32_t fms = msl ? (uint32_t)(64 * fl + lowest_bit(readlane64(st.msw, fl))) : (uint32_t)kB;
 #if CPK_PREWALK > 0
   {
     uint64_t pm = shfl64(st.msw, l > 0 ? l - 1 : 0);
@@ -1918,7 +2073,7 @@ unpack_tiles_kernel(UnpackArgs a) {
     }
   }
 #endif
-  const uint32_t Eg = guess ? (uint32_t)readlane32((uint32_t)e0, 0) : 0u;
+  Eg = guess ? (uint32_t)readlane32((uint32_t)e0, 0) : 0u;
 #ifdef CPK_DIAG
   int dn = 0, dit[3] = {0, 0, 0};
   if (e0 < st.pend && !(a.debug_skip & 4)) sx = walk(d, st, e0, 0, &chain, &runm, &dn);
@@ -1931,12 +2086,10 @@ unpack_tiles_kernel(UnpackArgs a) {
 #endif
   if (e0 >= st.pend) sx = kDead;
   int e = e0;
-  uint64_t tm0 = 0;
   int out = st.end;
-  const bool settled =
-      (a.debug_skip & 4) ? true : settle(d, st, chain, sx, (int)Eg, e, tm0, out, runm, diag_it);
+  settled = (a.debug_skip & 4) ? true : settle(d, st, chain, sx, (int)Eg, e, tm0, out, runm, diag_it);
   CPK_DIAG_ONLY(diag_add(5, dit[0]));
-  uint32_t x0 = readlane32((uint32_t)out, 63);
+  x0 = readlane32((uint32_t)out, 63);
   // Flat streams (stream split): inside long raw stretches (text) the chain from the tile's first
   // byte parses raw bytes as records and rarely finds the true chain within the tile, so its exit
   // -- the next tile's optimistic entry -- is wrong tile after tile and the entries resolve one
@@ -1944,8 +2097,7 @@ unpack_tiles_kernel(UnpackArgs a) {
   // that chain is a better guess: when the chain through it never meets chain 0, it stands in for
   // chain 0 (any chain of the tile serves as the base the entry's chain is traced onto; its exit
   // is only ever a guess the look-back checks).
-  int q0 = 0;  // where the tile's base chain starts
-  if (a.rec_pos && st.no_starts && t > 0 && settled && !(a.debug_skip & 4)) {
+  if (FLAT && a.rec_pos && st.no_starts && t > 0 && settled && !(a.debug_skip & 4)) {
     const uint64_t ffm = ff_heads(d, st.s) & ~tm0;
     const uint64_t fl = ballot(ffm != 0);
     if (fl) {
@@ -1964,6 +2116,12 @@ unpack_tiles_kernel(UnpackArgs a) {
     }
   }
   if (l == 0) store_agent32(a.x0p + t, 0x80000000u | x0);
+  if constexpr (PHASE == 1) {
+    // the expansion launch's chain 0 (coalesced: 512 bytes per tile)
+    a.tbits[t * 64 + l] = tm0;
+    if (l == 0) a.tegs[t] = Eg;
+  }
+  }
   CPK_DIAG_ONLY(ck[2] = ck[3] = ck[4] = ck[5] = clock64(); wk[2] = wk[3] = wk[4] = wk[5] = wall_clock64());
   if (a.debug_skip & 128) return;  // diagnostic: + chain-0 walks and settle
   if (!settled) {
@@ -1978,7 +2136,9 @@ unpack_tiles_kernel(UnpackArgs a) {
   const uint64_t hm = ballot(lastms >= 0);
   const bool has_start = hm != 0;
   CPK_DIAG_ONLY(diag_add(11, has_start));
-  if (has_start) {
+  // (the expansion launch rebuilds chain 0's run records only where words are counted again)
+  if (gated) runm = run_bytes(d, st.s);
+  if (has_start && PHASE != 2) {
     const int lm = highest_bit(hm);
     const uint64_t from = l > lm ? ~0ull : (l == lm ? ~mask_lt(lastms) : 0ull);
     const uint32_t wl = mask_words(d, st.s, tm0 & from, runm);
@@ -1989,18 +2149,20 @@ unpack_tiles_kernel(UnpackArgs a) {
   // ---- the tile's entry and the words before it ------------------------------------------
   uint64_t tm = tm0, excl = 0;
   uint32_t Ein = 0;  // the tile's true entry
+  uint64_t tile_words = ~0ull;  // words of the tile's records (a tile without a message start)
   if (t == 0 || fms == 0) {
-    if (!has_start) {  // (tile 0 without a message start: bytes before the first message)
+    if (!has_start && PHASE != 2) {  // (tile 0 without a message start: bytes before the first message)
       const uint64_t w = readlane32(wave_incl_sum32(mask_words(d, st.s, tm0, runm)), 63);
       if (l == 0) store_agent(a.desc + t, make_desc(kDescIncl, x0, x0, w));
     }
   } else if constexpr (!FLAT) {
-    // the guessed entry's AGG, at once (a tile with a message start published its INCL already)
+    // the guessed entry's AGG, at once (a tile with a message start published its INCL already;
+    // the expansion launch's tiles find the index launch's)
     uint32_t xE = x0;
     uint64_t runs = runm, w = 0;
-    if (!has_start) {
+    if (!has_start && (PHASE != 2 || gated)) {
       w = readlane32(wave_incl_sum32(mask_words(d, st.s, tm0, runm)), 63);
-      if (l == 0) store_agent(a.desc + t, make_agg(x0, w, Eg, false));
+      if (PHASE != 2 && l == 0) store_agent(a.desc + t, make_agg(x0, w, Eg, false));
     }
     CPK_DIAG_ONLY(ck[3] = clock64(); wk[3] = wall_clock64());
     // the final AGG: for the entry the predecessor's base-chain exit gives
@@ -2030,10 +2192,22 @@ unpack_tiles_kernel(UnpackArgs a) {
       if (l == 0) store_agent(a.desc + t, make_agg(xO, wO, Eo, true));
       fin = true;
     };
-    finalize(false);
-    CPK_DIAG_ONLY(ck[4] = clock64(); wk[4] = wall_clock64());
+    if constexpr (PHASE == 1) {
+      // the index launch: the final AGG too when the predecessor's exit is out already (else the
+      // resolve launch traces the entry); no look-back, no expansion
+      finalize(false);
+      return;
+    }
     uint32_t xprev = (uint32_t)kB + Eg;
-    if (!(a.debug_skip & 8)) excl = lookback_tiles(a, t, &xprev, [&]() { finalize(true); });
+    if (PHASE == 2 && !gated) {
+      // resolved: every tile's true exit is its base-chain exit (the resolve launch checked it)
+      excl = a.texcl[t];
+      xprev = uniform32(a.x0p[t - 1]) & 0x7fffffffu;
+    } else {
+      if (PHASE == 0) finalize(false);
+      CPK_DIAG_ONLY(ck[4] = clock64(); wk[4] = wall_clock64());
+      if (!(a.debug_skip & 8)) excl = lookback_tiles(a, t, &xprev, [&]() { finalize(true); });
+    }
     CPK_DIAG_ONLY(ck[5] = clock64(); wk[5] = wall_clock64());
     const uint32_t E = entry_from_exit(xprev, fms);
     Ein = E;
@@ -2050,9 +2224,12 @@ unpack_tiles_kernel(UnpackArgs a) {
         tm = enter_chain(d, aux, st, tm0, (int)E, (int)fms, x0, &xE, &runs);
       else
         tm = clip_below(tm0, fms, st.s, &xE);
-      if (!has_start) w = readlane32(wave_incl_sum32(mask_words(d, st.s, tm, runs)), 63);
+      if (!has_start && (PHASE != 2 || gated))
+        w = readlane32(wave_incl_sum32(mask_words(d, st.s, tm, runs)), 63);
     }
-    if (!has_start && l == 0) store_agent(a.desc + t, make_desc(kDescIncl, xE, x0, excl + w));
+    if (!has_start && (PHASE != 2 || gated) && l == 0)
+      store_agent(a.desc + t, make_desc(kDescIncl, xE, x0, excl + w));
+    if (!has_start && (PHASE != 2 || gated)) tile_words = w;
     if (a.stamps && l == 0 && t < 1024) {  // diagnostic dump (CPK_STAMPS=1)
       a.stamps[4 * t] = E | ((uint64_t)Eg << 32);
       a.stamps[4 * t + 1] = xE | ((uint64_t)x0 << 32);
@@ -2133,10 +2310,11 @@ unpack_tiles_kernel(UnpackArgs a) {
   }
 
   // ---- expansion -------------------------------------------------------------------------
+  if constexpr (PHASE == 1) return;
   if (a.debug_skip & 256) return;  // diagnostic: + the entry and the look-back
-  if (a.prio) __builtin_amdgcn_s_setprio(0);
+  if (PHASE == 0 && a.prio) __builtin_amdgcn_s_setprio(0);
   if (!FLAT && a.mode == 0 && a.words && Ein > kRunSplit) run_tail(a, A, d, Ein, excl, win);
-  expand_records(a, A, d, aux, dep_tab, tm, excl, win, mfirst, mlast, msw);
+  expand_records(a, A, d, aux, dep_tab, tm, excl, win, mfirst, mlast, msw, tile_words);
   // a fused single-tile batch: this wave is the whole call -- its error word for the host, last:
   // its stores done, then a system-scope release
   if (a.err_host) {
@@ -2156,6 +2334,152 @@ unpack_tiles_kernel(UnpackArgs a) {
     g_timeline[8 * t + 7] = FLAT ? wflat : __builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_ID
   }
 #endif
+}
+
+// ---------------------------------------------------------------------------------------------
+// Split decode (message batches, cpk_unpack_messages): the one-pass tile kernel above spends a
+// quarter of a tile's life in its look-back, waiting for predecessors that are still walking
+// their own chain 0.  Split into three launches, no tile ever waits on another tile:
+//   index    (PHASE 1) stage, chain 0 and the tile's descriptor (AGG with its guessed entry, or
+//            INCL when a message starts in it) exactly as the one-pass kernel publishes them,
+//            plus chain 0's record-start bits (512 B per tile) and the guessed entry;
+//   resolve  (below) every tile's true entry is where its predecessor's base-chain exit leads --
+//            true as long as every tile's exit is its base-chain exit, which this launch checks
+//            -- so each tile's words follow from its own descriptor (or, when its guessed entry was
+//            not that one, from its chain re-traced from the true entry) and the words before
+//            every tile are one segmented scan (decoupled look-back over 64-tile groups);
+//   expand   (PHASE 2) stage, chain 0 from the bits, the entry from the predecessor's exit, the
+//            expansion.
+// A tile whose true exit is not its base-chain exit (chains that do not meet within a tile) sets
+// the gate, and the expansion launch then runs the one-pass look-back on the index launch's
+// descriptors instead -- the same results, the one-pass kernel's speed.
+__global__ __launch_bounds__(256) void unpack_resolve_kernel(ResolveArgs r) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds_data[4][kB + kPad + 16];
+  __shared__ uint64_t lds_aux[4][128];
+  __shared__ unsigned int s_ticket;
+  const int l = lane_id();
+  const int wv = (int)uniform32(threadIdx.x >> 6);
+  // groups in ticket order: a group waits only on groups whose workgroups took their tickets
+  // before its own (running or done), whatever else shares the device
+  if (threadIdx.x == 0) s_ticket = atomicAdd(r.ticket, 1u);
+  __syncthreads();
+  const uint64_t g = (uint64_t)uniform32(s_ticket) * 4 + (uint64_t)wv;
+  const uint64_t ngroups = resolve_groups(r.ntiles);
+  if (g >= ngroups) return;
+  const uint64_t P = r.nbytes;
+  const uint64_t t = g * kResolveGroup + (uint64_t)l;
+  const bool valid = t < r.ntiles;
+  const uint64_t tc = valid ? t : r.ntiles - 1;
+  // (the index launch is complete: plain loads)
+  const uint64_t dv = r.desc[tc];
+  const uint32_t x0 = r.x0p[tc] & 0x7fffffffu;
+  const uint32_t xp = tc > 0 ? (r.x0p[tc - 1] & 0x7fffffffu) : 0u;
+  const uint64_t A = tc * kB;
+  // an AGG tile holds no message start; its first "start" is the batch end, if inside it
+  const uint32_t fmsn = (P - A) < (uint64_t)kB ? (uint32_t)(P - A) : (uint32_t)kB;
+  const uint64_t stt = dv & kDescFlags;
+  uint64_t v = 0;
+  uint32_t reset = 0, bad = 0, fix = 0;
+  const uint32_t E = entry_from_exit(xp, fmsn);
+  if (valid) {
+    if (stt == kDescIncl) {
+      v = dv & kWordsMask;  // words after the last message start in the tile
+      reset = 1;
+    } else if (stt == kDescAgg) {
+      if (desc_entry(dv) == E) {
+        v = dv & kWordsMask;
+        bad = desc_exit(dv) != x0;  // (a final AGG whose chain never met chain 0)
+      } else {
+        fix = 1;
+      }
+    } else {
+      bad = 1;  // (unreachable: the index launch publishes every tile)
+    }
+  }
+  // tiles whose guessed entry is not the true one: the chain from the true entry, traced onto
+  // chain 0 in LDS (as the one-pass kernel's finalisation does)
+  uint64_t fixes = ballot(fix != 0);
+  uint8_t* const d = lds_data[wv];
+  uint64_t* const aux = lds_aux[wv];
+  const bool aligned = ((uintptr_t)r.packed & 15) == 0;
+  while (fixes) {
+    const int j = lowest_bit(fixes);
+    fixes &= fixes - 1;
+    const uint64_t tj = g * kResolveGroup + (uint64_t)j;
+    const uint64_t Aj = tj * kB;
+    const uint32_t Ej = readlane32(E, j), x0j = readlane32(x0, j), fj = readlane32(fmsn, j);
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+      const int o = 16 * (64 * k + l);
+      if (o < kB + kPad) {
+        const uint64_t b = Aj + (uint64_t)o;
+        u32x4 q = {0, 0, 0, 0};
+        if (aligned && b + 16 <= P) {
+          q = *(const u32x4*)(r.packed + b);
+        } else {
+          uint32_t w4[4] = {0, 0, 0, 0};
+          for (int i = 0; i < 16; i++)
+            if (b + i < P) w4[i >> 2] |= (uint32_t)r.packed[b + i] << (8 * (i & 3));
+          q = (u32x4){w4[0], w4[1], w4[2], w4[3]};
+        }
+        *(u32x4*)(d + o) = q;
+      }
+    }
+    lane_handoff();
+    const uint64_t tm0 = r.tbits[tj * 64 + (uint64_t)l];
+    uint64_t runs = run_bytes(d, 64 * l);
+    const uint64_t pe = P - Aj;  // the batch end, tile-relative (a start when inside the tile)
+    const uint64_t msw = (pe < (uint64_t)kB && (int)(pe >> 6) == l) ? 1ull << (pe & 63) : 0ull;
+    const uint64_t fp = r.tile_firstpos[tj];
+    const uint64_t na = (fp < P ? fp : P) - Aj;
+    const SubTile st = make_subtile(Aj, P, msw, na < (uint64_t)kDead ? (int)na : kDead);
+    uint32_t xO = x0j;
+    uint64_t tmO;
+    if (Ej < fj)
+      tmO = enter_chain(d, aux, st, tm0, (int)Ej, (int)fj, x0j, &xO, &runs);
+    else
+      tmO = clip_below(tm0, fj, st.s, &xO);
+    const uint64_t wO = readlane32(wave_incl_sum32(mask_words(d, st.s, tmO, runs)), 63);
+    if (l == j) {
+      v = wO;
+      bad = xO != x0j;
+    }
+    lane_handoff();  // (the next fix overwrites d and aux)
+  }
+  // inclusive segmented scan over the group (a tile with a message start restarts the sum)
+  uint64_t s = v;
+  uint32_t f = reset;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int src = l >= o ? l - o : l;
+    const uint64_t ps = shfl64(s, src);
+    const uint32_t pf = shfl32(f, src);
+    if (l >= o) {
+      if (!f) s += ps;
+      f |= pf;
+    }
+  }
+  const uint64_t agg = readlane64(s, 63);
+  const bool aggf = ballot(reset != 0) != 0;
+  uint64_t gex = 0;
+  if (g == 0) {
+    if (l == 0) store_agent(r.gdesc, kDescIncl | agg);
+  } else if (aggf) {
+    // (the group's total is its words after its last restart: inclusive at once; its tiles up to
+    // that restart still need the words before the group)
+    if (l == 0) store_agent(r.gdesc + g, kDescIncl | agg);
+    gex = lookback<8>(r.gdesc, g, r.err);
+  } else {
+    if (l == 0) store_agent(r.gdesc + g, kDescAgg | agg);
+    gex = lookback<8>(r.gdesc, g, r.err);
+    if (l == 0) store_agent(r.gdesc + g, kDescIncl | (gex + agg));
+  }
+  const int pl = l > 0 ? l - 1 : 0;
+  const uint64_t se = shfl64(s, pl);
+  const uint32_t fe = shfl32(f, pl);
+  const uint64_t ex = l == 0 ? gex : (fe ? se : gex + se);
+  if (valid) r.texcl[t] = ex;
+  if (ballot(bad != 0) && l == 0) store_agent32(r.gate, 1u);
 }
 
 // Status before any record is seen (buffers with no records keep it): flat-packed chunks read
@@ -2213,14 +2537,24 @@ hipError_t launch_unpack_header(const uint8_t* packed, uint64_t P, const uint64_
   return hipGetLastError();
 }
 
+hipError_t launch_unpack_resolve(const ResolveArgs& r, hipStream_t stream) {
+  const uint64_t ng = resolve_groups(r.ntiles);
+  if (ng == 0) return hipSuccess;
+  hipLaunchKernelGGL(unpack_resolve_kernel, dim3((unsigned)((ng + 3) / 4)), dim3(256), 0, stream, r);
+  return hipGetLastError();
+}
+
 hipError_t launch_unpack_stage(int stage, const UnpackArgs& a, hipStream_t stream) {
   if (a.ntiles == 0) return hipSuccess;
   const dim3 grid((unsigned)((a.ntiles + 3) / 4));
-  if (a.desc2)
-    hipLaunchKernelGGL((unpack_tiles_kernel<true>), grid, dim3(256), 0, stream, a);
+  if (stage == kUnpackIndex)
+    hipLaunchKernelGGL((unpack_tiles_kernel<false, 1>), grid, dim3(256), 0, stream, a);
+  else if (stage == kUnpackExpand)
+    hipLaunchKernelGGL((unpack_tiles_kernel<false, 2>), grid, dim3(256), 0, stream, a);
+  else if (a.desc2)
+    hipLaunchKernelGGL((unpack_tiles_kernel<true, 0>), grid, dim3(256), 0, stream, a);
   else
-    hipLaunchKernelGGL((unpack_tiles_kernel<false>), grid, dim3(256), 0, stream, a);
-  (void)stage;
+    hipLaunchKernelGGL((unpack_tiles_kernel<false, 0>), grid, dim3(256), 0, stream, a);
   return hipGetLastError();
 }
 

@@ -97,6 +97,11 @@ def gather_packed(packed, msg_out_off, nmsgs: int, dst: int = 0, dist=None, devi
     P = int(msg_out_off[nmsgs].item())
     if dist is None:
         return packed[:P], msg_out_off[: nmsgs + 1]
+    if first_msg is not None and packed.device.type != "cpu" and codec is None:
+        # (checked on every rank before any collective: the placement of non-contiguous shards on
+        # the device needs the codec, and a rank failing after the exchange would strand the rest)
+        raise ValueError("gather_packed: pass codec= to place device tensors of round-robin "
+                         "shards (first_msg given)")
     world, rank = dist.get_world_size(), dist.get_rank()
     contiguous_flag = 1 if first_msg is None else 0
     meta = torch.tensor([P, nmsgs, 0 if first_msg is None else first_msg, msg_stride,
@@ -176,8 +181,6 @@ def gather_packed(packed, msg_out_off, nmsgs: int, dst: int = 0, dist=None, devi
         for s_, d_, n_ in zip(src.tolist(), dst_off.tolist(), msize.tolist()):
             out[d_:d_ + n_] = buf[s_:s_ + n_]
     else:
-        if codec is None:
-            raise ValueError("gather_packed: pass codec= to place device tensors")
         codec.copy_ranges(buf, src, dst_off, msize, out)
     return out, goff
 

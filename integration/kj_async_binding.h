@@ -49,7 +49,11 @@ class FlatWordsMessageReader final : public capnp::MessageReader {
                          capnp::ReaderOptions options)
       : capnp::MessageReader(options), owned_(kj::mv(owned)) {
     const uint32_t* t = reinterpret_cast<const uint32_t*>(words.begin());
+    // (the device read rejected such a header already; this reader allocates from it, so it checks
+    // again: serialize.c++:217, and the UINT_MAX case of serialize-test.c++:533-543)
+    KJ_REQUIRE(words.size() > 0 && t[0] < 511, "Message has too many segments.");
     const size_t nseg = size_t(t[0]) + 1;
+    KJ_REQUIRE(nseg / 2 + 1 <= words.size(), "segment table disagrees with the words");
     size_t off = nseg / 2 + 1;
     segs_ = kj::heapArray<kj::ArrayPtr<const capnp::word>>(nseg);
     for (size_t i = 0; i < nseg; i++) {

@@ -214,6 +214,24 @@ void clean_eof(kj::AsyncIoStream& a, kj::AsyncIoStream& b, const Fixture& f, kj:
   check(eof == kj::none, kind + ": clean EOF -> none");
 }
 
+// serialize-test.c++:533-543 on the async reader the advisory is about
+// (security-advisories/2026-03-12-0-segment-count-overflow.md): a first word of
+// ff ff ff ff 00 00 00 00 (packed 0f ff ff ff ff) is "Message has too many segments.".
+void uint_max_segment_count(kj::AsyncIoStream& a, kj::AsyncIoStream& b, kj::WaitScope& ws,
+                            const std::string& kind) {
+  step(kind + ": UINT_MAX segment count");
+  static const kj::byte bytes[] = {0x0f, 0xff, 0xff, 0xff, 0xff};
+  // (not waited for before the read: an in-memory pipe's write completes only as it is read)
+  auto w = a.write(kj::arrayPtr(bytes, sizeof(bytes))).eagerlyEvaluate(nullptr);
+  cpk_kj::PackedMessageStream sb(b);
+  bool threw = false;
+  KJ_IF_SOME(e, kj::runCatchingExceptions([&]() { sb.readMessage().wait(ws); })) {
+    threw = e.getDescription().contains("Message has too many segments.");
+  }
+  w.wait(ws);
+  check(threw, kind + ": UINT_MAX segment count rejected (Message has too many segments.)");
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -249,6 +267,14 @@ int main(int argc, char** argv) {
   {
     auto mem = kj::newTwoWayPipe();
     clean_eof(*mem.ends[0], *mem.ends[1], fx[0], ws, "in-memory");
+  }
+  {
+    auto sock = io.provider->newTwoWayPipe();
+    uint_max_segment_count(*sock.ends[0], *sock.ends[1], ws, "socket");
+  }
+  {
+    auto mem = kj::newTwoWayPipe();
+    uint_max_segment_count(*mem.ends[0], *mem.ends[1], ws, "in-memory");
   }
   std::printf("async binding ok: %d checks (socket pair + in-memory pipe, %zu fixtures)\n",
               checks, fx.size());

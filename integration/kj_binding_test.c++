@@ -458,6 +458,21 @@ void reference_round_trips() {
   }
 }
 
+// serialize-test.c++:533-543: a segment count of UINT_MAX + 1 is "Message has too many segments."
+// (security-advisories/2026-03-12-0-segment-count-overflow.md).  Its first word
+// ff ff ff ff 00 00 00 00 packs to the record 0f ff ff ff ff.
+void uint_max_segment_count() {
+  const kj::byte bytes[] = {0x0f, 0xff, 0xff, 0xff, 0xff};
+  kj::ArrayInputStream in(kj::arrayPtr(bytes, sizeof(bytes)));
+  bool threw = false;
+  try {
+    cpk_kj::PackedMessageReader r(in);
+  } catch (const cpk_capnp::Exception& e) {
+    threw = std::string(e.what()).find("Message has too many segments.") != std::string::npos;
+  }
+  check(threw, "UINT_MAX segment count: PackedMessageReader throws \"Message has too many segments.\"");
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -481,7 +496,8 @@ int main(int argc, char** argv) {
   fixture(dir, "segmented", "segmented-packed");
   addressbook(dir);
   reference_round_trips();
+  uint_max_segment_count();
   std::printf("binding ok: %d checks (%d KATs, 2 fixtures, addressbook, the RoundTrip tests of "
-              "serialize-packed-test.c++:225-585)\n", checks, k);
+              "serialize-packed-test.c++:225-585, the UINT_MAX segment count)\n", checks, k);
   return 0;
 }

@@ -86,3 +86,87 @@ def test_gather_placement_of_round_robin_shards(codec):
     codec.sync()
     P = int(woff[-1].item())
     assert torch.equal(goff, woff) and torch.equal(out, whole[:P])
+
+
+class _OneProcessDist:
+    """torch.distributed's calls as gather_packed makes them, for `world` simulated ranks whose
+    packed shards live in this process: rank `rank` is the destination, the others' sends are
+    the copies out of their tensors (the device branch of gather_packed runs for real)."""
+
+    class P2POp:
+        def __init__(self, op, tensor, peer):
+            self.op, self.tensor, self.peer = op, tensor, peer
+
+    def __init__(self, shards, rank=0):
+        self.shards, self.rank = shards, rank  # shards[r] = (packed[:P], offsets[:n + 1], first, stride)
+
+    def get_world_size(self):
+        return len(self.shards)
+
+    def get_rank(self):
+        return self.rank
+
+    def all_gather(self, parts, meta):
+        import torch
+
+        for r, (p, o, first, stride) in enumerate(self.shards):
+            n = int(o.numel()) - 1
+            parts[r].copy_(torch.tensor([int(p.numel()), n, first, stride, 0], dtype=torch.int64))
+
+    def isend(self, *a):  # (never called on the destination)
+        raise AssertionError("send on the destination rank")
+
+    def irecv(self, *a):
+        pass
+
+    def batch_isend_irecv(self, ops):
+        class Done:
+            def wait(self):
+                return True
+
+        # rank r sends its bytes first, then its offsets (gather_packed's order)
+        seen = {}
+        for op in ops:
+            assert op.op == self.irecv
+            k = seen.get(op.peer, 0)
+            p, o, _, _ = self.shards[op.peer]
+            op.tensor.copy_(p if k == 0 else o[:-1])
+            seen[op.peer] = k + 1
+        return [Done() for _ in ops]
+
+
+def test_gather_packed_device_branch(codec):
+    """gather_packed itself (shard.py) on device tensors of round-robin shards: the all-gather
+    of the ranks' metadata, the receives into the staging buffer, the global message ids and
+    their checks, and the device placement by copy_ranges -- with the other ranks simulated in
+    this process.  The result equals one pack of the whole batch; without codec= it refuses
+    before any exchange."""
+    import torch
+
+    from capnproto_amd.shard import gather_packed, shard_messages
+
+    world, n_global = 3, 151
+    off, total = codec.gen_offsets(n_global, seed=13)
+    words = codec.gen_messages("mixed", off, total, seed=13)
+    whole, woff, _ = codec.pack_messages(words, off)
+    codec.sync()
+    shards = []
+    for r in range(world):
+        first, stride, count = shard_messages(r, world, n_global, "round_robin")
+        o, tot = codec.gen_offsets(count, seed=13, first_msg=first, msg_stride=stride)
+        w = codec.gen_messages("mixed", o, tot, seed=13, first_msg=first, msg_stride=stride)
+        p, po, st = codec.pack_messages(w, o)
+        codec.sync()
+        assert (st == 0).all()
+        shards.append((p[: int(po[-1].item())].clone(), po.clone(), first, stride))
+    dist = _OneProcessDist(shards)
+    p0, o0, first0, stride0 = shards[0]
+    n0 = int(o0.numel()) - 1
+    out, goff = gather_packed(p0, o0, n0, dst=0, dist=dist, device="cpu", first_msg=first0,
+                              msg_stride=stride0, codec=codec)
+    codec.sync()
+    P = int(woff[-1].item())
+    assert torch.equal(goff, woff) and torch.equal(out, whole[:P])
+    with pytest.raises(ValueError, match="codec"):
+        gather_packed(p0, o0, n0, dst=0, dist=dist, device="cpu", first_msg=first0,
+                      msg_stride=stride0)

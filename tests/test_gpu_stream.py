@@ -146,6 +146,10 @@ def test_reader_failures(codec, oracle):
     # a header claiming 512 segments (serialize.c++:217)
     too_many = oracle.pack_chunk(np.array([511 | (1 << 32)], np.uint64))
     check(codec, oracle, b"".join(good) + too_many + good[0])
+    # segment count UINT_MAX + 1 (serialize-test.c++:533-543): the first word ff ff ff ff 00 00 00 00
+    uint_max = bytes([0x0F, 0xFF, 0xFF, 0xFF, 0xFF])
+    check(codec, oracle, uint_max)
+    check(codec, oracle, b"".join(good) + uint_max + good[0])
     # a message larger than the traversal limit (serialize.c++:235)
     big = oracle.pack_flat(cases.flat_message(rng, 1, [300], "mixed"))[0]
     check(codec, oracle, good[0] + big + good[1], limit=100)

@@ -109,6 +109,35 @@ def test_parity_locked_chains(codec, oracle):
         check_against_oracle(codec, oracle, [tiny] + msgs[::-1])
 
 
+def test_uint_max_segment_count(codec, oracle):
+    """serialize-test.c++:533-543: a first word of ff ff ff ff 00 00 00 00 (segment count
+    UINT_MAX + 1, packed 0f ff ff ff ff) is "Message has too many segments." -- alone, among
+    valid messages, and inside a batch of many tiles (the split decode)."""
+    bad = bytes([0x0F, 0xFF, 0xFF, 0xFF, 0xFF])
+    assert oracle.pack_chunk(np.frombuffer(bytes([0xFF] * 4 + [0] * 4), "<u8")) == bad
+    _, st, woff = gpu_unpack(codec, [bad])
+    assert st[0] == P.TOO_MANY_SEGMENTS and woff[1] == woff[0]
+    rng = np.random.default_rng(44)
+    good = [oracle.pack_flat(cases.flat_message(rng, 2, [700, 900], "mixed"))[0] for _ in range(12)]
+    msgs = good[:5] + [bad] + good[5:] + [bad]
+    check_against_oracle(codec, oracle, msgs)
+    _, st, _ = gpu_unpack(codec, msgs)
+    assert list(np.nonzero(st)[0]) == [5, len(msgs) - 1]
+    assert (st[[5, len(msgs) - 1]] == P.TOO_MANY_SEGMENTS).all()
+    # the host entry point (its own staging path: one pinned buffer, one launch)
+    import ctypes as C
+
+    src = np.frombuffer(bad, np.uint8).copy()
+    ioff = np.array([0, len(bad)], np.uint64)
+    back = np.zeros(16, np.uint64)
+    wo = np.zeros(2, np.uint64)
+    st2 = np.full(1, -1, np.int32)
+    ptr = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+    r = codec.lib.cpk_unpack_messages_host(codec.ctx, ptr(src), len(bad), ptr(ioff), 1, ptr(back),
+                                           16, ptr(wo), ptr(st2), None)
+    assert r == 0 and st2[0] == P.TOO_MANY_SEGMENTS and wo[1] == wo[0]
+
+
 def test_error_cases(codec, oracle):
     rng = np.random.default_rng(21)
     msgs = []

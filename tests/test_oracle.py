@@ -149,6 +149,24 @@ def test_batch_vs_reference(oracle):
     assert wr.tobytes() == np.concatenate(segs).tobytes()
 
 
+# serialize-test.c++:533-543 ("large segment counts are rejected -- even UINT_MAX";
+# security-advisories/2026-03-12-0-segment-count-overflow.md): first word ff ff ff ff 00 00 00 00,
+# packed as the record 0f ff ff ff ff.
+UINT_MAX_SEGMENTS = bytes([0x0F, 0xFF, 0xFF, 0xFF, 0xFF])
+
+
+def test_uint_max_segment_count(oracle):
+    w = np.frombuffer(bytes([0xFF] * 4 + [0] * 4), "<u8")
+    assert oracle.pack_chunk(w) == UINT_MAX_SEGMENTS
+    st, _, _ = oracle.read_message(UINT_MAX_SEGMENTS)
+    assert st == P.TOO_MANY_SEGMENTS
+    if P.reference_available():
+        ref = P.Reference()
+        assert ref.pack_chunk(w) == UINT_MAX_SEGMENTS
+        assert ref.read_message(UINT_MAX_SEGMENTS)[0] == P.TOO_MANY_SEGMENTS
+        assert "too many segments" in ref.last_error()
+
+
 def test_c1_addressbook_fixture(oracle):
     """Config C1: the addressbook sample's message (samples/addressbook.c++:47-76) and its
     packed form, both hash-pinned to the compiled sample; the oracle packs the

@@ -23,6 +23,12 @@ KERNELS = {"unpack_tiles_kernel": "unpack_tiles", "header_kernel": "unpack_heade
 def short(name):
     if "cpk::" not in name:
         return None
+    if "unpack_tiles_kernel<false, 1>" in name:
+        return "unpack_index"
+    if "unpack_tiles_kernel<false, 2>" in name:
+        return "unpack_expand"
+    if "unpack_resolve_kernel" in name:
+        return "unpack_resolve"
     if "pack_tile_kernel" in name:
         return "pack_tile"
     if "pack_place_kernel" in name:
