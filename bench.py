@@ -75,7 +75,7 @@ def parse():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--sub", default=None,
                     help="comma-separated extra configs measured after the headline "
-                         "(default at N=1: c3,c4,c5; 'none' to skip)")
+                         "(default at N=1: c3,c4,c4g,c5; 'none' to skip)")
     ap.add_argument("--sub-steps", type=int, default=5)
     ap.add_argument("--shard", default=None, choices=["block", "round_robin", "bytes"],
                     help="message assignment to ranks (default: the config's)")
@@ -268,9 +268,9 @@ def measure_copy(codec, nbytes=1 << 31, reps=6):
     """Device-to-device copy ceiling in the same run: our streaming copy kernel (16 B per lane;
     capnproto_amd/csrc/cpk_stream.hip copy_kernel), the best of a sweep over 4 / 8 / 16 loads in
     flight per lane, default or non-temporal loads and stores, grid-strided or contiguous
-    per-block shares, and four grid sizes; read + write bytes / time of 2 GiB each way, timed with
-    HIP events on the stream it runs on.  (MI355X_MICROARCH.md quotes 6.29 TB/s for a float4
-    copy.)"""
+    per-block shares, LDS-DMA staging (global_load_lds_dwordx4, 2 / 4 / 8 KiB per wave), and six
+    grid sizes; read + write bytes / time of 2 GiB each way, timed with HIP events on the stream it
+    runs on.  (MI355X_MICROARCH.md quotes 6.29 TB/s for a float4 copy.)"""
     import ctypes as C
 
     torch = codec.torch
@@ -281,7 +281,8 @@ def measure_copy(codec, nbytes=1 << 31, reps=6):
     best = 0.0
     sweep = {}
     names = {0: "x4", 1: "x8", 2: "x16"}
-    for form in (0, 1, 2, 4, 5, 6, 8, 9, 10, 12, 13, 14):
+    # forms 16+: LDS-DMA staging (global_load_lds_dwordx4) of 2 / 4 / 8 KiB per wave
+    for form in (0, 1, 2, 4, 5, 6, 8, 9, 10, 12, 13, 14, 16, 17, 18, 20, 21, 22):
       for g in (1024, 2048, 4096, 8192, 16384, 32768):
         blocks = (form << 24) | g
 
@@ -299,7 +300,8 @@ def measure_copy(codec, nbytes=1 << 31, reps=6):
         e1.record(s)
         torch.cuda.synchronize()
         gbps = 2 * nbytes / (e0.elapsed_time(e1) / reps * 1e-3) / 1e9
-        tag = names[form & 3] + ("nt" if form & 4 else "") + ("c" if form & 8 else "")
+        tag = (("lds%dk" % (2 << (form & 3))) if form & 16 else names[form & 3]) + \
+            ("nt" if form & 4 else "") + ("c" if form & 8 else "")
         sweep[f"{tag}/{g}"] = round(gbps, 1)
         best = max(best, gbps)
     ok = torch.equal(a, b)
@@ -527,10 +529,11 @@ def summarize(res, world, copy_gbps):
             "traffic": traffic,
             "read_only_frac": round(rd / HBM_PEAK_GBS, 4),
             "measured_copy_GBps": round(copy_gbps, 1) if copy_gbps else None,
-            "measured_copy_kernel": "copy_kernel (cpk_stream.hip): 16 B/lane streaming copy, "
-                                    "best of a sweep over loads in flight per lane (4, 8, 16), "
-                                    "default or non-temporal access, grid-strided or contiguous "
-                                    "blocks, and grid size; read + write bytes, 1 GiB each way",
+            "measured_copy_kernel": "copy_kernel / copy_lds_kernel (cpk_stream.hip): 16 B/lane "
+                                    "streaming copy, best of a sweep over loads in flight per "
+                                    "lane (4, 8, 16), default or non-temporal access, grid-strided "
+                                    "or contiguous blocks, LDS-DMA staging (2 / 4 / 8 KiB per "
+                                    "wave), and grid size; read + write bytes, 2 GiB each way",
             "frac_of_measured_copy": round(rt / copy_gbps, 4) if copy_gbps else None,
             "dominant_kernel": {
                 "kernel": dom,
@@ -607,7 +610,7 @@ def main():
     torch.cuda.empty_cache()
 
     subs = []
-    sub = args.sub if args.sub is not None else ("c3,c4,c5" if world == 1 else "none")
+    sub = args.sub if args.sub is not None else ("c3,c4,c4g,c5" if world == 1 else "none")
     for nm in [s for s in sub.split(",") if s and s != "none" and s != args.config]:
         r = run_config(nm, args, args.sub_steps, 2, rank, world, dist, codec)
         r["cpu_baseline"] = None

@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <mutex>
 #include <chrono>
 #include <new>
 #include <utility>
@@ -289,6 +290,45 @@ struct TimedLaunch {
 // Orders this call after the context's previous call when they come on different streams: the
 // scratch, the tile tables and stage[] belong to the context, not to a stream.  (Inside a graph
 // capture the previous stream's work is outside the graph: captured sequences use one stream.)
+//
+// And no two of the codec's waiting launches (tile look-backs, the header scan), from any context
+// of the process, run at the same time on one device.  Within one launch a tile waits only on
+// tiles dealt earlier to the per-XCD dispatchers, which dispatch in order, so the lowest unfinished
+// tile is always resident; two such launches side by side could each fill the XCDs the other's
+// next workgroup needs (forward progress).  Kernels of other libraries never wait on
+// a codec tile: they only delay it.  So a call that launches waiting kernels (DeviceTurn::waiting)
+// records the device's order event behind them, and a call on another stream waits for it first;
+// DeviceTurn holds the device's order lock for the whole call, so the event covers the launches.
+struct DeviceOrder {
+  std::recursive_mutex m;
+  hipStream_t last = nullptr;
+  bool has = false;
+  hipEvent_t ev = nullptr;
+};
+DeviceOrder& device_order(int device) {
+  static DeviceOrder orders[64];
+  return orders[device & 63];
+}
+bool capturing(hipStream_t s) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone;
+}
+struct DeviceTurn {
+  DeviceOrder& o;
+  std::unique_lock<std::recursive_mutex> lk;
+  hipStream_t stream = nullptr;
+  bool waiting = false;  // this call launched waiting kernels on `stream`
+  explicit DeviceTurn(cpk_ctx* ctx) : o(device_order(ctx ? ctx->device : 0)), lk(o.m) {}
+  ~DeviceTurn() {
+    if (!waiting || capturing(stream)) return;
+    if (!o.ev && hipEventCreateWithFlags(&o.ev, hipEventDisableTiming) != hipSuccess) return;
+    if (hipEventRecord(o.ev, stream) == hipSuccess) {
+      o.last = stream;
+      o.has = true;
+    }
+  }
+};
+
 cpk_status order_streams(cpk_ctx* ctx, hipStream_t s) {
   if (ctx->used && s != ctx->last_stream) {
     // an event recorded on (or waited for by) a capturing stream would join the other stream to
@@ -307,6 +347,10 @@ cpk_status order_streams(cpk_ctx* ctx, hipStream_t s) {
   }
   ctx->used = true;
   ctx->last_stream = s;
+  // the device's last waiting launches, when on another stream (of any context)
+  DeviceOrder& o = device_order(ctx->device);
+  if (o.has && o.last != s && !capturing(s) && hipStreamWaitEvent(s, o.ev, 0) != hipSuccess)
+    return CPK_ERR_HIP;
   return CPK_OK;
 }
 
@@ -372,6 +416,7 @@ cpk_status pack_common(cpk_ctx* ctx, const uint64_t* d_words, uint64_t N, const 
                        uint64_t* d_out_off, int32_t* d_status, hipStream_t stream) {
   if (!ctx || (!d_off && n) || (!d_words && N) || (!d_out && cap)) return CPK_ERR_INVALID_ARGUMENT;
   if (hipSetDevice(ctx->device) != hipSuccess) return CPK_ERR_HIP;
+  DeviceTurn turn(ctx);  // (for the rest of the call)
   if (order_streams(ctx, stream) != CPK_OK) return CPK_ERR_HIP;
   const uint64_t T = cpk::kPackTileWords;
   const uint64_t ntiles = (N + T - 1) / T;
@@ -448,6 +493,8 @@ cpk_status pack_common(cpk_ctx* ctx, const uint64_t* d_words, uint64_t N, const 
   a.frame_off = d_off;
   a.frame_n = n;
   a.frame_status = d_status;
+  turn.stream = stream;
+  turn.waiting = !single;  // (the tile kernel's waits, the placement's look-back)
   TimedLaunch tl(ctx, 0, stream);
   // tiles -> output (offset known in time) or arena pieces, placed by the placement launch
   e = cpk::launch_pack_tiles(a, stream);
@@ -521,7 +568,7 @@ UnpackScratch carve_unpack(void* base, uint64_t ntiles, uint64_t n, bool flat = 
   s.desc2 = flat ? c.take<uint64_t>(ntiles) : nullptr;
   s.gdesc = split ? c.take<uint64_t>(cpk::resolve_groups(ntiles)) : nullptr;
   s.gate = split ? c.take<uint32_t>(4) : nullptr;
-  s.ticket = split ? (unsigned int*)(s.gate + 1) : nullptr;
+  s.ticket = split ? (unsigned int*)(s.gate + 1) : nullptr;  // the resolve launch's group tickets
   s.zero_bytes = c.off;
   s.tile_first = c.take<uint64_t>(ntiles);
   s.tile_firstpos = c.take<uint64_t>(ntiles);
@@ -551,6 +598,7 @@ cpk_status unpack_common(cpk_ctx* ctx, uint32_t mode, const uint8_t* d_packed, u
   if (!ctx || (!d_in_off && n) || (!d_packed && P) || (!d_status && n) || (d_rec_pos && !d_rec_gen))
     return CPK_ERR_INVALID_ARGUMENT;
   if (hipSetDevice(ctx->device) != hipSuccess) return CPK_ERR_HIP;
+  DeviceTurn turn(ctx);  // (for the rest of the call)
   if (order_streams(ctx, stream) != CPK_OK) return CPK_ERR_HIP;
   const uint64_t B = cpk::kUnpackTileBytes;
   const uint64_t ntiles = (P + B - 1) / B;
@@ -577,6 +625,9 @@ cpk_status unpack_common(cpk_ctx* ctx, uint32_t mode, const uint8_t* d_packed, u
   tf.zero_words = s.zero_bytes / 8;
   // a single-tile batch of few messages: one launch, the tile kernel reading the headers itself
   const bool fuse = mode == 0 && ntiles == 1 && n <= cpk::kUnpackFuseMsgs;
+  // (waiting launches: the tile kernel's look-back, the header launch's scan)
+  turn.stream = stream;
+  turn.waiting = ntiles > 1 || (mode == 0 && !fuse && cpk::header_scan_blocks(n) > 1);
   if (mode == 0) {
     if (!d_word_off_out) return CPK_ERR_INVALID_ARGUMENT;
     if (n == 0) return hip_status(cpk::launch_fill(d_word_off_out, 8, 0, stream));
@@ -637,7 +688,6 @@ cpk_status unpack_common(cpk_ctx* ctx, uint32_t mode, const uint8_t* d_packed, u
   a.tegs = s.tegs;
   a.texcl = s.texcl;
   a.gate = s.gate;
-  a.ticket = nullptr;
   TimedLaunch tl(ctx, 1, stream);
   if (split) {
     cpk::ResolveArgs r;
@@ -822,6 +872,7 @@ cpk_status cpk_pack_segments(cpk_ctx* ctx, const uint64_t* const* h_seg_ptrs,
   if (nseg > (1u << 20)) return CPK_ERR_INVALID_ARGUMENT;
   if (hipSetDevice(ctx->device) != hipSuccess) return CPK_ERR_HIP;
   hipStream_t s = (hipStream_t)stream;
+  DeviceTurn turn(ctx);  // (for the rest of the call)
   if (order_streams(ctx, s) != CPK_OK) return CPK_ERR_HIP;
   const uint64_t tw = nseg / 2 + 1;
   // meta: seg_ptr[nseg], chunk_off[nseg + 2], table[tw]
@@ -975,6 +1026,7 @@ cpk_status cpk_split_packed_stream(cpk_ctx* ctx, const uint8_t* d_packed, uint64
   if (hipSetDevice(ctx->device) != hipSuccess) return CPK_ERR_HIP;
   const uint64_t limit = limits ? limits->traversal_limit_words : 8ull * 1024 * 1024;
   hipStream_t s = (hipStream_t)stream;
+  DeviceTurn turn(ctx);  // (for the rest of the call)
   if (order_streams(ctx, s) != CPK_OK) return CPK_ERR_HIP;
   // (record positions share their u64 with the call's generation: kRecGenShift bits)
   if (nbytes >> cpk::kRecGenShift) return CPK_ERR_INVALID_ARGUMENT;

@@ -179,6 +179,20 @@ __device__ __forceinline__ void frame_message(const uint64_t* __restrict__ words
   if (status) status[i] = st;
 }
 
+// Workgroup ticket: a launch's tiles in the order their workgroups START (thread 0 takes the next
+// ticket from a zeroed counter; the workgroup reads it back from LDS).  A tile that waits only on
+// lower tickets then waits only on workgroups that are running or done, whatever else the device
+// runs.  The tickets of one launch serialize on one counter (~13 ns each on MI355X: C4's pack
+// with a ticket per tile took 20.2 ms instead of 7.6), so only the small resolve launch of the
+// split decode uses them; the tile kernels keep blockIdx order, whose forward progress rests on
+// the per-XCD in-order dispatch and on the codec never running two of its waiting launches at
+// once (cpk_api.cpp DeviceOrder).
+__device__ __forceinline__ uint32_t wg_ticket(unsigned int* counter, unsigned int* s_slot) {
+  if (threadIdx.x == 0) *s_slot = atomicAdd(counter, 1u);
+  __syncthreads();
+  return uniform32(*(volatile unsigned int*)s_slot);
+}
+
 // Workgroup b's tile-order index when consecutive tiles should share an XCD: workgroups are
 // dealt to the 8 XCDs round robin (b % 8 -- for speed only, nothing relies on it), so the j-th
 // workgroup of XCD x takes index (j / C) * 8C + x * C + j % C -- chunks of C consecutive indices
@@ -267,17 +281,18 @@ __host__ __device__ inline bool tile_first_search(const TileFirstJob& tf) {
 __host__ __device__ inline uint64_t tile_first_threads(const TileFirstJob& tf) {
   return !tf.ntiles ? 0 : (tile_first_search(tf) ? tf.ntiles : tf.npos + 1);
 }
-__device__ __forceinline__ bool run_tile_first(const TileFirstJob& tf, uint32_t first_block) {
-  if (blockIdx.x < first_block) return false;
+__device__ __forceinline__ bool run_tile_first(const TileFirstJob& tf, uint32_t first_block,
+                                               uint32_t bid) {
+  if (bid < first_block) return false;
   const uint32_t tfb = (uint32_t)((tile_first_threads(tf) + 255) / 256);
-  if (blockIdx.x - first_block >= tfb) {
-    const uint64_t z0 = (uint64_t)(blockIdx.x - first_block - tfb) * kZeroBlockWords;
+  if (bid - first_block >= tfb) {
+    const uint64_t z0 = (uint64_t)(bid - first_block - tfb) * kZeroBlockWords;
     for (uint64_t i = z0 + threadIdx.x; i < z0 + kZeroBlockWords && i < tf.zero_words; i += 256)
       tf.zero[i] = 0;
     return true;
   }
   if (tile_first_search(tf)) {
-    const uint64_t t = (uint64_t)(blockIdx.x - first_block) * blockDim.x + threadIdx.x;
+    const uint64_t t = (uint64_t)(bid - first_block) * blockDim.x + threadIdx.x;
     if (t >= tf.ntiles) return true;
     // first m in [0, npos] with pos[m] >= t*T (npos + 1: none)
     const uint64_t x = t * tf.T;
@@ -295,7 +310,7 @@ __device__ __forceinline__ bool run_tile_first(const TileFirstJob& tf, uint32_t 
     if (tf.outpos) tf.outpos[t] = lo <= tf.npos ? tf.pos[lo] : ~0ull;
     return true;
   }
-  const uint64_t m = (uint64_t)(blockIdx.x - first_block) * blockDim.x + threadIdx.x;
+  const uint64_t m = (uint64_t)(bid - first_block) * blockDim.x + threadIdx.x;
   if (m > tf.npos) return true;
   const uint64_t pm = tf.pos[m];
   const uint64_t lo = m == 0 ? 0 : tf.pos[m - 1] / tf.T + 1;  // first tile starting past pos[m-1]
@@ -313,6 +328,9 @@ __device__ __forceinline__ bool run_tile_first(const TileFirstJob& tf, uint32_t 
     }
   }
   return true;
+}
+__device__ __forceinline__ bool run_tile_first(const TileFirstJob& tf, uint32_t first_block) {
+  return run_tile_first(tf, first_block, blockIdx.x);
 }
 inline unsigned tile_first_blocks(const TileFirstJob& tf) {
   return (unsigned)((tile_first_threads(tf) + 255) / 256 +

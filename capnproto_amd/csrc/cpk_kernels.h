@@ -129,7 +129,6 @@ struct UnpackArgs {
   uint32_t* tegs;               // ntiles: each tile's guessed entry
   const uint64_t* texcl;        // ntiles: words of the tile's first message before the tile
   const uint32_t* gate;         // non-zero: the resolve launch could not place every tile
-  unsigned int* ticket;         // tile tickets of a launch whose tiles wait (zeroed), else NULL
 };
 constexpr uint64_t kUnpackFuseMsgs = 256;
 

@@ -78,6 +78,38 @@ __global__ __launch_bounds__(256) void copy_kernel(const cu32x4* __restrict__ sr
   for (; i < end; i += stride) dst[i] = src[i];
 }
 
+// The same copy through CDNA4's LDS-DMA: each wave stages U KiB of its block's contiguous share
+// with global_load_lds_dwordx4 (no VGPR destination: the bytes land in the wave's LDS, lane-linear),
+// waits for them, and stores them from LDS.  (The bench's copy ceiling: MI355X_MICROARCH.md
+// measures LDS-DMA streams at 6.4-6.8 TB/s chip-wide, read side.)
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void copy_lds_kernel(const cu32x4* __restrict__ src,
+                                                       cu32x4* __restrict__ dst, uint64_t n16) {
+  __shared__ __attribute__((aligned(16))) cu32x4 buf[4][U * 64];
+  const int w = (int)(threadIdx.x >> 6), l = (int)(threadIdx.x & 63);
+  const uint64_t per = (n16 + gridDim.x - 1) / gridDim.x;
+  const uint64_t b0 = (uint64_t)blockIdx.x * per;
+  const uint64_t end = b0 + per < n16 ? b0 + per : n16;
+  constexpr uint64_t kChunk = (uint64_t)U * 64;
+  uint64_t i = b0 + (uint64_t)w * kChunk;
+  for (; i + kChunk <= end; i += 4 * kChunk) {
+#pragma unroll
+    for (int k = 0; k < U; k++)
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(src + i + 64 * k + l),
+          (__attribute__((address_space(3))) void*)&buf[w][64 * k], 16, 0, NT ? 2 : 0);
+    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): the wave's DMA into its own LDS is done
+#pragma unroll
+    for (int k = 0; k < U; k++) {
+      const cu32x4 v = buf[w][64 * k + l];
+      if (NT) __builtin_nontemporal_store(v, dst + i + 64 * k + l);
+      else dst[i + 64 * k + l] = v;
+    }
+  }
+  // (one partial chunk per wave at most: plain copies)
+  for (uint64_t j = i + (uint64_t)l; j < end && j < i + kChunk; j += 64) dst[j] = src[j];
+}
+
 struct Flat {
   const uint8_t* packed;
   uint64_t nbytes;
@@ -807,12 +839,25 @@ hipError_t launch_copy(void* dst, const void* src, uint64_t nbytes, uint32_t blo
   if (nbytes == 0) return hipSuccess;
   if (((uintptr_t)dst | (uintptr_t)src | nbytes) & 15) return hipErrorInvalidValue;
   // blocks: low 24 bits the grid; bits 24-25 the loads in flight per lane (4, 8, 16), bit 26
-  // non-temporal loads and stores, bit 27 contiguous per-block shares instead of grid strides
+  // non-temporal loads and stores, bit 27 contiguous per-block shares instead of grid strides;
+  // bit 28: LDS-DMA staging (copy_lds_kernel, contiguous shares) of 2 / 4 / 8 KiB per wave
   const unsigned g = (blocks & 0xffffffu) ? (blocks & 0xffffffu) : 4096u;
   const auto* s16 = (const cu32x4*)src;
   auto* d16 = (cu32x4*)dst;
   const uint64_t n = nbytes / 16;
-  const unsigned form = (blocks >> 24) & 15u;
+  const unsigned form = (blocks >> 24) & 31u;
+  if (form & 16u) {
+    switch (form & 7u) {
+      case 0: copy_lds_kernel<2, false><<<g, 256, 0, stream>>>(s16, d16, n); break;
+      case 1: copy_lds_kernel<4, false><<<g, 256, 0, stream>>>(s16, d16, n); break;
+      case 2: copy_lds_kernel<8, false><<<g, 256, 0, stream>>>(s16, d16, n); break;
+      case 4: copy_lds_kernel<2, true><<<g, 256, 0, stream>>>(s16, d16, n); break;
+      case 5: copy_lds_kernel<4, true><<<g, 256, 0, stream>>>(s16, d16, n); break;
+      case 6: copy_lds_kernel<8, true><<<g, 256, 0, stream>>>(s16, d16, n); break;
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
 #define CPK_COPY_CASE(F, U, NT, C) \
   case F: copy_kernel<U, NT, C><<<g, 256, 0, stream>>>(s16, d16, n); break;
   switch (form) {

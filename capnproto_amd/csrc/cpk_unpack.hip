@@ -1573,6 +1573,16 @@ __device__ __forceinline__ void lean_special(const uint8_t* d, int p, uint64_t A
   run_jobs(a, job, d, A, (uint32_t)(kB + kPad));
 }
 
+// A record that ends its message exactly -- its last word the message's last, its last byte the
+// message's last -- is the reference's clean end (handle_record: kOK, the header launch's status
+// stands): the lean batch writes it like any other record.  Not when the call reports where each
+// message ends (in_end), nor for a raw run whose bytes leave the staged ones (handle_record writes
+// such a run whole: the next tile's run_tail skips runs that end a message).
+__device__ __forceinline__ bool clean_end(const UnpackArgs& a, bool words_end, bool bytes_end,
+                                          bool raw, uint32_t rb, uint32_t cnt) {
+  return words_end && bytes_end && !a.in_end && (!raw || rb + 8u * cnt + 4u <= (uint32_t)(kB + kPad));
+}
+
 // Lean expansion (mode 0; every message touching the tile in the window, accepted, fitting the
 // output; no empty message in the tile; at most kB/8 records per quarter tile).  Record lists
 // per quarter tile in LDS, one lane per record, 64 consecutive records per batch, coalesced
@@ -1697,7 +1707,8 @@ __device__ __forceinline__ void expand_lean(const UnpackArgs& a, uint64_t A, con
         if (mw0 + btot >= ctot || A + maxp + 2050 >= cend) {
           const uint32_t len = 1u + __popc(tag) + ((z || f) ? 1u : 0u) + (f ? 8u * cnt : 0u);
           wb = mw0 + o;
-          special = act && (wb + w >= ctot || A + p + len >= cend);
+          special = act && (wb + w >= ctot || A + p + len >= cend) &&
+                    !clean_end(a, wb + w == ctot, A + p + len == cend, f, rb, cnt);
         }
       } else {
         // message starts in the batch: the latest start at or before each record (key-max scan)
@@ -1710,7 +1721,8 @@ __device__ __forceinline__ void expand_lean(const UnpackArgs& a, uint64_t A, con
         wp = a.words + mbase + wb;
         const uint64_t mtot = shfl64(win.total, wl), mend = shfl64(win.end, wl);
         const uint32_t len = 1u + __popc(tag) + ((z || f) ? 1u : 0u) + (f ? 8u * cnt : 0u);
-        special = act && (wb + w >= mtot || A + p + len >= mend);
+        special = act && (wb + w >= mtot || A + p + len >= mend) &&
+                  !clean_end(a, wb + w == mtot, A + p + len == mend, f, rb, cnt);
       }
       const bool put = act && !special;
       if (put) {
@@ -1994,6 +2006,9 @@ unpack_tiles_kernel(UnpackArgs a) {
   __syncthreads();
   const uint64_t t = (uint64_t)blockIdx.x * 4 + wv;
   if (t >= a.ntiles) return;
+  // the expansion launch of a split decode whose resolve launch could not place every tile runs
+  // the one-pass look-back instead (wave-uniform)
+  const bool gated = PHASE == 2 && uniform32(*(const volatile uint32_t*)a.gate) != 0;
   if (a.debug_skip & 512) return;  // diagnostic: the launch alone
   // batches of very long messages (whose look-backs reach back to the previous occupancy round):
   // the phases later tiles wait on (chain 0, the entry, the descriptors) ahead of other waves'
@@ -2004,9 +2019,6 @@ unpack_tiles_kernel(UnpackArgs a) {
   if (PHASE != 2)
     for (uint64_t i = t + a.ntiles * (uint64_t)l; i < a.hdr_nblocks; i += 64 * a.ntiles)
       a.hdr_desc[i] = 0;
-  // the expansion launch of a split decode whose resolve launch could not place every tile runs the
-  // one-pass look-back instead (wave-uniform)
-  const bool gated = PHASE == 2 && uniform32(*(const volatile uint32_t*)a.gate) != 0;
   uint8_t* const d = lds_data[wv] + kPre;
   uint64_t* const aux = lds_aux[wv];
   const uint64_t P = a.nbytes;
@@ -2361,9 +2373,7 @@ __global__ __launch_bounds__(256) void unpack_resolve_kernel(ResolveArgs r) {
   const int wv = (int)uniform32(threadIdx.x >> 6);
   // groups in ticket order: a group waits only on groups whose workgroups took their tickets
   // before its own (running or done), whatever else shares the device
-  if (threadIdx.x == 0) s_ticket = atomicAdd(r.ticket, 1u);
-  __syncthreads();
-  const uint64_t g = (uint64_t)uniform32(s_ticket) * 4 + (uint64_t)wv;
+  const uint64_t g = (uint64_t)wg_ticket(r.ticket, &s_ticket) * 4 + (uint64_t)wv;
   const uint64_t ngroups = resolve_groups(r.ntiles);
   if (g >= ngroups) return;
   const uint64_t P = r.nbytes;
