@@ -18,7 +18,7 @@ for e in ${ENVS:--}; do
   for c in ${CFGS-c2 c3 c4 c5}; do
     if [ "$e" = "-" ]; then EV=""; else EV="$e"; fi
     env $EV timeout -k 10 300 python bench.py --config $c --sub none --steps ${STEPS:-10} --warmup 2 \
-      --no-split --no-host --no-cpu-baseline > gpurun_out/${TAG}_${c}_${e//=/_}.json \
+      --no-split --no-host --no-cpu-baseline ${AB:+--ab} > gpurun_out/${TAG}_${c}_${e//=/_}.json \
       2> gpurun_out/${TAG}_${c}_${e//=/_}.err || { echo "bench $c $e failed"; tail -20 gpurun_out/${TAG}_${c}_${e//=/_}.err; exit 1; }
     python - gpurun_out/${TAG}_${c}_${e//=/_}.json "$e" <<'PY'
 import json, sys
@@ -31,6 +31,7 @@ PY
 done
 cd /tmp
 for c in ${PROF-c2}; do
+  [ "$c" = none ] && continue
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/${TAG}_prof_$c" -o run \
     -- python3 "$R/bench.py" --config $c --sub none --steps 10 --warmup 2 --no-cpu-baseline --no-host --no-split \
     > "$R/gpurun_out/${TAG}_prof_$c.log" 2>&1 || { echo "rocprof $c failed"; tail -20 "$R/gpurun_out/${TAG}_prof_$c.log"; exit 1; }
