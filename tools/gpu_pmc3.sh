@@ -21,3 +21,5 @@ for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU S
 done
 python3 "$R/tools/pmc_summary.py" "$R/gpurun_out" "$TAG" "$CFG" > "$R/gpurun_out/${TAG}_summary.txt" 2>&1
 cat "$R/gpurun_out/${TAG}_summary.txt"
+# (the passes' raw traces stay on the box: gpurun copies back at most 64 MiB)
+[ -n "$KEEP_RAW" ] || rm -rf "$R/gpurun_out/${TAG}"_p[0-9]
