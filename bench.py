@@ -62,10 +62,9 @@ CONFIGS = {
 }
 DEBUG_ENV = ("CPK_DEBUG_SKIP", "CPK_STAMPS")
 # kernel-selection knobs (env): a headline number comes from the default kernels unless --ab is
-# given.  The library's measured alternatives: CPK_UNPACK_SPLIT=1 the split message
-# decode, CPK_AB_PACK_DMA=1 the pack tiles' words through LDS-DMA.  Every CPK_* variable that is
-# set is recorded in the result's "kernels.knobs".
-KERNEL_ENV: tuple = ("CPK_UNPACK_SPLIT", "CPK_AB_PACK_DMA")
+# given.  The library's measured alternative: CPK_UNPACK_SPLIT=1 the split message
+# decode.  Every CPK_* variable that is set is recorded in the result's "kernels.knobs".
+KERNEL_ENV: tuple = ("CPK_UNPACK_SPLIT",)
 
 
 def parse():

@@ -297,8 +297,9 @@ struct TimedLaunch {
 // tile is always resident; two such launches side by side could each fill the XCDs the other's
 // next workgroup needs (forward progress).  Kernels of other libraries never wait on
 // a codec tile: they only delay it.  So a call that launches waiting kernels (DeviceTurn::waiting)
-// records the device's order event behind them, and a call on another stream waits for it first;
-// DeviceTurn holds the device's order lock for the whole call, so the event covers the launches.
+// records the device's order event behind them, and a call on another stream waits (on the host)
+// until they are done before it launches; DeviceTurn holds the device's order lock for the whole
+// call, so the event covers the launches.
 struct DeviceOrder {
   std::recursive_mutex m;
   hipStream_t last = nullptr;
@@ -347,10 +348,16 @@ cpk_status order_streams(cpk_ctx* ctx, hipStream_t s) {
   }
   ctx->used = true;
   ctx->last_stream = s;
-  // the device's last waiting launches, when on another stream (of any context)
+  // the device's last waiting launches, when on another stream (of any context): waited for on
+  // the host -- a stream-side wait on another stream's event puts a barrier into a hardware queue
+  // the two streams may share, and the pipelined host path (bench.py host_inclusive: one stream
+  // per chunk, each its own context) then ran its copies one after another (C2 host-inclusive
+  // 24.9 -> 13.3 GiB/s)
   DeviceOrder& o = device_order(ctx->device);
-  if (o.has && o.last != s && !capturing(s) && hipStreamWaitEvent(s, o.ev, 0) != hipSuccess)
-    return CPK_ERR_HIP;
+  if (o.has && o.last != s && !capturing(s)) {
+    if (hipEventSynchronize(o.ev) != hipSuccess) return CPK_ERR_HIP;
+    o.has = false;
+  }
   return CPK_OK;
 }
 

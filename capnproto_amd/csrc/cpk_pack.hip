@@ -297,7 +297,7 @@ struct TileLoads {
 // a branch, so uniform values come through scalar loads and lane-varying guards are clamped
 // addresses).
 __device__ __forceinline__ void tile_loads(const PackTileArgs& a, uint64_t T, int w, int l,
-                                           TileLoads& L, bool words = true) {
+                                           TileLoads& L) {
   const uint64_t N = a.nwords;
   const uint64_t nbitw = (N + 63) >> 6;
   const uint64_t tbase = T * kTW;
@@ -309,7 +309,6 @@ __device__ __forceinline__ void tile_loads(const PackTileArgs& a, uint64_t T, in
   // tile goes to the direct kernel)
 #pragma unroll
   for (int i = 0; i < kK / 2; i++) {
-    if (!words) break;
     const uint64_t j = w0 + 2 * i;
     const u32x4 v = *(const u32x4*)(a.words + (j + 2 <= N ? j : N - 2));
     const bool k0 = j < N, k1 = j + 1 < N, sh = j + 2 > N;  // sh: the pair ending at word N - 1
@@ -332,11 +331,6 @@ __device__ __forceinline__ void tile_loads(const PackTileArgs& a, uint64_t T, in
   L.p00 = (a.pos ? a.pos : a.words)[a.pos && pi <= a.npos ? pi : 0];
 }
 
-// DMA: a full wave's 4 KiB of words come in through LDS-DMA (global_load_lds_dwordx4, lane l
-// loading 16-byte pieces l, l + 64, ... of the wave's share: coalesced, no VGPR destination) into
-// the staging slot, and each lane reads its 8 consecutive words back from there; the slot is
-// zeroed for the emission after barrier A, once every wave has read its words.
-template <bool DMA>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void
 pack_tile_kernel(PackTileArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t stg[kSlotDw];
@@ -380,40 +374,17 @@ pack_tile_kernel(PackTileArgs a) {
     __syncthreads();  // (the bitmap's atomics are done at the L2; no wave has read it yet)
   }
   TileLoads cur;
+  tile_loads(a, T, w, l, cur);
+  for (int i = tid; i < kSlotDw / 4; i += 64 * kWv) ((u32x4*)stg)[i] = (u32x4){0, 0, 0, 0};
   const uint64_t tbase = T * kTW;
   const uint64_t tend = tbase + kTW < N ? tbase + kTW : N;
   const uint64_t wbase = tbase + (uint64_t)kWW * w;
-  const bool dma = DMA && wbase + kWW <= N;  // wave-uniform
-  static_assert(kSlotDw * 4 >= kTW * 8, "a tile's words fit the staging slot");
-  if (dma) {
-    const u32x4* const src = (const u32x4*)(a.words + wbase) + l;
-#pragma unroll
-    for (int k = 0; k < kWW * 8 / 1024; k++)
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + 64 * k),
-                                       (__attribute__((address_space(3))) void*)(stg + 1024 * w + 256 * k),
-                                       16, 0, 0);
-  }
-  tile_loads(a, T, w, l, cur, !dma);
-  if (!DMA)
-    for (int i = tid; i < kSlotDw / 4; i += 64 * kWv) ((u32x4*)stg)[i] = (u32x4){0, 0, 0, 0};
   const int nvw = wbase >= N ? 0 : (int)((N - wbase) < (uint64_t)kWW ? (N - wbase) : kWW);
   uint32_t xlo[kK], xhi[kK];
-  if (dma) {
-    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): the wave's DMA into the slot is done
 #pragma unroll
-    for (int i = 0; i < kK / 2; i++) {
-      const u32x4 v = ((const u32x4*)stg)[256 * w + 4 * l + i];
-      xlo[2 * i] = v.x;
-      xhi[2 * i] = v.y;
-      xlo[2 * i + 1] = v.z;
-      xhi[2 * i + 1] = v.w;
-    }
-  } else {
-#pragma unroll
-    for (int k = 0; k < kK; k++) {
-      xlo[k] = cur.xlo[k];
-      xhi[k] = cur.xhi[k];
-    }
+  for (int k = 0; k < kK; k++) {
+    xlo[k] = cur.xlo[k];
+    xhi[k] = cur.xhi[k];
   }
   const uint64_t cbi = (wbase >> 6) + (uint64_t)(l >> 3);
   const uint64_t xw0 = cur.xw0, nb0 = cur.nb0;
@@ -496,8 +467,6 @@ pack_tile_kernel(PackTileArgs a) {
     next_sync = tend >= N || readlane32(ns ? 1u : 0u, 63) != 0;
   }
   lds_barrier();  // ---- A: wave summaries ---------------------------------------------
-  if (DMA)  // (every wave has its words: the slot is free; barrier B orders this before the emission)
-    for (int i = tid; i < kSlotDw / 4; i += 64 * kWv) ((u32x4*)stg)[i] = (u32x4){0, 0, 0, 0};
   // the chunk-start bits are zero at rest: this tile clears what only it reads (its bitmap words;
   // the bit of its successor's first word, read here and nowhere else)
   if ((l & 7) == 0 && cbi < nbitw && cbw != 0) a.chunk_bits[cbi] = (uint64_t)opaque_zero();
@@ -997,11 +966,7 @@ __global__ __launch_bounds__(256) void pack_place_kernel(PackTileArgs a) {
 hipError_t launch_pack_tiles(const PackTileArgs& a, hipStream_t stream) {
   if (a.ntiles == 0) return hipSuccess;
   if (a.ntiles >= (1ull << 31)) return hipErrorInvalidValue;
-  static const bool dma = getenv("CPK_AB_PACK_DMA") && atoi(getenv("CPK_AB_PACK_DMA")) != 0;
-  if (dma)
-    pack_tile_kernel<true><<<(unsigned)a.ntiles, 256, 0, stream>>>(a);
-  else
-    pack_tile_kernel<false><<<(unsigned)a.ntiles, 256, 0, stream>>>(a);
+  pack_tile_kernel<<<(unsigned)a.ntiles, 256, 0, stream>>>(a);
   return hipGetLastError();
 }
 

@@ -91,14 +91,18 @@ __global__ __launch_bounds__(256) void copy_lds_kernel(const cu32x4* __restrict_
   const uint64_t b0 = (uint64_t)blockIdx.x * per;
   const uint64_t end = b0 + per < n16 ? b0 + per : n16;
   constexpr uint64_t kChunk = (uint64_t)U * 64;
-  uint64_t i = b0 + (uint64_t)w * kChunk;
-  for (; i + kChunk <= end; i += 4 * kChunk) {
+  // (every wave of the block the same trip count: the barrier below is block-wide)
+  uint64_t base = b0;
+  for (; base + 4 * kChunk <= end; base += 4 * kChunk) {
+    const uint64_t i = base + (uint64_t)w * kChunk;
 #pragma unroll
     for (int k = 0; k < U; k++)
       __builtin_amdgcn_global_load_lds(
           (const __attribute__((address_space(1))) void*)(src + i + 64 * k + l),
           (__attribute__((address_space(3))) void*)&buf[w][64 * k], 16, 0, NT ? 2 : 0);
-    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): the wave's DMA into its own LDS is done
+    // LDS-DMA bytes are ordered for a ds_read by the issuing wave's vmcnt and then a barrier
+    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
+    __builtin_amdgcn_s_barrier();
 #pragma unroll
     for (int k = 0; k < U; k++) {
       const cu32x4 v = buf[w][64 * k + l];
@@ -106,8 +110,8 @@ __global__ __launch_bounds__(256) void copy_lds_kernel(const cu32x4* __restrict_
       else dst[i + 64 * k + l] = v;
     }
   }
-  // (one partial chunk per wave at most: plain copies)
-  for (uint64_t j = i + (uint64_t)l; j < end && j < i + kChunk; j += 64) dst[j] = src[j];
+  // (less than one round of chunks left: plain copies)
+  for (uint64_t j = base + threadIdx.x; j < end; j += 256) dst[j] = src[j];
 }
 
 struct Flat {

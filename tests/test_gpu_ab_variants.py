@@ -5,10 +5,7 @@ direction in a child process with the variable set:
 * CPK_UNPACK_SPLIT=1 -- the split message decode (index, resolve and expand launches;
   cpk_unpack.hip "Split decode") through tests/test_gpu_unpack.py: reference fixtures, error
   cases, locked chains that gate the expansion launch onto the look-back, the UINT_MAX segment
-  count;
-* CPK_AB_PACK_DMA=1 -- the pack tiles' words staged through LDS-DMA (cpk_pack.hip
-  pack_tile_kernel<true>) through tests/test_gpu_pack.py: oracle parity, chunk edges, the byte
-  arena, concurrent contexts."""
+  count."""
 import os
 import subprocess
 import sys
@@ -19,8 +16,7 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-@pytest.mark.parametrize("knob,suite", [("CPK_UNPACK_SPLIT", "test_gpu_unpack.py"),
-                                        ("CPK_AB_PACK_DMA", "test_gpu_pack.py")])
+@pytest.mark.parametrize("knob,suite", [("CPK_UNPACK_SPLIT", "test_gpu_unpack.py")])
 def test_suite_through_variant(knob, suite):
     env = dict(os.environ, **{knob: "1"})
     r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider",
