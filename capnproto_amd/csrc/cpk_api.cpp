@@ -823,7 +823,8 @@ cpk_status cpk_reserve(cpk_ctx* ctx, uint64_t max_words, uint64_t max_packed_byt
   size_t need = pack_scratch_bytes(max_words, pt);
   const uint64_t ut = (max_packed_bytes + cpk::kUnpackTileBytes - 1) / cpk::kUnpackTileBytes;
   // (the flat stream decode's second-candidate descriptors included)
-  const size_t un = carve_unpack(nullptr, ut, max_items, true).total + 64;
+  // (the flat decode's second descriptors and, when the split decode is on, its bits and prefixes)
+  const size_t un = carve_unpack(nullptr, ut, max_items, true, unpack_split_enabled()).total + 64;
   if (un > need) need = un;
   cpk_status st = ensure(&ctx->scratch, &ctx->scratch_size, need);
   if (st != CPK_OK) return st;

@@ -78,10 +78,10 @@ typedef struct cpk_ctx cpk_ctx;
 /* One context per (device, host thread).  Scratch grows on demand; cpk_reserve pre-sizes it so
  * that later calls allocate nothing (required before capturing calls into a hipGraph).  Device
  * scratch for a batch of W words in T = ceil(W / 2048) pack tiles: a byte arena of 4 KiB per
- * pack tile (2 W bytes, at most 8 GiB), ~41 B per pack tile and 1 bit per word; for unpack ~552 B
- * per 4 KiB of packed input (a message batch of more than one tile: chain 0's record-start bits,
- * 512 B) and a few tens of bytes per message; for the stream split, 8 B per output word (the
- * record-head map). */
+ * pack tile (2 W bytes, at most 8 GiB), ~41 B per pack tile and 1 bit per word; for unpack ~44 B
+ * per 4 KiB of packed input (~570 B with the split message decode, CPK_UNPACK_SPLIT=1: chain 0's
+ * record-start bits, 512 B) and a few tens of bytes per message; for the stream split, 8 B per
+ * output word (the record-head map). */
 cpk_status cpk_init(int device, cpk_ctx** out);
 cpk_status cpk_destroy(cpk_ctx* ctx);
 cpk_status cpk_reserve(cpk_ctx* ctx, uint64_t max_words, uint64_t max_packed_bytes,
