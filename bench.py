@@ -62,9 +62,10 @@ CONFIGS = {
 }
 DEBUG_ENV = ("CPK_DEBUG_SKIP", "CPK_STAMPS")
 # kernel-selection knobs (env): a headline number comes from the default kernels unless --ab is
-# given.  The library's measured alternative: CPK_UNPACK_SPLIT=1 the split message
-# decode.  Every CPK_* variable that is set is recorded in the result's "kernels.knobs".
-KERNEL_ENV: tuple = ("CPK_UNPACK_SPLIT",)
+# given.  The library's measured alternatives: CPK_UNPACK_SPLIT=1 the split
+# message decode, CPK_FLAT_SPLIT=0 the one-pass flat decode of the stream split.  Every CPK_*
+# variable that is set is recorded in the result's "kernels.knobs".
+KERNEL_ENV: tuple = ("CPK_UNPACK_SPLIT", "CPK_FLAT_SPLIT")
 
 
 def parse():

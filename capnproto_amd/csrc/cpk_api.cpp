@@ -590,6 +590,12 @@ UnpackScratch carve_unpack(void* base, uint64_t ntiles, uint64_t n, bool flat = 
 // The split message decode (index, resolve, expand launches: cpk_unpack.hip) for message batches
 // of more than one tile, with CPK_UNPACK_SPLIT=1 (A/B; measured slower than the one-pass kernel,
 // DESIGN.md 3.2).
+// The stream split's flat decode in two launches (cpk_unpack.hip, FLAT with PHASE 1 / 2): the
+// default; CPK_FLAT_SPLIT=0 selects the one-pass flat decode (the measured alternative).
+bool flat_split_enabled() {
+  static const bool v = !(getenv("CPK_FLAT_SPLIT") && atoi(getenv("CPK_FLAT_SPLIT")) == 0);
+  return v;
+}
 bool unpack_split_enabled() {
   static const bool v = getenv("CPK_UNPACK_SPLIT") && atoi(getenv("CPK_UNPACK_SPLIT")) != 0;
   return v;
@@ -615,10 +621,13 @@ cpk_status unpack_common(cpk_ctx* ctx, uint32_t mode, const uint8_t* d_packed, u
   // stream readers' message ends, skips and the flat decode keep the one-pass kernel)
   const bool split = mode == 0 && ntiles > 1 && !flat && !d_in_end && !store_free && d_words &&
                      unpack_split_enabled();
-  UnpackScratch probe = carve_unpack(nullptr, ntiles, n, flat, split);
+  // the flat decode in two launches (index, then decode over published descriptors; the index
+  // launch leaves the base chain's record-start bits for the second)
+  const bool flat_split = flat && ntiles > 1 && flat_split_enabled();
+  UnpackScratch probe = carve_unpack(nullptr, ntiles, n, flat, split || flat_split);
   cpk_status st = ensure(&ctx->scratch, &ctx->scratch_size, probe.total + 64);
   if (st != CPK_OK) return st;
-  UnpackScratch s = carve_unpack(ctx->scratch, ntiles, n, flat, split);
+  UnpackScratch s = carve_unpack(ctx->scratch, ntiles, n, flat, split || flat_split);
   const uint64_t* word_off = d_word_off_in;
   hipError_t e = hipSuccess;
   cpk::TileFirstJob tf;  // each tile's first message, in the same launch as the headers
@@ -725,7 +734,9 @@ cpk_status unpack_common(cpk_ctx* ctx, uint32_t mode, const uint8_t* d_packed, u
     tl.done();
     return CPK_OK;
   }
-  for (int stage = cpk::kUnpackTiles; stage <= cpk::kUnpackTiles; stage++) {
+  const int first_stage = flat_split ? cpk::kUnpackIndex : cpk::kUnpackTiles;
+  const int last_stage = flat_split ? cpk::kUnpackExpand : cpk::kUnpackTiles;
+  for (int stage = first_stage; stage <= last_stage; stage++) {
     TimedLaunch tk(ctx, 2 + stage, stream);
     e = cpk::launch_unpack_stage(stage, a, stream);
     tk.done();
@@ -824,7 +835,9 @@ cpk_status cpk_reserve(cpk_ctx* ctx, uint64_t max_words, uint64_t max_packed_byt
   const uint64_t ut = (max_packed_bytes + cpk::kUnpackTileBytes - 1) / cpk::kUnpackTileBytes;
   // (the flat stream decode's second-candidate descriptors included)
   // (the flat decode's second descriptors and, when the split decode is on, its bits and prefixes)
-  const size_t un = carve_unpack(nullptr, ut, max_items, true, unpack_split_enabled()).total + 64;
+  const size_t un =
+      carve_unpack(nullptr, ut, max_items, true, unpack_split_enabled() || flat_split_enabled())
+          .total + 64;
   if (un > need) need = un;
   cpk_status st = ensure(&ctx->scratch, &ctx->scratch_size, need);
   if (st != CPK_OK) return st;

@@ -1282,6 +1282,10 @@ __device__ bool flat_wait(const uint64_t* p, uint64_t mask, uint64_t want, uint3
   return true;
 }
 
+// PUB: every tile's AGG, second candidate and chain-0 exit are published before the launch (the
+// split flat decode's second launch): a window's three reads go out together, the last two as
+// plain loads (nothing changes them during the launch), one round trip per window instead of two.
+template <bool PUB>
 __device__ uint64_t lookback_flat_scan(const UnpackArgs& a, uint64_t t, uint32_t* xprev) {
   const int l = lane_id();
   uint32_t spins = 0;
@@ -1306,6 +1310,12 @@ __device__ uint64_t lookback_flat_scan(const UnpackArgs& a, uint64_t t, uint32_t
       const int64_t u = base - l;
       // before tile 0: an inclusive zero whose exit enters tile 0 at byte 0
       const uint64_t dv = u >= 0 ? load_agent(a.desc + u) : (kDescIncl | kOkBit);
+      uint64_t d2p = kD2None;
+      uint32_t xqp = 0;
+      if (PUB) {
+        d2p = u >= 0 ? a.desc2[u] : kD2None;
+        xqp = u >= 1 ? a.x0p[u - 1] : 0u;
+      }
       const uint64_t stt = dv & kDescFlags;
       const uint64_t ib = ballot(stt == kDescIncl);
       const int k = ib ? lowest_bit(ib) : 64;
@@ -1316,8 +1326,8 @@ __device__ uint64_t lookback_flat_scan(const UnpackArgs& a, uint64_t t, uint32_t
         continue;
       }
       const bool agg = l < k;  // (AGG: published, not INCL)
-      const uint64_t d2 = agg ? load_agent(a.desc2 + u) : kD2None;
-      const uint32_t xq = agg ? (load_agent32(a.x0p + u - 1) & 0x7fffffffu) : 0u;
+      const uint64_t d2 = agg ? (PUB ? d2p : load_agent(a.desc2 + u)) : kD2None;
+      const uint32_t xq = agg ? ((PUB ? xqp : load_agent32(a.x0p + u - 1)) & 0x7fffffffu) : 0u;
       const uint64_t n2 = ballot(agg && d2 == 0);
       if (n2) {
         CPK_DIAG_ONLY(diag_add(27, 1));
@@ -1973,7 +1983,9 @@ __device__ __forceinline__ void expand_records(const UnpackArgs& a, uint64_t A, 
 template <bool FLAT, int PHASE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CPK_UNPACK_WPE))) void
 unpack_tiles_kernel(UnpackArgs a) {
-  static_assert(!FLAT || PHASE == 0, "the flat stream decode is one pass");
+  // (FLAT with PHASE 1 / 2: the split flat decode -- the index launch publishes every tile's
+  // chain-0 exit, AGG and second candidate and leaves; the decode launch re-stages, recomputes
+  // chain 0 and looks back over descriptors that are all published)
   __shared__ __attribute__((aligned(16))) uint8_t lds_data[4][kPre + kB + kPad];
   // per wave 1 KiB: message starts while they are found, then chain 0 and the walked starts
   // while the entry's chain is traced, then the record list of a quarter tile
@@ -2011,7 +2023,7 @@ unpack_tiles_kernel(UnpackArgs a) {
   if (t >= a.ntiles) return;
   // the expansion launch of a split decode whose resolve launch could not place every tile runs
   // the one-pass look-back instead (wave-uniform)
-  const bool gated = PHASE == 2 && uniform32(*(const volatile uint32_t*)a.gate) != 0;
+  const bool gated = PHASE == 2 && !FLAT && uniform32(*(const volatile uint32_t*)a.gate) != 0;
   if (a.debug_skip & 512) return;  // diagnostic: the launch alone
   // batches of very long messages (whose look-backs reach back to the previous occupancy round):
   // the phases later tiles wait on (chain 0, the entry, the descriptors) ahead of other waves'
@@ -2050,11 +2062,18 @@ unpack_tiles_kernel(UnpackArgs a) {
   uint32_t Eg = 0, x0 = 0;
   bool settled = true;
   int q0 = 0;  // where the tile's base chain starts
-  if constexpr (PHASE == 2) {
+  if constexpr (PHASE == 2 && !FLAT) {
     // chain 0 as the index launch left it (its run records are rebuilt only where needed)
     tm0 = a.tbits[t * 64 + l];
     Eg = t > 0 ? uniform32(a.tegs[t]) : 0u;
     x0 = uniform32(a.x0p[t]) & 0x7fffffffu;
+  } else if constexpr (PHASE == 2 && FLAT) {
+    // the split flat decode: the base chain as the index launch left it (from byte 0, or from
+    // the raw-record head that replaced it), its run records from the staged bytes
+    tm0 = a.tbits[t * 64 + l];
+    q0 = (int)uniform32(a.tegs[t]);
+    x0 = uniform32(a.x0p[t]) & 0x7fffffffu;
+    runm = run_bytes(d, st.s);
   } else {
   // ---- chain 0 (entered at the tile's first byte): speculative walks, then the lane fixed point
   uint64_t chain = 0;
@@ -2130,11 +2149,11 @@ unpack_tiles_kernel(UnpackArgs a) {
       }
     }
   }
-  if (l == 0) store_agent32(a.x0p + t, 0x80000000u | x0);
+  if (l == 0 && !(FLAT && PHASE == 2)) store_agent32(a.x0p + t, 0x80000000u | x0);
   if constexpr (PHASE == 1) {
-    // the expansion launch's chain 0 (coalesced: 512 bytes per tile)
+    // the expansion launch's chain 0 (coalesced: 512 bytes per tile) and where it starts
     a.tbits[t * 64 + l] = tm0;
-    if (l == 0) a.tegs[t] = Eg;
+    if (l == 0) a.tegs[t] = FLAT ? (uint32_t)q0 : Eg;
   }
   }
   CPK_DIAG_ONLY(ck[2] = ck[3] = ck[4] = ck[5] = clock64(); wk[2] = wk[3] = wk[4] = wk[5] = wall_clock64());
@@ -2254,17 +2273,21 @@ unpack_tiles_kernel(UnpackArgs a) {
   } else {
     // optimistic entry: where the predecessor's chain 0 leads (a tile with a message start
     // publishes its descriptor already, so it goes straight to the look-back)
-    const uint32_t xp = has_start ? 0u : wait_nonzero32(a.x0p + t - 1, a.err) & 0x7fffffffu;
+    // (the split flat decode's second launch: published by the index launch)
+    const uint32_t xp = has_start ? 0u
+                        : (PHASE == 2 ? uniform32(a.x0p[t - 1])
+                                      : wait_nonzero32(a.x0p + t - 1, a.err)) & 0x7fffffffu;
     CPK_DIAG_ONLY(ck[3] = ck[4] = ck[5] = clock64(); wk[3] = wk[4] = wk[5] = wall_clock64());
     const uint32_t Eopt = has_start ? ~0u : entry_from_exit(xp, fms);
     uint32_t xE = x0;
     uint64_t runs = runm;
+    uint64_t w = 0;
+    if (PHASE != 2) {  // (the split decode's second launch: the index launch published these)
     if (has_start) {
     } else if (Eopt != (uint32_t)q0 && Eopt < fms)
       tm = enter_chain(d, aux, st, tm0, (int)Eopt, (int)fms, x0, &xE, &runs);
     else if (Eopt >= fms)
       tm = clip_below(tm0, fms, st.s, &xE);
-    uint64_t w = 0;
     if (!has_start) {
       w = readlane32(wave_incl_sum32(mask_words(d, st.s, tm, runs)), 63);
       if (l == 0) store_agent(a.desc + t, make_desc(kDescAgg, xE, x0, w));
@@ -2293,16 +2316,19 @@ unpack_tiles_kernel(UnpackArgs a) {
       }
       if (l == 0) store_agent(a.desc2 + t, d2);
     }
+    }
+    if constexpr (PHASE == 1) return;  // the split decode's index launch: published, done
     uint32_t xprev = xp;
     CPK_DIAG_ONLY(ck[4] = clock64(); wk[4] = wall_clock64());
     if (!(a.debug_skip & 8)) {
-      excl = lookback_flat_scan(a, t, &xprev);
+      excl = lookback_flat_scan<PHASE == 2>(a, t, &xprev);
     }
     CPK_DIAG_ONLY(ck[5] = clock64(); wk[5] = wall_clock64());
     const uint32_t E = entry_from_exit(xprev, fms);
     CPK_DIAG_ONLY(diag_add(9, E != Eopt); diag_add(10, Eopt > 0 && Eopt < fms));
-    if (E != Eopt) {
-      // the predecessor's chain did not lead where its chain 0 does
+    if (PHASE == 2 || E != Eopt) {
+      // the predecessor's chain did not lead where its chain 0 does (or, in the split decode's
+      // second launch, the entry's chain is traced here for the first time)
       runs = runm;
       xE = x0;
       if (E != (uint32_t)q0 && E < fms)
@@ -2560,7 +2586,11 @@ hipError_t launch_unpack_resolve(const ResolveArgs& r, hipStream_t stream) {
 hipError_t launch_unpack_stage(int stage, const UnpackArgs& a, hipStream_t stream) {
   if (a.ntiles == 0) return hipSuccess;
   const dim3 grid((unsigned)((a.ntiles + 3) / 4));
-  if (stage == kUnpackIndex)
+  if (stage == kUnpackIndex && a.desc2)
+    hipLaunchKernelGGL((unpack_tiles_kernel<true, 1>), grid, dim3(256), 0, stream, a);
+  else if (stage == kUnpackExpand && a.desc2)
+    hipLaunchKernelGGL((unpack_tiles_kernel<true, 2>), grid, dim3(256), 0, stream, a);
+  else if (stage == kUnpackIndex)
     hipLaunchKernelGGL((unpack_tiles_kernel<false, 1>), grid, dim3(256), 0, stream, a);
   else if (stage == kUnpackExpand)
     hipLaunchKernelGGL((unpack_tiles_kernel<false, 2>), grid, dim3(256), 0, stream, a);
