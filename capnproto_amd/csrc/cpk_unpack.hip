@@ -1821,8 +1821,13 @@ __device__ __forceinline__ void run_tail(const UnpackArgs& a, uint64_t A, const 
 // messages).  Then no record can end or break its message, and the record batches need none of
 // expand_lean's per-record message logic: one wave-uniform word pointer, one store per record, the
 // runs' other words by the wave.  (Same stores as expand_lean for such a tile.)
-__device__ __forceinline__ void expand_simple(const UnpackArgs& a, const uint8_t* d, uint64_t* aux,
-                                              const uint64_t* dep_tab, uint64_t tm, uint64_t* wp) {
+// FLAT (the split flat decode): each record's packed byte goes to the record-head map too, and a
+// raw run leaving the staged bytes is written whole here (its far words from global memory: the
+// flat decode has no run_tail).
+template <bool FLAT>
+__device__ __forceinline__ void expand_simple(const UnpackArgs& a, uint64_t A, const uint8_t* d,
+                                              uint64_t* aux, const uint64_t* dep_tab, uint64_t tm,
+                                              uint64_t* wp, uint64_t* rp, uint64_t gen_tag) {
   const int l = lane_id();
   __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): as expand_lean
   aux[l] = tm;
@@ -1875,6 +1880,7 @@ __device__ __forceinline__ void expand_simple(const UnpackArgs& a, const uint8_t
       const uint32_t wlo = __builtin_amdgcn_perm(dhi, dlo, (uint32_t)sel);
       const uint32_t whi = __builtin_amdgcn_perm(dhi, dlo, (uint32_t)(sel >> 32));
       if (act) wp[o] = ((uint64_t)whi << 32) | wlo;
+      if (FLAT && act) rp[o] = (A + p) | gen_tag;
       if (runs) {
         // a run's first word with its record (a raw run's from the staged bytes when they hold
         // it), the rest by the whole wave -- as expand_lean
@@ -1913,10 +1919,17 @@ __device__ __forceinline__ void expand_simple(const UnpackArgs& a, const uint8_t
               dst[k] = ((uint64_t)__builtin_amdgcn_alignbyte(x2, x1, s3) << 32) |
                        __builtin_amdgcn_alignbyte(x1, x0, s3);
             }
+            if (FLAT)
+              for (uint32_t k = (ke > k0 ? ke : k0) + l; k < nj; k += 64) {
+                uint64_t v;
+                __builtin_memcpy(&v, a.packed + A + sj + 8ull * k, 8);
+                dst[k] = v;
+              }
           }
         }
       }
       wp += btot;
+      if (FLAT) rp += btot;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
@@ -1925,6 +1938,7 @@ __device__ __forceinline__ void expand_simple(const UnpackArgs& a, const uint8_t
 // Expansion of a tile's records given its true record-start masks (lane = sub-tile) and excl,
 // the words of the tile's first message before the tile: the lean path when the tile's window
 // allows it, else the general one.
+template <bool FLAT = false>
 __device__ __forceinline__ void expand_records(const UnpackArgs& a, uint64_t A, const uint8_t* d,
                                                uint64_t* aux, const uint64_t* dep_tab, uint64_t tm,
                                                uint64_t excl, MsgWin& win, uint64_t mfirst,
@@ -1932,17 +1946,18 @@ __device__ __forceinline__ void expand_records(const UnpackArgs& a, uint64_t A, 
                                                uint64_t tile_words = ~0ull) {
   const int l = lane_id();
   // a tile in the middle of one accepted message (no start in it; its words and bytes short of
-  // the message's end; the message fits the output).  (Also taking it in flat-packed chunks and in
-  // the stream split's flat decode, there with whole raw runs from global memory, measured slower:
-  // flat decode 9.55 -> 10.8 ms -- that kernel's bound is its look-back, and the path's registers
-  // cost it spills.)
-  if (a.mode == 0 && a.words && a.word_off && !a.rec_pos && tile_words != ~0ull &&
-      ballot(msw != 0) == 0) {
+  // the message's end; the message fits the output); FLAT: the split flat decode's tiles in the
+  // middle of the stream.  (Taken in the one-pass flat decode too it measured slower: 9.55 ->
+  // 10.8 ms -- that kernel's bound was its look-back, and the path's registers cost it spills.)
+  if ((FLAT ? (a.rec_pos != nullptr) : (a.mode == 0 && !a.rec_pos)) && a.words && a.word_off &&
+      tile_words != ~0ull && ballot(msw != 0) == 0) {
     const uint64_t cbase = readlane64(win.base, 0), ctot = readlane64(win.total, 0);
     const uint64_t cend = readlane64(win.end, 0);
     if (readlane32(win.ok, 0) && cbase + ctot <= a.words_capacity && excl + tile_words < ctot &&
         A + (uint64_t)kB + 2050u < cend) {
-      expand_simple(a, d, aux, dep_tab, tm, a.words + cbase + excl);
+      expand_simple<FLAT>(a, A, d, aux, dep_tab, tm, a.words + cbase + excl,
+                          FLAT ? a.rec_pos + cbase + excl : nullptr,
+                          FLAT ? (*a.rec_gen << kRecGenShift) : 0ull);
       return;
     }
   }
@@ -2341,6 +2356,7 @@ unpack_tiles_kernel(UnpackArgs a) {
     }
     if (!has_start) {
       if (l == 0) store_agent(a.desc + t, make_desc(kDescIncl, xE, x0, excl + w));
+      if (PHASE == 2) tile_words = w;
     }
     if (a.stamps && l == 0 && t < 1024) {  // diagnostic dump (CPK_STAMPS=1)
       a.stamps[4 * t] = E | ((uint64_t)Eopt << 32);
@@ -2355,7 +2371,8 @@ unpack_tiles_kernel(UnpackArgs a) {
   if (a.debug_skip & 256) return;  // diagnostic: + the entry and the look-back
   if (PHASE == 0 && a.prio) __builtin_amdgcn_s_setprio(0);
   if (!FLAT && a.mode == 0 && a.words && Ein > kRunSplit) run_tail(a, A, d, Ein, excl, win);
-  expand_records(a, A, d, aux, dep_tab, tm, excl, win, mfirst, mlast, msw, tile_words);
+  expand_records<FLAT && PHASE == 2>(a, A, d, aux, dep_tab, tm, excl, win, mfirst, mlast, msw,
+                                     tile_words);
   // a fused single-tile batch: this wave is the whole call -- its error word for the host, last:
   // its stores done, then a system-scope release
   if (a.err_host) {
