@@ -217,6 +217,7 @@ __device__ WalkEnd walk_messages(const Flat& F, const uint64_t* __restrict__ wor
   const int l = lane_id();
   uint64_t k = 0;
   uint64_t L = 0, prevL = 0;  // the last two message sizes (a stride is tried when they agree)
+  bool exact = false;         // the next message goes through message_at
   WalkEnd r;
   r.stop = kRunOn;
   while (k < kmax && s < wend) {
@@ -254,6 +255,79 @@ __device__ WalkEnd walk_messages(const Flat& F, const uint64_t* __restrict__ wor
       prevL = 0;  // the stretch ended: the next message goes the serial way
       continue;
     }
+    if (!Meet::kActive && !exact) {
+      // ---- up to 64 messages followed on their first words alone, checked together ----
+      // Lane 0 follows the chain through each message's first words only (one dependent load per
+      // message: the sizes of up to 7 segments share the first four words); every lane then
+      // checks one message's reads against the record heads as message_at does, in its order
+      // (first word, table, segments).  A message whose table is longer, ends past the decoded
+      // words or exceeds the limit goes through message_at next (`exact`).
+      __shared__ uint64_t b_s[64], b_x[64];
+      __shared__ uint32_t b_tw[64];
+      uint32_t nb = 0, fall = 0;
+      if (l == 0) {
+        uint64_t cs = s;
+        while (nb < 64 && k + nb < kmax && cs < wend && cs < F.Tc) {
+          const uint64_t w0 = words[cs];
+          const uint32_t nm1 = (uint32_t)w0;
+          const uint64_t tw = (nm1 + 1) / 2 + 1;
+          if (nm1 > 6 || cs + tw > F.Tc) {
+            fall = 1;
+            break;
+          }
+          uint64_t total = w0 >> 32;
+          if (nm1) {
+            const uint32_t* t32 = reinterpret_cast<const uint32_t*>(words + cs);
+            for (uint32_t i = 1; i <= nm1; i++) total += t32[i + 1];
+          }
+          const uint64_t x = cs + tw + total;
+          if (total > limit || x > F.Tc) {
+            fall = 1;
+            break;
+          }
+          b_s[nb] = cs;
+          b_x[nb] = x;
+          b_tw[nb] = (uint32_t)tw | (nm1 ? 0x80000000u : 0u);
+          nb++;
+          cs = x;
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      nb = readlane32(nb, 0);
+      fall = readlane32(fall, 0);
+      if (nb) {
+        const bool act = (uint32_t)l < nb;
+        const uint32_t j = act ? (uint32_t)l : 0u;
+        const uint64_t sj = b_s[j], xj = b_x[j];
+        const uint32_t twj = b_tw[j];
+        int32_t e = F.read_to(sj + 1, F.head(sj + 1));
+        const uint64_t st = sj + (twj & 0x7fffffffu);
+        if (!e && (twj >> 31)) e = F.read_to(st, F.head(st));
+        const uint64_t hxj = F.head(xj);  // (xj <= Tc)
+        if (!e) e = F.read_to(xj, hxj);
+        const uint64_t bad = ballot(act && e != 0);
+        const uint32_t n = bad ? (uint32_t)lowest_bit(bad) : nb;
+        const uint64_t hprev = shfl64(hxj, l > 0 ? l - 1 : 0);
+        const uint64_t hsj = l == 0 ? hs : hprev;
+        if ((uint32_t)l < n) emit(k + (uint64_t)l, sj, hsj);
+        if (bad) {
+          r.stop = (int32_t)readlane32((uint32_t)e, (int)n);
+          k += n;
+          s = readlane64(sj, (int)n);
+          hs = readlane64(hsj, (int)n);
+          break;
+        }
+        const uint64_t single = (twj >> 31) ? 0ull : xj - sj;
+        prevL = nb >= 2 ? readlane64(single, (int)nb - 2) : L;
+        L = readlane64(single, (int)nb - 1);
+        k += nb;
+        s = readlane64(xj, (int)nb - 1);
+        hs = readlane64(hxj, (int)nb - 1);
+      }
+      exact = fall != 0;
+      continue;
+    }
+    exact = false;
     uint64_t x = 0, hx = kNone, single = 0;
     int32_t e = 0;
     if (l == 0) e = message_at(F, words, s, limit, &x, &hx, &single);
