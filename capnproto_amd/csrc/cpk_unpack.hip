@@ -1992,15 +1992,16 @@ __device__ __forceinline__ void expand_records(const UnpackArgs& a, uint64_t A, 
 #endif
 // FLAT: the flat stream decode's second-candidate descriptors and look-back are compiled in (a
 // variant of its own: their registers cost the other variant spills).
-// PHASE (the split message decode, "Split decode" below): 0 one pass; 1 the index launch (stage,
-// chain 0, descriptors and record-start bits; no look-back, no expansion); 2 the expansion launch
-// (chain 0 from the index launch's bits, the tile's prefix from the resolve launch).
+// PHASE: 0 one pass; 1 an index launch (stage, chain 0, descriptors and the base chain's
+// record-start bits; no look-back, no expansion); 2 its second launch (the base chain from the
+// bits).  For message batches ("Split decode" below, the measured alternative CPK_UNPACK_SPLIT=1)
+// the tile's prefix then comes from the resolve launch between the two.  For the flat decode
+// (FLAT, the stream split's default) the index launch publishes every tile's chain-0 exit, AGG
+// and second candidate, and the second launch looks back over descriptors that are all
+// published (lookback_flat_scan<true>: one round trip per window, waits only for INCLs).
 template <bool FLAT, int PHASE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CPK_UNPACK_WPE))) void
 unpack_tiles_kernel(UnpackArgs a) {
-  // (FLAT with PHASE 1 / 2: the split flat decode -- the index launch publishes every tile's
-  // chain-0 exit, AGG and second candidate and leaves; the decode launch re-stages, recomputes
-  // chain 0 and looks back over descriptors that are all published)
   __shared__ __attribute__((aligned(16))) uint8_t lds_data[4][kPre + kB + kPad];
   // per wave 1 KiB: message starts while they are found, then chain 0 and the walked starts
   // while the entry's chain is traced, then the record list of a quarter tile
