@@ -336,3 +336,22 @@ def test_reserve_then_capture_fresh_context():
         assert (ust == 0).all()
     finally:
         c.close()
+
+
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 200, 300])
+def test_single_tile_batches(codec, oracle, n):
+    """Batches of tiny messages within one 2048-word tile: the tile kernel frames the batch
+    itself in the call's single launch (no framing or placement launch).  One message with a bad
+    segment table rides along (writeMessage's framing, serialize.c++:311-357)."""
+    rng = np.random.default_rng(2000 + n)
+    words, off = cases.message_batch(rng, n, max_seg=2, max_words=2, profile="mixed")
+    assert len(words) <= 2048
+    if n >= 2:
+        m = n // 2
+        t32 = words[off[m]:off[m] + 1].view("<u4").copy()
+        t32[1] += 1  # a segment size past the message
+        words[off[m]] = t32.view("<u8")[0]
+    data, moff, st = gpu_pack_messages(codec, words, off.astype(np.int64))
+    ref, roff, rst = oracle.pack_batch(words, off)
+    assert (st == rst).all() and (moff == roff.astype(np.int64)).all()
+    assert data == ref.tobytes()

@@ -349,3 +349,20 @@ def test_raw_runs_across_tiles(codec, oracle):
         head = oracle.pack_chunk(np.frombuffer(np.array([0, nw], "<u4").tobytes(), "<u8"))
         pad = oracle.pack_flat(cases.flat_message(rng, 1, [17 * k], "mixed"))[0]
         check_against_oracle(codec, oracle, [pad, head + bytes(body), after])
+
+
+@pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 200, 256, 257])
+def test_single_tile_batches(codec, oracle, n):
+    """Batches of tiny messages that fit one 4 KiB tile: up to kUnpackFuseMsgs (256) messages the
+    tile kernel reads the headers itself in the call's single launch (one thread per message,
+    the word offsets by one workgroup scan), above that the header launch runs.  One
+    truncated message and one with a UINT_MAX segment count ride along (serialize.c++:214-221)."""
+    rng = np.random.default_rng(1000 + n)
+    msgs = [oracle.pack_flat(cases.flat_message(rng, 1, [int(rng.integers(0, 2))], "mixed"))[0]
+            for _ in range(n)]
+    if n >= 2:
+        msgs[n // 2] = msgs[n // 2][:-1]  # truncated
+    if n >= 64:
+        msgs[n - 2] = bytes([0x0F, 0xFF, 0xFF, 0xFF, 0xFF])  # segment count UINT_MAX + 1
+    assert sum(len(m) for m in msgs) <= 4096
+    check_against_oracle(codec, oracle, msgs)
